@@ -1,0 +1,71 @@
+/* vv_dsp_amd.h -- ADDITIVE batched / device-pointer entry points of the MI355X
+ * backend.  The reference API (fft.h, stft.h, ...) is host-pointer and one
+ * transform per call, which pays PCIe per call; these entry points take
+ * device (HBM) pointers and whole batches and run asynchronously on a HIP
+ * stream passed as void* (NULL = default stream).  Nothing here changes the
+ * reference's C99 ABI. */
+#ifndef VV_DSP_AMD_H
+#define VV_DSP_AMD_H
+#include "vv_dsp/vv_dsp_types.h"
+#include "vv_dsp/spectral/fft.h"
+#include "vv_dsp/spectral/stft.h"
+#include "vv_dsp/spectral/dct.h"
+#include "vv_dsp/filter/fir.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* number of usable HIP devices */
+int vv_dsp_amd_device_count(void);
+const char* vv_dsp_amd_last_error(void);
+
+/* FFT: `batch` contiguous transforms per execute (host or device pointers). */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_fft_make_plan_many(size_t n, vv_dsp_fft_type type, vv_dsp_fft_dir dir,
+                                                         size_t batch, vv_dsp_fft_plan** out_plan);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_fft_execute_device(const vv_dsp_fft_plan* plan, const void* d_in,
+                                                         void* d_out, void* stream);
+
+/* STFT over nch channels (ch_stride floats apart) into [ch][frame][fft_size]
+ * rows (out_ch_stride floats apart): magnitudes (_spectrogram_) or complex
+ * spectra (_spectrum_). */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_spectrogram_device(vv_dsp_stft* h, const vv_dsp_real* d_signal,
+                                                              size_t n, size_t nch, size_t ch_stride,
+                                                              vv_dsp_real* d_out_mag, size_t out_ch_stride,
+                                                              void* stream, size_t* out_frames);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_spectrum_device(vv_dsp_stft* h, const vv_dsp_real* d_signal,
+                                                           size_t n, size_t nch, size_t ch_stride,
+                                                           vv_dsp_cpx* d_out, size_t out_ch_stride,
+                                                           void* stream, size_t* out_frames);
+/* count frames real[count][fft_size] -> cpx[count][fft_size] (vv_dsp_stft_process batched) */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_process_device(vv_dsp_stft* h, const vv_dsp_real* d_frames,
+                                                          size_t count, vv_dsp_cpx* d_spec, void* stream);
+/* count spectra overlap-added at the handle's hop (vv_dsp_stft_reconstruct batched) */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_reconstruct_device(vv_dsp_stft* h, const vv_dsp_cpx* d_spec,
+                                                              size_t count, vv_dsp_real* d_out_add,
+                                                              vv_dsp_real* d_norm_add, void* stream);
+
+/* FIR plan: coefficients resident on the device; overlap-save for fir_apply_fft
+ * semantics, direct form (bit-identical to vv_dsp_fir_apply) on request. */
+typedef struct vv_dsp_fir_plan vv_dsp_fir_plan;
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_fir_plan_create(const vv_dsp_real* coeffs, size_t num_taps,
+                                                      vv_dsp_fir_plan** out);
+vv_dsp_status vv_dsp_fir_plan_destroy(vv_dsp_fir_plan* p);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_fir_apply_fft_device(vv_dsp_fir_plan* p, const vv_dsp_real* d_x,
+                                                           vv_dsp_real* d_y, size_t n, size_t nch,
+                                                           size_t x_stride, size_t y_stride, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_fir_apply_direct_device(vv_dsp_fir_plan* p, const vv_dsp_real* d_x,
+                                                              vv_dsp_real* d_y, size_t n, size_t nch,
+                                                              size_t x_stride, size_t y_stride, void* stream);
+
+/* Hilbert analytic signal of `batch` contiguous real[N] rows -> cpx[batch][N] */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_hilbert_analytic_device(const vv_dsp_real* d_x, size_t N, size_t batch,
+                                                              vv_dsp_cpx* d_z, void* stream);
+/* DCT of `batch` contiguous rows with the plan's type/direction */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_dct_execute_device(const vv_dsp_dct_plan* plan, const vv_dsp_real* d_in,
+                                                         vv_dsp_real* d_out, size_t batch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

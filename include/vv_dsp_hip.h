@@ -1,0 +1,114 @@
+/*
+ * vv_dsp_hip.h -- the thin extern "C" HIP shim of the MI355X (gfx950) backend.
+ *
+ * Plain C ABI: opaque handles, raw pointers, sizes, int status codes with the
+ * values of the reference's vv_dsp_status (include/vv_dsp/vv_dsp_types.h:120-128:
+ * 0 OK, 1 NULL_POINTER, 2 INVALID_SIZE, 3 OUT_OF_RANGE, 4 INTERNAL,
+ * 5 NAN_INF, 6 UNSUPPORTED).  No HIP or torch types appear here: streams are
+ * passed as `void*` (a hipStream_t; NULL = the handle's own stream).
+ *
+ * Two calling conventions per operation:
+ *   *_host   : host pointers, synchronous (what the reference's C API needs);
+ *   *_device : device pointers, asynchronous on the given stream (the batched
+ *              entry points; inputs already resident in HBM).
+ *
+ * The C99 front-end in vv-dsp_amd/csrc/host/ (the reference's vv_dsp_* API) is
+ * the only intended caller of the *_host functions; the *_device functions are
+ * also reachable through include/vv_dsp/vv_dsp_amd.h.
+ *
+ * Reference interfaces each group replaces:
+ *   vvhip_fft_*  : the FFT backend vtable slot, src/spectral/fft_backend.h:32-38
+ *                  (make_plan / execute / free_plan / is_available)
+ *   vvhip_stft_* : src/spectral/stft.c:30-144 (create, process, reconstruct, spectrogram)
+ *   vvhip_fir_*  : src/filter/fir.c:75-196 (apply_fft, apply)
+ *   vvhip_hilbert_*: src/spectral/hilbert.c:14-75
+ *   vvhip_dct_*  : src/spectral/dct.c:86-136
+ */
+#ifndef VV_DSP_HIP_H
+#define VV_DSP_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#pragma GCC visibility push(default)
+
+typedef struct vvhip_fft vvhip_fft;
+typedef struct vvhip_stft vvhip_stft;
+typedef struct vvhip_fir vvhip_fir;
+
+/* Number of usable HIP devices (0 when none: every other call then fails). */
+int vvhip_available(void);
+/* Text of the last error seen by this thread ("" if none). */
+const char* vvhip_last_error(void);
+/* Build identification, e.g. "vvhip gfx950 ROCm 7.2". */
+const char* vvhip_version(void);
+
+/* ---- device memory helpers (tests / host front-end) ---- */
+void* vvhip_malloc(size_t bytes);
+void vvhip_free(void* p);
+int vvhip_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int vvhip_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int vvhip_memset(void* dst, int value, size_t bytes);
+int vvhip_stream_sync(void* stream);
+int vvhip_device_sync(void);
+
+/* ---- FFT: replaces the backend vtable slot (fft_backend.h:32-38) ----
+ * type: 0 C2C, 1 R2C, 2 C2R (fft.h:152-156); dir: +1 forward, -1 backward.
+ * Layout per transform as fft.h:169-172; `batch` transforms back to back. */
+int vvhip_fft_plan_create(size_t n, int type, int dir, size_t batch, vvhip_fft** out);
+int vvhip_fft_exec_host(vvhip_fft* plan, const void* in, void* out);
+int vvhip_fft_exec_device(vvhip_fft* plan, const void* d_in, void* d_out, size_t batch,
+                          void* stream);
+void vvhip_fft_plan_destroy(vvhip_fft* plan);
+
+/* ---- STFT (stft.c) ---- window: nfft floats computed by the caller. */
+int vvhip_stft_create(size_t nfft, size_t hop, const float* window, vvhip_stft** out);
+void vvhip_stft_destroy(vvhip_stft* h);
+/* frames = n < nfft ? 1 : 1 + (n - nfft + hop) / hop   (stft.c:119) */
+size_t vvhip_stft_num_frames(size_t n, size_t nfft, size_t hop);
+int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, float* out_mag);
+/* nch channels at ch_stride floats; magnitudes [ch][frame][nfft] at out_ch_stride floats.
+ * complex_out != 0 writes the full complex spectrum rows (float pairs) instead. */
+int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
+                                  size_t ch_stride, void* d_out, size_t out_ch_stride,
+                                  int complex_out, void* stream);
+int vvhip_stft_process_host(vvhip_stft* h, const float* frame, float* spec_out);
+int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count, float* d_spec,
+                              void* stream);
+int vvhip_stft_reconstruct_host(vvhip_stft* h, const float* spec, float* out_add, float* norm_add);
+/* count frames (cpx[count][nfft]) overlap-added at `hop` into out_add/norm_add
+ * (length (count-1)*hop + nfft); norm_add may be NULL. */
+int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t count, size_t hop,
+                                  float* d_out_add, float* d_norm_add, void* stream);
+
+/* ---- FIR (fir.c) ---- */
+int vvhip_fir_create(const float* h, size_t taps, vvhip_fir** out);
+void vvhip_fir_destroy(vvhip_fir* f);
+/* mode 0: FFT overlap-save (fir_apply_fft semantics), mode 1: direct form,
+ * same summation order as fir.c:170-186 (bit-identical to vv_dsp_fir_apply).
+ * prefix: taps-1 samples preceding x[0] in time order (oldest first), or NULL
+ * for zero initial state. */
+int vvhip_fir_apply_host(vvhip_fir* f, const float* x, float* y, size_t n, const float* prefix,
+                         int mode);
+int vvhip_fir_apply_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n, size_t nch,
+                           size_t x_stride, size_t y_stride, const float* d_prefix, int mode,
+                           void* stream);
+/* Block length (real FFT size) the overlap-save path uses for a signal of n samples. */
+size_t vvhip_fir_block_size(vvhip_fir* f, size_t n);
+
+/* ---- Hilbert analytic signal (hilbert.c:14-75) ---- */
+int vvhip_hilbert_host(const float* x, size_t n, float* z_out);
+int vvhip_hilbert_device(const float* d_x, size_t n, size_t batch, float* d_z, void* stream);
+
+/* ---- DCT (dct.c:86-136); nan_policy as core/nan_policy.h (0..3) ---- */
+int vvhip_dct_host(const float* in, float* out, size_t n, int type, int dir, int nan_policy);
+int vvhip_dct_device(const float* d_in, float* d_out, size_t n, size_t batch, int type, int dir,
+                     int nan_policy, void* stream);
+
+#pragma GCC visibility pop
+#ifdef __cplusplus
+}
+#endif
+#endif

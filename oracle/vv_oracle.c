@@ -1,0 +1,380 @@
+/*
+ * vv_oracle.c -- CPU restatement of the vv-dsp reference spectral hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see vv_oracle.h).  Never linked into the product.
+ * Each routine follows the floating-point operation order of the cited
+ * reference function so the results are bit-identical when built with the
+ * reference's flags; tests/test_oracle.py checks exactly that.
+ */
+#include "vv_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_PI_D 3.141592653589793238462643383279502884
+/* vv_dsp_math.h: VV_DSP_PI = (float)PI_D; VV_DSP_TWO_PI = (float)(2.0 * PI_D) */
+static const float kPi = (float)ORC_PI_D;
+static const float kTwoPi = (float)(2.0 * ORC_PI_D);
+
+typedef struct { float re, im; } ocpx;
+
+static int pow2(size_t n) { return n != 0 && (n & (n - 1)) == 0; }
+
+/* In-place bit-reversal permutation (any method gives the same permutation). */
+static void bitrev_permute(ocpx* a, size_t n) {
+    size_t j = 0;
+    for (size_t i = 0; i + 1 < n; ++i) {
+        if (i < j) { ocpx t = a[i]; a[i] = a[j]; a[j] = t; }
+        size_t m = n >> 1;
+        while (m >= 1 && (j & m)) { j ^= m; m >>= 1; }
+        j |= m;
+    }
+}
+
+/* fft_kiss.c:27-74 -- radix-2 DIT; per-stage twiddle by complex recurrence. */
+static void radix2_inplace(ocpx* a, size_t n, int sign) {
+    bitrev_permute(a, n);
+    for (size_t span = 2; span <= n; span <<= 1) {
+        const float theta = (float)(-sign) * 2.0f * kPi / (float)span;
+        const float step_re = cosf(theta);
+        const float step_im = sinf(theta);
+        const size_t half = span >> 1;
+        for (size_t base = 0; base < n; base += span) {
+            float w_re = 1.0f, w_im = 0.0f;
+            ocpx* lo = a + base;
+            ocpx* hi = a + base + half;
+            for (size_t k = 0; k < half; ++k) {
+                const float t_re = w_re * hi[k].re - w_im * hi[k].im;
+                const float t_im = w_re * hi[k].im + w_im * hi[k].re;
+                hi[k].re = lo[k].re - t_re;
+                hi[k].im = lo[k].im - t_im;
+                lo[k].re += t_re;
+                lo[k].im += t_im;
+                const float nr = w_re * step_re - w_im * step_im;
+                const float ni = w_re * step_im + w_im * step_re;
+                w_re = nr;
+                w_im = ni;
+            }
+        }
+    }
+    if (sign < 0) {
+        const float s = 1.0f / (float)n;
+        for (size_t i = 0; i < n; ++i) { a[i].re *= s; a[i].im *= s; }
+    }
+}
+
+/* fft_kiss.c:76-92 -- O(n^2) DFT with per-term cosf/sinf. */
+static void naive_dft(const ocpx* x, ocpx* y, size_t n, int sign) {
+    const float scale = (sign < 0) ? (1.0f / (float)n) : 1.0f;
+    for (size_t k = 0; k < n; ++k) {
+        float acc_re = 0, acc_im = 0;
+        for (size_t t = 0; t < n; ++t) {
+            const float ang = (float)(-sign) * 2.0f * kPi * (float)(k * t) / (float)n;
+            const float c = cosf(ang), s = sinf(ang);
+            acc_re += x[t].re * c - x[t].im * s;
+            acc_im += x[t].re * s + x[t].im * c;
+        }
+        y[k].re = acc_re * scale;
+        y[k].im = acc_im * scale;
+    }
+}
+
+int orc_fft_c2c(const float* in, float* out, size_t n, int dir) {
+    if (!in || !out || n == 0) return 1;
+    const int sign = (dir >= 0) ? +1 : -1;
+    if (pow2(n)) {
+        if (out != in) memcpy(out, in, sizeof(ocpx) * n);
+        radix2_inplace((ocpx*)out, n, sign);
+    } else {
+        naive_dft((const ocpx*)in, (ocpx*)out, n, sign);
+    }
+    return 0;
+}
+
+int orc_fft_r2c(const float* in, float* out, size_t n) {
+    if (!in || !out || n == 0) return 1;
+    ocpx* buf = (ocpx*)malloc(sizeof(ocpx) * n);
+    ocpx* spec = (ocpx*)malloc(sizeof(ocpx) * n);
+    if (!buf || !spec) { free(buf); free(spec); return 4; }
+    for (size_t i = 0; i < n; ++i) { buf[i].re = in[i]; buf[i].im = 0.0f; }
+    if (pow2(n)) {
+        memcpy(spec, buf, sizeof(ocpx) * n);
+        radix2_inplace(spec, n, +1);
+    } else {
+        naive_dft(buf, spec, n, +1);
+    }
+    const size_t nh = n / 2 + 1;
+    memcpy(out, spec, sizeof(ocpx) * nh);
+    if ((n & 1) == 0 && nh > 1) out[2 * (nh - 1) + 1] = 0.0f;  /* Nyquist imag forced 0 */
+    free(buf);
+    free(spec);
+    return 0;
+}
+
+int orc_fft_c2r(const float* in, float* out, size_t n) {
+    if (!in || !out || n == 0) return 1;
+    const size_t nh = n / 2 + 1;
+    const ocpx* half = (const ocpx*)in;
+    ocpx* full = (ocpx*)malloc(sizeof(ocpx) * n);
+    ocpx* tim = (ocpx*)malloc(sizeof(ocpx) * n);
+    if (!full || !tim) { free(full); free(tim); return 4; }
+    for (size_t k = 0; k < n; ++k) {
+        if (k < nh) {
+            full[k] = half[k];
+        } else {
+            const size_t m = n - k;
+            if (m > 0 && m < nh) { full[k].re = half[m].re; full[k].im = -half[m].im; }
+            else { full[k].re = 0.0f; full[k].im = 0.0f; }
+        }
+    }
+    naive_dft(full, tim, n, -1);   /* the reference always takes the O(n^2) path here */
+    for (size_t i = 0; i < n; ++i) out[i] = tim[i].re;
+    free(full);
+    free(tim);
+    return 0;
+}
+
+/* window.c:16-49 (boxcar / hann / hamming, symmetric, N==1 -> 1) */
+int orc_window(int kind, size_t n, float* out) {
+    if (!out || n == 0) return 1;
+    if (kind == 0) { for (size_t i = 0; i < n; ++i) out[i] = 1.0f; return 0; }
+    if (kind != 1 && kind != 2) return 3;
+    if (n == 1) { out[0] = 1.0f; return 0; }
+    const float a = (kind == 1) ? 0.5f : 0.54f;
+    const float b = (kind == 1) ? 0.5f : 0.46f;
+    const float step = kTwoPi / (float)(n - 1);
+    for (size_t i = 0; i < n; ++i) {
+        const float c = cosf(step * (float)i);
+        out[i] = a - b * c;
+    }
+    return 0;
+}
+
+/* stft.c:74-92 -- window (vectorized_math_fallback.c:13-29) then C2C forward. */
+int orc_stft_process(const float* win, size_t nfft, const float* frame, float* spec_out) {
+    if (!win || !frame || !spec_out || nfft == 0) return 1;
+    float* cin = (float*)malloc(sizeof(float) * 2 * nfft);
+    if (!cin) return 4;
+    for (size_t i = 0; i < nfft; ++i) { cin[2 * i] = frame[i] * win[i]; cin[2 * i + 1] = 0.0f; }
+    int rc = orc_fft_c2c(cin, spec_out, nfft, +1);
+    free(cin);
+    return rc;
+}
+
+size_t orc_stft_num_frames(size_t n, size_t nfft, size_t hop) {
+    return (n < nfft) ? 1 : (1 + (n - nfft + hop) / hop);
+}
+
+/* stft.c:112-144 */
+int orc_stft_spectrogram(const float* win, size_t nfft, size_t hop,
+                         const float* signal, size_t n, float* out_mag, size_t* frames) {
+    if (!win || !signal || !out_mag || !frames) return 1;
+    if (nfft == 0 || hop == 0) return 2;
+    const size_t nf = orc_stft_num_frames(n, nfft, hop);
+    *frames = nf;
+    float* frame = (float*)malloc(sizeof(float) * nfft);
+    float* spec = (float*)malloc(sizeof(float) * 2 * nfft);
+    if (!frame || !spec) { free(frame); free(spec); return 4; }
+    for (size_t f = 0; f < nf; ++f) {
+        const size_t s0 = f * hop;
+        for (size_t i = 0; i < nfft; ++i) frame[i] = (s0 + i < n) ? signal[s0 + i] : 0.0f;
+        orc_stft_process(win, nfft, frame, spec);
+        float* row = out_mag + f * nfft;
+        for (size_t k = 0; k < nfft; ++k) {
+            const float re = spec[2 * k], im = spec[2 * k + 1];
+            row[k] = sqrtf(re * re + im * im);
+        }
+    }
+    free(frame);
+    free(spec);
+    return 0;
+}
+
+/* stft.c:95-110 -- inverse C2C (1/n) then out_add += re*w, norm_add += w*w */
+int orc_stft_reconstruct(const float* win, size_t nfft, const float* spec,
+                         float* out_add, float* norm_add) {
+    if (!win || !spec || !out_add) return 1;
+    float* t = (float*)malloc(sizeof(float) * 2 * nfft);
+    if (!t) return 4;
+    orc_fft_c2c(spec, t, nfft, -1);
+    for (size_t i = 0; i < nfft; ++i) {
+        const float w = win[i];
+        out_add[i] += t[2 * i] * w;
+        if (norm_add) norm_add[i] += w * w;
+    }
+    free(t);
+    return 0;
+}
+
+/* hilbert.c:14-75 -- R2C, Hermitian expand, one-sided mask, inverse C2C. */
+int orc_hilbert_analytic(const float* x, size_t n, float* z_out) {
+    if (!x || !z_out) return 1;
+    if (n == 0) return 2;
+    const size_t nh = n / 2 + 1;
+    float* half = (float*)malloc(sizeof(float) * 2 * nh);
+    float* zs = (float*)calloc(2 * n, sizeof(float));
+    if (!half || !zs) { free(half); free(zs); return 4; }
+    orc_fft_r2c(x, half, n);
+    /* Z[k]: DC (and N/2 for even N) pass, positive bins doubled, negatives zero.
+     * The mirrored Xfull entries only feed bins the mask zeroes. */
+    zs[0] = half[0];
+    zs[1] = half[1];
+    const size_t kpos_end = (n % 2 == 0) ? n / 2 : nh;
+    for (size_t k = 1; k < kpos_end; ++k) {
+        zs[2 * k] = 2.0f * half[2 * k];
+        zs[2 * k + 1] = 2.0f * half[2 * k + 1];
+    }
+    if (n % 2 == 0) { zs[n] = half[n]; zs[n + 1] = half[n + 1]; }
+    orc_fft_c2c(zs, z_out, n, -1);
+    free(half);
+    free(zs);
+    return 0;
+}
+
+/* dct.c:21-68 naive kernels; :86-136 dispatch (NaN policy PROPAGATE = identity) */
+int orc_dct(const float* in, float* out, size_t n, int type, int dir) {
+    if (!in || !out) return 1;
+    if (n == 0) return 2;
+    const float N = (float)n;
+    if ((type == 2 && dir > 0)) {
+        for (size_t k = 0; k < n; ++k) {
+            float acc = 0;
+            for (size_t i = 0; i < n; ++i) {
+                const float ang = kPi * ((float)i + 0.5f) * (float)k / N;
+                acc += in[i] * cosf(ang);
+            }
+            out[k] = acc;
+        }
+    } else if ((type == 2 || type == 3) && dir < 0) {
+        const float scale = 2.0f / N;
+        for (size_t i = 0; i < n; ++i) {
+            float acc = 0.5f * in[0];
+            for (size_t k = 1; k < n; ++k) {
+                const float ang = kPi * (float)k * ((float)i + 0.5f) / N;
+                acc += in[k] * cosf(ang);
+            }
+            out[i] = scale * acc;
+        }
+    } else if (type == 3 && dir > 0) {
+        for (size_t k = 0; k < n; ++k) {
+            float acc = in[0];
+            for (size_t i = 1; i < n; ++i) {
+                const float ang = kPi * (float)k * ((float)i + 0.5f) / N;
+                acc += 2.0f * in[i] * cosf(ang);
+            }
+            out[k] = acc;
+        }
+    } else if (type == 4) {
+        for (size_t k = 0; k < n; ++k) {
+            float acc = 0;
+            for (size_t i = 0; i < n; ++i) {
+                const float ang = kPi * ((float)i + 0.5f) * ((float)k + 0.5f) / N;
+                acc += in[i] * cosf(ang);
+            }
+            if (dir < 0) acc *= 2.0f / N;
+            out[k] = acc;
+        }
+    } else {
+        return 3;
+    }
+    return 0;
+}
+
+/* fir.c:8-15 */
+static float sinc_f(float v) {
+    if (v == 0.0f) return 1.0f;
+    return (float)(sinf(kPi * v) / (kPi * v));
+}
+
+/* fir.c:17-45 */
+static int fir_window(float* w, size_t n, int kind) {
+    const float den = (float)(n - 1);
+    for (size_t i = 0; i < n; ++i) {
+        switch (kind) {
+        case 0: w[i] = 1.0f; break;
+        case 1: w[i] = (float)(0.54f - 0.46f * cosf(kTwoPi * (float)i / den)); break;
+        case 2: w[i] = (float)(0.5f - 0.5f * cosf(kTwoPi * (float)i / den)); break;
+        case 3: {
+            const double d1 = (float)cosf((float)((2.0 * ORC_PI_D) * (double)i / (double)(n - 1)));
+            const double d2 = (float)cosf((float)(2.0 * (2.0 * ORC_PI_D) * (double)i / (double)(n - 1)));
+            w[i] = (float)(0.42 - 0.5 * d1 + 0.08 * d2);
+            break;
+        }
+        default: return 4;
+        }
+    }
+    return 0;
+}
+
+/* fir.c:47-73 */
+int orc_fir_design_lowpass(float* h, size_t taps, float fc, int wkind) {
+    if (!h) return 1;
+    if (taps == 0) return 2;
+    if (!(fc > 0.0f && fc < 1.0f)) return 3;
+    const float centre = (float)(taps - 1) / 2.0f;
+    for (size_t i = 0; i < taps; ++i) {
+        const float m = (float)i - centre;
+        h[i] = 2 * fc * sinc_f(2 * fc * m);
+    }
+    float* w = (float*)malloc(sizeof(float) * taps);
+    if (!w) return 4;
+    int rc = fir_window(w, taps, wkind);
+    if (rc) { free(w); return rc; }
+    for (size_t i = 0; i < taps; ++i) h[i] *= w[i];
+    free(w);
+    return 0;
+}
+
+/* fir.c:160-196 */
+int orc_fir_apply(const float* h, size_t taps, float* history, size_t* hist_idx,
+                  const float* x, float* y, size_t n) {
+    if (!h || !x || !y || !hist_idx) return 1;
+    if (taps == 0) return 2;
+    const size_t hs = taps - 1;
+    for (size_t i = 0; i < n; ++i) {
+        float acc = 0;
+        acc += h[0] * x[i];
+        if (hs) {
+            size_t r = (*hist_idx == 0) ? hs - 1 : *hist_idx - 1;
+            for (size_t t = 1; t < taps; ++t) {
+                acc += h[t] * history[r];
+                r = (r == 0) ? hs - 1 : r - 1;
+            }
+        }
+        y[i] = acc;
+        if (hs) {
+            history[*hist_idx] = x[i];
+            *hist_idx = (*hist_idx + 1) % hs;
+        }
+    }
+    return 0;
+}
+
+/* fir.c:75-135 */
+int orc_fir_apply_fft(const float* h, size_t taps, const float* x, float* y, size_t n) {
+    if (!h || !x || !y) return 1;
+    if (taps == 0) return 2;
+    size_t nfft = 1;
+    while (nfft < n + taps - 1) nfft <<= 1;
+    const size_t nc = nfft / 2 + 1;
+    float* xb = (float*)calloc(nfft, sizeof(float));
+    float* hb = (float*)calloc(nfft, sizeof(float));
+    float* X = (float*)calloc(2 * nc, sizeof(float));
+    float* H = (float*)calloc(2 * nc, sizeof(float));
+    float* Y = (float*)calloc(2 * nc, sizeof(float));
+    if (!xb || !hb || !X || !H || !Y) { free(xb); free(hb); free(X); free(H); free(Y); return 4; }
+    memcpy(xb, x, n * sizeof(float));
+    memcpy(hb, h, taps * sizeof(float));
+    orc_fft_r2c(xb, X, nfft);
+    orc_fft_r2c(hb, H, nfft);
+    for (size_t k = 0; k < nc; ++k) {   /* vectorized_math_fallback.c:31-53 */
+        const float ar = X[2 * k], ai = X[2 * k + 1], br = H[2 * k], bi = H[2 * k + 1];
+        Y[2 * k] = ar * br - ai * bi;
+        Y[2 * k + 1] = ar * bi + ai * br;
+    }
+    orc_fft_c2r(Y, xb, nfft);
+    for (size_t i = 0; i < n; ++i) y[i] = xb[i];
+    free(xb); free(hb); free(X); free(H); free(Y);
+    return 0;
+}

@@ -1,0 +1,58 @@
+/*
+ * vv_oracle.h -- CPU restatement of the vv-dsp reference's spectral hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in vv-dsp_amd/ links, loads or calls this.
+ * It is the parity checker used by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py.  Every function restates the arithmetic of one
+ * reference function (file:line given beside it, paths under /root/reference)
+ * in the same floating-point operation order, so that, compiled with the same
+ * flags as the reference (-O3 -std=gnu99, no FMA contraction), its outputs are
+ * bit-identical to the reference's.  tests/test_oracle.py pins that against
+ * oracle/_ref/libvvref.so (the reference's own sources, compiled by
+ * oracle/Makefile) and against the committed golden vectors in tests/golden/.
+ *
+ * Layout conventions are the reference's: complex = interleaved {re, im} f32.
+ */
+#ifndef VV_ORACLE_H
+#define VV_ORACLE_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* FFT (src/spectral/fft_kiss.c).  dir = +1 forward (unscaled), -1 backward (x 1/n). */
+int orc_fft_c2c(const float* in, float* out, size_t n, int dir);          /* :101-118 */
+int orc_fft_r2c(const float* in, float* out, size_t n);                   /* :120-147 */
+int orc_fft_c2r(const float* in, float* out, size_t n);                   /* :149-174 */
+
+/* Windows (src/window/window.c). kind: 0 boxcar, 1 hann, 2 hamming (stft.h enum). */
+int orc_window(int kind, size_t n, float* out);                           /* :16-49 */
+
+/* STFT (src/spectral/stft.c) */
+int orc_stft_process(const float* win, size_t nfft, const float* frame, float* spec_out); /* :74-92 */
+size_t orc_stft_num_frames(size_t n, size_t nfft, size_t hop);            /* :119 */
+int orc_stft_spectrogram(const float* win, size_t nfft, size_t hop,
+                         const float* signal, size_t n, float* out_mag, size_t* frames); /* :112-144 */
+int orc_stft_reconstruct(const float* win, size_t nfft, const float* spec,
+                         float* out_add, float* norm_add);                /* :95-110 */
+
+/* Hilbert analytic signal (src/spectral/hilbert.c:14-75) */
+int orc_hilbert_analytic(const float* x, size_t n, float* z_out);
+
+/* DCT (src/spectral/dct.c). type 2/3/4, dir +1/-1 (NaN policy: PROPAGATE). */
+int orc_dct(const float* in, float* out, size_t n, int type, int dir);    /* :86-136 */
+
+/* FIR (src/filter/fir.c). wkind: 0 rect, 1 hamming, 2 hanning, 3 blackman (filter/common.h). */
+int orc_fir_design_lowpass(float* h, size_t taps, float fc, int wkind);   /* :47-73 */
+/* Direct form with a ring-buffer history of taps-1 samples (:160-196).
+ * history/hist_idx are the caller's state (zeroed history + idx 0 = fresh state). */
+int orc_fir_apply(const float* h, size_t taps, float* history, size_t* hist_idx,
+                  const float* x, float* y, size_t n);
+/* Single-block FFT convolution exactly as :75-135 (its C2R is O(Nfft^2): small n only). */
+int orc_fir_apply_fft(const float* h, size_t taps, const float* x, float* y, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

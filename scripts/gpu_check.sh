@@ -1,0 +1,10 @@
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x --timeout=600 > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
+if [ $rc -le 1 ]; then
+  timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench1.log 2>&1
+  echo "bench rc=$?" >> gpurun_out/bench1.log
+fi
+tail -5 gpurun_out/gpu_tests.log; tail -3 gpurun_out/bench1.log

@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks for iteration on the GPU box (not the driver bench).
+
+Times each hot kernel with HIP events on the launch stream, interleaving
+repetitions of all cases in one process (methodology rule 24), and prints
+algorithmic GB/s and the fraction of the 8 TB/s HBM peak.
+
+    python scripts/kbench.py [--reps 20] [--cases c2c1024,stft,fir,...]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "vv-dsp_amd"))
+import vvdsp_amd as vv  # noqa: E402
+
+PEAK = 8000.0
+
+
+def case_c2c(n, batch, fwd=True):
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.complex(torch.rand(batch, n, device="cuda", generator=g) - 0.5,
+                      torch.rand(batch, n, device="cuda", generator=g) - 0.5)
+    y = torch.empty_like(x)
+    p = vv.FftPlan(n, vv.C2C, vv.FWD if fwd else vv.BWD, batch=batch)
+    return (lambda: p(x, out=y)), 2 * batch * n * 8, (x, y, p)
+
+
+def case_r2c(n, batch):
+    x = torch.rand(batch, n, device="cuda")
+    y = torch.empty(batch, n // 2 + 1, dtype=torch.complex64, device="cuda")
+    p = vv.FftPlan(n, vv.R2C, vv.FWD, batch=batch)
+    return (lambda: p(x, out=y)), batch * n * 4 + batch * (n // 2 + 1) * 8, (x, y, p)
+
+
+def case_c2r(n, batch):
+    X = torch.complex(torch.rand(batch, n // 2 + 1, device="cuda"), torch.rand(batch, n // 2 + 1, device="cuda"))
+    y = torch.empty(batch, n, device="cuda")
+    p = vv.FftPlan(n, vv.C2R, vv.BWD, batch=batch)
+    return (lambda: p(X, out=y)), batch * n * 4 + batch * (n // 2 + 1) * 8, (X, y, p)
+
+
+def case_stft(nch, seconds, complex_out=False):
+    n = seconds * 48000
+    sig = torch.rand(nch, n, device="cuda") * 2 - 1
+    st = vv.Stft(1024, 256)
+    fr = st.frames(n)
+    out = torch.empty(nch, fr, 1024, dtype=torch.complex64 if complex_out else torch.float32, device="cuda")
+    byts = nch * n * 4 + nch * fr * 1024 * (8 if complex_out else 4)
+    return (lambda: st.spectrogram(sig, out=out, complex_out=complex_out)), byts, (sig, out, st)
+
+
+def case_fir(nch, n, taps=257):
+    h = torch.hann_window(taps, periodic=False) * 0.01
+    x = torch.rand(nch, n, device="cuda") * 2 - 1
+    y = torch.empty_like(x)
+    p = vv.FirPlan(h)
+    return (lambda: p(x, out=y)), 2 * nch * n * 4, (x, y, p)
+
+
+def case_copy(nbytes):
+    a = torch.empty(nbytes // 4, device="cuda")
+    b = torch.empty_like(a)
+    return (lambda: b.copy_(a)), 2 * nbytes, (a, b)
+
+
+CASES = {
+    "copy1G": lambda: case_copy(1 << 29),
+    "c2c1024": lambda: case_c2c(1024, 65536),
+    "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),
+    "c2c4096": lambda: case_c2c(4096, 16384),
+    "c2c256": lambda: case_c2c(256, 262144),
+    "r2c1024": lambda: case_r2c(1024, 131072),
+    "c2r1024": lambda: case_c2r(1024, 131072),
+    "stft": lambda: case_stft(32, 600),
+    "stft60": lambda: case_stft(1, 60),
+    "stftc": lambda: case_stft(8, 600, complex_out=True),
+    "fir": lambda: case_fir(8, 1 << 24),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--cases", default=",".join(CASES))
+    a = ap.parse_args()
+    names = a.cases.split(",")
+    built = {k: CASES[k]() for k in names}
+    res = {k: [] for k in names}
+    s = torch.cuda.current_stream()
+    for _ in range(a.rounds):
+        for k in names:
+            fn, byts, _keep = built[k]
+            for _ in range(3):
+                fn()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+            for e0, e1 in ev:
+                e0.record(s)
+                fn()
+                e1.record(s)
+            torch.cuda.synchronize()
+            res[k] += [e0.elapsed_time(e1) for e0, e1 in ev]
+    for k in names:
+        byts = built[k][1]
+        ms = np.array(res[k])
+        gbs = byts / (np.median(ms) * 1e-3) / 1e9
+        print(json.dumps({"case": k, "ms_median": round(float(np.median(ms)), 4),
+                          "ms_min": round(float(ms.min()), 4), "GBs": round(gbs, 1),
+                          "frac": round(gbs / PEAK, 4), "bytes": byts}))
+
+
+if __name__ == "__main__":
+    main()

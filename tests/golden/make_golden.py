@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors in tests/golden/*.npz.
+
+Inputs follow the reference harness conventions (python/test_fft.py:41-54,
+python/test_filters.py:36-44 of the reference) and SURVEY.md section 8c row 6.
+Each file holds: the f32 input(s), `kiss` = the reference's own output
+(oracle/_ref/libvvref.so, i.e. the reference sources compiled by
+oracle/Makefile), and `np64` = NumPy/SciPy float64 on the same f32 inputs.
+
+Run in the build container (needs oracle/_ref, i.e. /root/reference):
+    make -C oracle && python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import scipy.fft
+import scipy.signal
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+from vvapi import VvDsp, C2C, R2C, C2R, FWD, BWD, FIRWIN_HANNING  # noqa: E402
+
+REF = os.path.join(HERE, "..", "..", "oracle", "_ref", "libvvref.so")
+
+
+def save(name, manifest, desc, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    manifest[name] = {"desc": desc, "arrays": {k: [str(v.dtype), list(v.shape)]
+                                               for k, v in arrays.items()}}
+
+
+def main():
+    ref = VvDsp(REF)
+    man = {}
+
+    # 1. python/test_fft.py exactly: default_rng(0), C2C, then R2C, then C2R.
+    for n in (16, 1024):
+        rng = np.random.default_rng(0)
+        x = rng.random(n) + 1j * rng.random(n)
+        x32 = x.astype(np.complex64)
+        xr = rng.random(n).astype(np.float32)
+        X = np.fft.rfft(xr.astype(np.float64))
+        X32 = X.astype(np.complex64)
+        save(f"fft_testpy_n{n}", man, "python/test_fft.py inputs (seed 0): c2c fwd+bwd, r2c, c2r",
+             x=x32, c2c_fwd_kiss=ref.fft(x32, C2C, FWD), c2c_fwd_np64=np.fft.fft(x32.astype(np.complex128)),
+             c2c_bwd_kiss=ref.fft(x32, C2C, BWD), c2c_bwd_np64=np.fft.ifft(x32.astype(np.complex128)),
+             xr=xr, r2c_kiss=ref.fft(xr, R2C), r2c_np64=np.fft.rfft(xr.astype(np.float64)),
+             X=X32, c2r_kiss=ref.fft(X32, C2R, BWD, n=n),
+             c2r_np64=np.fft.irfft(X32.astype(np.complex128), n=n))
+
+    # 2. batched c2c 64 x 1024, uniform [-0.5, 0.5), seed 1
+    rng = np.random.default_rng(1)
+    xb = (rng.uniform(-0.5, 0.5, (64, 1024)) + 1j * rng.uniform(-0.5, 0.5, (64, 1024))).astype(np.complex64)
+    kiss = np.stack([ref.fft(r, C2C, FWD) for r in xb])
+    save("fft_batch64_n1024", man, "batched c2c forward 64x1024 uniform[-0.5,0.5) seed 1",
+         x=xb, kiss=kiss, np64=np.fft.fft(xb.astype(np.complex128), axis=1))
+
+    # 3. STFT spectrogram: 48000 samples uniform[-1,1) seed 3, nfft 1024 hop 256 Hann
+    rng = np.random.default_rng(3)
+    sig = rng.uniform(-1, 1, 48000).astype(np.float32)
+    mag = ref.spectrogram(sig, 1024, 256)
+    win = ref.hann(1024)
+    nfr = mag.shape[0]
+    pad = np.concatenate([sig.astype(np.float64), np.zeros(1024, np.float64)])
+    fr = np.stack([pad[f * 256:f * 256 + 1024] for f in range(nfr)])
+    np_mag = np.abs(np.fft.fft(fr * win.astype(np.float64), axis=1))
+    save("stft_48000_n1024_h256", man, "stft spectrogram 48000 samples uniform[-1,1) seed 3, 1024/256 Hann",
+         x=sig, window=win, kiss=mag.astype(np.float32), np64=np_mag)
+
+    # 4. Hilbert N = 1024 and odd N = 255 (standard normal, seed 5)
+    rng = np.random.default_rng(5)
+    for n in (1024, 255):
+        x = rng.standard_normal(n).astype(np.float32)
+        save(f"hilbert_n{n}", man, f"hilbert analytic N={n} standard normal seed 5",
+             x=x, kiss=ref.hilbert(x), np64=scipy.signal.hilbert(x.astype(np.float64)))
+
+    # 5. DCT-II N in {64, 1024} (+ its inverse), standard normal seed 6
+    rng = np.random.default_rng(6)
+    for n in (64, 1024):
+        x = rng.standard_normal(n).astype(np.float32)
+        y = ref.dct(x, 2, False)
+        save(f"dct2_n{n}", man, f"DCT-II forward/inverse N={n} standard normal seed 6",
+             x=x, kiss=y, np64=scipy.fft.dct(x.astype(np.float64), type=2) / 2.0,
+             inv_kiss=ref.dct(y, 2, True),
+             inv_np64=scipy.fft.idct(2.0 * y.astype(np.float64), type=2))
+
+    # 6. FIR: 257 taps Hann fc 0.25 on 16384 samples standard normal seed 1
+    rng = np.random.default_rng(1)
+    h = ref.fir_design_lowpass(257, 0.25, FIRWIN_HANNING)
+    x = rng.standard_normal(16384).astype(np.float32)
+    save("fir_257_n16384", man, "FIR 257-tap Hann fc=0.25, 16384 samples N(0,1) seed 1; "
+         "kiss = vv_dsp_fir_apply (direct, fresh state)",
+         h=h, x=x, kiss=ref.fir_apply(h, x), np64=scipy.signal.lfilter(h.astype(np.float64), [1.0],
+                                                                        x.astype(np.float64)))
+    # 6b. the reference's fir_apply_fft itself on a small block (its C2R is O(n^2))
+    xs = x[:1500].copy()
+    save("firfft_257_n1500", man, "vv_dsp_fir_apply_fft (single block) 257 taps on 1500 samples",
+         h=h, x=xs, kiss=ref.fir_apply(h, xs, fft=True),
+         np64=scipy.signal.lfilter(h.astype(np.float64), [1.0], xs.astype(np.float64)))
+
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(man, f, indent=1, sort_keys=True)
+    print("wrote", len(man), "golden sets")
+
+
+if __name__ == "__main__":
+    main()

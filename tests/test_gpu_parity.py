@@ -1,0 +1,333 @@
+"""GPU parity tests (MI355X): the HIP backend through the C ABI vs the oracle.
+
+Tolerances are the reference harness's own (python/test_fft.py:37-38,62:
+rtol = atol = 5e-5, overridable with VV_PY_RTOL / VV_PY_ATOL), applied against
+NumPy float64 on the same f32 inputs (the arbiter: the reference's Kiss itself
+fails them at n >= 4096), plus a secondary check against the
+oracle (Kiss restatement) within 2x that bound for n <= 1024, and the
+reference's own known-answer tests restated.
+"""
+import numpy as np
+import pytest
+
+from conftest import tolerances
+from vvapi import C2C, R2C, C2R, FWD, BWD, KISS, HIP, OK, ERR_UNSUPPORTED, FirState
+
+pytestmark = pytest.mark.gpu
+
+POW2 = [2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096]
+NONPOW2 = [3, 5, 6, 7, 9, 10, 12, 15, 20, 24, 30, 48, 100, 200]   # gtest/test_fft.cpp:300-316
+
+
+def close(y, ref, rtol=None, atol=None, factor=1.0):
+    r, a = tolerances()
+    r = (rtol if rtol is not None else r) * factor
+    a = (atol if atol is not None else a) * factor
+    np.testing.assert_allclose(y, ref, rtol=r, atol=a)
+
+
+def kiss_check(y, kiss, f64, n):
+    """Secondary check against the Kiss restatement: within 2x the
+    harness bound for power-of-two n <= 1024 (its radix-2 path).  For other n the
+    reference runs an f32 O(n^2) DFT whose own error exceeds that bound, so there we
+    require ours to be at least as close to f64 as Kiss is (elementwise, + tolerance)."""
+    r, a = tolerances()
+    if n & (n - 1) == 0:
+        if n <= 1024:
+            close(y, kiss, factor=2.0)
+        return
+    assert np.all(np.abs(y - f64) <= np.abs(kiss - f64) + a + r * np.abs(f64))
+
+
+# ---------------------------------------------------------------- FFT
+def test_backend_is_hip(amd):
+    L = amd.lib
+    assert L.vv_dsp_fft_is_backend_available(HIP) == 1
+    assert L.vv_dsp_fft_get_backend() == HIP
+    assert L.vv_dsp_fft_is_backend_available(KISS) == 0   # no CPU backend inside the product
+
+
+@pytest.mark.parametrize("n", POW2 + NONPOW2 + [1])
+def test_c2c_vs_numpy(amd, orc, n):
+    rng = np.random.default_rng(n)
+    x = (rng.random(n) + 1j * rng.random(n)).astype(np.complex64)
+    x64 = x.astype(np.complex128)
+    yf = amd.fft(x, C2C, FWD)
+    yb = amd.fft(x, C2C, BWD)
+    close(yf, np.fft.fft(x64))
+    close(yb, np.fft.ifft(x64))
+    kiss_check(yf, orc.fft(x, C2C, FWD), np.fft.fft(x64), n)
+    kiss_check(yb, orc.fft(x, C2C, BWD), np.fft.ifft(x64), n)
+
+
+@pytest.mark.parametrize("n", POW2 + [8192] + NONPOW2 + [1, 33, 1000])
+def test_r2c_c2r_vs_numpy(amd, orc, n):
+    rng = np.random.default_rng(1000 + n)
+    xr = rng.random(n).astype(np.float32)
+    X = amd.fft(xr, R2C)
+    close(X, np.fft.rfft(xr.astype(np.float64)))
+    if n % 2 == 0 and n > 1:
+        assert X[-1].imag == 0.0   # fft_kiss.c:141-143
+    Xin = np.fft.rfft(xr.astype(np.float64)).astype(np.complex64)
+    y = amd.fft(Xin, C2R, BWD, n=n)
+    close(y, np.fft.irfft(Xin.astype(np.complex128), n=n))
+    kiss_check(X, orc.fft(xr, R2C), np.fft.rfft(xr.astype(np.float64)), n)
+
+
+def test_impulse_known_answer(amd):
+    """tests/fft_backend_tests.c:70-99 and spectral_tests.c:14-35 of the reference."""
+    for n in (8, 16, 1024):
+        x = np.zeros(n, np.complex64)
+        x[0] = 1
+        X = amd.fft(x, C2C, FWD)
+        np.testing.assert_allclose(X, np.ones(n), atol=1e-5)
+        xr = amd.fft(X, C2C, BWD)
+        np.testing.assert_allclose(xr, x, atol=1e-5)
+
+
+def test_r2c_c2r_sine_roundtrip(amd):
+    """fft_backend_tests.c:156-238 / spectral_tests.c:37-66 (tol 1e-3)."""
+    for n in (8, 16, 1024):
+        i = np.arange(n, dtype=np.float32)
+        xr = np.sin(np.float32(2.0) * np.float32(np.pi) * i / np.float32(n)).astype(np.float32)
+        X = amd.fft(xr, R2C)
+        y = amd.fft(X, C2R, BWD, n=n)
+        np.testing.assert_allclose(y, xr, atol=1e-3)
+
+
+@pytest.mark.parametrize("n", [16, 64, 128])
+def test_backend_consistency_with_kiss(amd, orc, n):
+    """gtest/test_fft.cpp:322-358: complex exponential at bin 1 vs Kiss, 1e-5 abs."""
+    t = np.arange(n)
+    x = np.exp(2j * np.pi * t / n).astype(np.complex64)
+    np.testing.assert_allclose(amd.fft(x, C2C, FWD), orc.fft(x, C2C, FWD), atol=1e-5, rtol=0)
+
+
+def test_golden_fft_testpy(amd, golden):
+    for n in (16, 1024):
+        g = golden(f"fft_testpy_n{n}")
+        close(amd.fft(g["x"], C2C, FWD), g["c2c_fwd_np64"])
+        close(amd.fft(g["x"], C2C, BWD), g["c2c_bwd_np64"])
+        close(amd.fft(g["xr"], R2C), g["r2c_np64"])
+        # the reference's own C2R fails this at n=1024 (1.22x); ours must pass
+        close(amd.fft(g["X"], C2R, BWD, n=n), g["c2r_np64"])
+
+
+def test_golden_batched_device(vdev, golden):
+    import torch
+    g = golden("fft_batch64_n1024")
+    x = torch.from_numpy(g["x"]).cuda()
+    plan = vdev.FftPlan(1024, vdev.C2C, vdev.FWD, batch=64)
+    y = plan(x).cpu().numpy()
+    close(y, g["np64"])
+    close(y, g["kiss"], factor=2.0)
+
+
+def test_device_plan_inplace_and_batch(vdev):
+    import torch
+    rng = np.random.default_rng(5)
+    for n in (64, 1024, 4096, 100):
+        b = 33
+        x = (rng.uniform(-0.5, 0.5, (b, n)) + 1j * rng.uniform(-0.5, 0.5, (b, n))).astype(np.complex64)
+        t = torch.from_numpy(x).cuda()
+        plan = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)
+        plan(t, out=t)   # in place
+        close(t.cpu().numpy(), np.fft.fft(x.astype(np.complex128), axis=1))
+
+
+# ---------------------------------------------------------------- STFT
+def test_golden_stft_spectrogram(amd, golden):
+    g = golden("stft_48000_n1024_h256")
+    mag = amd.spectrogram(g["x"], 1024, 256)
+    assert mag.shape == g["kiss"].shape
+    close(mag, g["np64"])
+    close(mag, g["kiss"], factor=2.0)
+
+
+@pytest.mark.parametrize("nfft,hop", [(1024, 256), (512, 128), (256, 1), (64, 64), (4096, 1024),
+                                      (8192, 2048), (100, 30), (16, 5)])
+def test_stft_vs_oracle(amd, orc, nfft, hop):
+    rng = np.random.default_rng(nfft + hop)
+    for n in (nfft // 2, nfft, 3 * nfft + 7):
+        x = rng.uniform(-1, 1, n).astype(np.float32)
+        mag = amd.spectrogram(x, nfft, hop)
+        ref = orc.spectrogram(x, nfft, hop)
+        assert mag.shape == ref.shape
+        w = orc.window(1, nfft).astype(np.float64)
+        fr = ref.shape[0]
+        pad = np.concatenate([x.astype(np.float64), np.zeros(nfft, np.float64)])
+        np_mag = np.abs(np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1))
+        close(mag, np_mag, factor=1.0 if nfft <= 1024 else 4.0)
+
+
+def test_stft_process_and_reconstruct(amd, orc):
+    """spectral_tests.c:82-121: STFT/OLA roundtrip MSE < 1e-2; plus process vs Kiss."""
+    import ctypes as C
+    N, F, H = 256, 64, 32
+    x = np.sin(np.float32(2 * np.pi) * np.arange(N, dtype=np.float32) / np.float32(32)).astype(np.float32)
+    st, h = amd.stft_create(F, H, 1)
+    assert st == OK
+    try:
+        y = np.zeros(N + F, np.float32)
+        norm = np.zeros(N + F, np.float32)
+        fp = lambda a, off=0: a[off:].ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+        start = 0
+        while start + F <= N + (F - H):
+            frame = np.array([x[start + i] if start + i < N else 0 for i in range(F)], np.float32)
+            spec = amd.stft_process(h, frame, F)
+            w = orc.window(1, F)
+            np.testing.assert_allclose(spec, orc.fft((frame * w).astype(np.complex64), C2C, FWD),
+                                       rtol=1e-4, atol=1e-5)
+            spec32 = np.ascontiguousarray(spec.view(np.float32))
+            assert amd.lib.vv_dsp_stft_reconstruct(h, fp(spec32), fp(y, start), fp(norm, start)) == OK
+            start += H
+        y[norm > 1e-12] /= norm[norm > 1e-12]
+        assert np.mean((x - y[:N]) ** 2) < 1e-2
+    finally:
+        amd.lib.vv_dsp_stft_destroy(h)
+
+
+def test_stft_multichannel_equals_single(vdev):
+    import torch
+    rng = np.random.default_rng(9)
+    sig = torch.from_numpy(rng.uniform(-1, 1, (5, 20000)).astype(np.float32)).cuda()
+    st = vdev.Stft(1024, 256)
+    multi = st.spectrogram(sig)
+    for c in range(5):
+        single = st.spectrogram(sig[c].contiguous())
+        assert torch.equal(multi[c], single)
+    spec = st.spectrogram(sig, complex_out=True)
+    torch.testing.assert_close(spec.abs(), multi, rtol=1e-5, atol=1e-5)
+
+
+# ---------------------------------------------------------------- FIR
+def test_golden_fir_direct_bitexact(amd, golden):
+    g = golden("fir_257_n16384")
+    y = amd.fir_apply(g["h"], g["x"])
+    assert np.array_equal(y, g["kiss"])   # same summation order as fir.c:170-186
+
+
+def test_golden_fir_fft(amd, golden):
+    g = golden("fir_257_n16384")
+    y = amd.fir_apply(g["h"], g["x"], fft=True)
+    np.testing.assert_allclose(y, g["np64"], rtol=3e-3, atol=3e-3)   # python/test_filters.py:32-33
+    np.testing.assert_allclose(y, g["np64"], rtol=1e-5, atol=2e-6)
+    g = golden("firfft_257_n1500")
+    np.testing.assert_allclose(amd.fir_apply(g["h"], g["x"], fft=True), g["np64"], rtol=1e-5, atol=2e-6)
+
+
+def test_fir_streaming_state_matches_reference(amd, orc):
+    """vv_dsp_fir_apply across calls: history ring continues exactly (bit-exact)."""
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    h = orc.fir_design_lowpass(33, 0.2, 1)
+    x = rng.standard_normal(5000).astype(np.float32)
+    st = FirState()
+    assert amd.lib.vv_dsp_fir_state_init(C.byref(st), 33) == OK
+    try:
+        chunks = [x[:7], x[7:40], x[40:41], x[41:3000], x[3000:]]
+        y = np.concatenate([amd.fir_apply(h, c, state=st) for c in chunks])
+    finally:
+        amd.lib.vv_dsp_fir_state_free(C.byref(st))
+    assert np.array_equal(y, orc.fir_apply(h, x))
+
+
+@pytest.mark.parametrize("taps", [1, 2, 7, 64, 257, 1025, 5000])
+def test_fir_fft_sizes(amd, orc, taps):
+    rng = np.random.default_rng(taps)
+    h = rng.standard_normal(taps).astype(np.float32) / np.sqrt(taps)
+    for n in (1, 100, 20000):
+        x = rng.standard_normal(n).astype(np.float32)
+        y = amd.fir_apply(h, x, fft=True)
+        ref = np.convolve(x.astype(np.float64), h.astype(np.float64))[:n]
+        np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_fir_filter_tests_impulse(amd):
+    """filter_tests.c:17-39: fir_apply_fft on a minimal state ({0}, num_taps only)."""
+    import ctypes as C
+    h = amd.fir_design_lowpass(7, 0.3, 2)
+    x = np.zeros(32, np.float32)
+    x[0] = 1
+    st = FirState()
+    st.num_taps = 7
+    y = np.zeros(32, np.float32)
+    fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+    assert amd.lib.vv_dsp_fir_apply_fft(C.byref(st), fp(h), fp(x), fp(y), 32) == OK
+    assert np.sum(y.astype(np.float64) ** 2) > 0
+    np.testing.assert_allclose(y[:7], h, atol=1e-6)
+
+
+def test_fir_multichannel_device(vdev, orc):
+    import torch
+    rng = np.random.default_rng(4)
+    h = orc.fir_design_lowpass(257, 0.25, 2)
+    x = rng.uniform(-1, 1, (3, 50000)).astype(np.float32)
+    plan = vdev.FirPlan(torch.from_numpy(h))
+    y = plan(torch.from_numpy(x).cuda()).cpu().numpy()
+    yd = plan(torch.from_numpy(x).cuda(), direct=True).cpu().numpy()
+    for c in range(3):
+        assert np.array_equal(yd[c], orc.fir_apply(h, x[c]))
+        np.testing.assert_allclose(y[c], yd[c], rtol=1e-5, atol=3e-6)
+
+
+# ---------------------------------------------------------------- Hilbert / DCT
+def test_golden_hilbert(amd, golden):
+    for n in (1024, 255):
+        g = golden(f"hilbert_n{n}")
+        z = amd.hilbert(g["x"])
+        np.testing.assert_allclose(z, g["np64"], rtol=1e-5, atol=1e-5)
+
+
+def test_hilbert_sine_known_answer(amd):
+    """hilbert_tests.c:16-48: bin-centred sine, real part within 1e-3, imag = -cos."""
+    N, fs, k = 256, 1000.0, 31
+    f0 = k * fs / N
+    x = np.sin(2 * np.pi * f0 * np.arange(N) / fs).astype(np.float32)
+    z = amd.hilbert(x)
+    assert np.max(np.abs(z.real - x)) < 1e-3
+    np.testing.assert_allclose(z.imag, -np.cos(2 * np.pi * f0 * np.arange(N) / fs), atol=1e-4)
+
+
+@pytest.mark.parametrize("n", [4, 7, 8, 63, 64, 257, 1024, 4096])
+def test_hilbert_sizes(amd, n):
+    import scipy.signal
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n).astype(np.float32)
+    np.testing.assert_allclose(amd.hilbert(x), scipy.signal.hilbert(x.astype(np.float64)), rtol=1e-4, atol=2e-5)
+
+
+def test_golden_dct(amd, golden):
+    for n in (64, 1024):
+        g = golden(f"dct2_n{n}")
+        y = amd.dct(g["x"], 2, False)
+        np.testing.assert_allclose(y, g["np64"], rtol=1e-4, atol=1e-4)
+        xi = amd.dct(y, 2, True)
+        np.testing.assert_allclose(xi, g["x"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 63, 64, 257, 1024, 8192])
+def test_dct_types_vs_formula(amd, n):
+    import scipy.fft
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n).astype(np.float32)
+    x64 = x.astype(np.float64)
+    tol = dict(rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(n) / 8))
+    np.testing.assert_allclose(amd.dct(x, 2), scipy.fft.dct(x64, 2) / 2, **tol)
+    np.testing.assert_allclose(amd.dct(x, 2, True), scipy.fft.idct(2 * x64, 2), **tol)
+    np.testing.assert_allclose(amd.dct(x, 3, True), scipy.fft.idct(2 * x64, 2), **tol)
+    np.testing.assert_allclose(amd.dct(x, 4), scipy.fft.dct(x64, 4) / 2, **tol)
+    np.testing.assert_allclose(amd.dct(x, 4, True), scipy.fft.dct(x64, 4) / n, **tol)
+    kk = np.arange(n)[:, None]
+    nn = np.arange(n)[None, :]
+    y3 = x64[0] + 2 * (np.cos(np.pi * kk * (nn + 0.5) / n)[:, 1:] @ x64[1:]) if n > 1 else x64[:1]
+    np.testing.assert_allclose(amd.dct(x, 3), y3, **tol)
+
+
+def test_dct_roundtrip_known_answer(amd):
+    """dct_tests.c:11-50: DCT-II -> inverse and DCT-IV involution at n=8, 1e-5."""
+    n = 8
+    x = np.sin(np.float32(2 * np.pi) * np.arange(n, dtype=np.float32) / np.float32(n)).astype(np.float32)
+    np.testing.assert_allclose(amd.dct(amd.dct(x, 2), 2, True), x, atol=1e-5)
+    x4 = np.cos(2 * np.pi * (np.arange(n) + 0.3) / n).astype(np.float32)
+    np.testing.assert_allclose(amd.dct(amd.dct(x4, 4), 4, True), x4, atol=1e-5)

@@ -1,0 +1,94 @@
+"""CPU tests: the oracle (oracle/vv_oracle.c, our restatement of the reference)
+is pinned bit-for-bit against the reference's own compiled sources
+(oracle/_ref/libvvref.so) and against the committed golden vectors, and the
+golden vectors themselves are checked against NumPy/SciPy f64 with the
+reference harness tolerances (python/test_fft.py:37-38,62; test_filters.py:32-33)."""
+import numpy as np
+import pytest
+
+from vvapi import C2C, R2C, C2R, FWD, BWD
+
+SIZES = [1, 2, 3, 4, 5, 7, 8, 12, 16, 17, 31, 64, 100, 128, 256, 1024, 4096]
+
+
+def test_oracle_fft_bitexact_vs_reference(orc, ref):
+    rng = np.random.default_rng(11)
+    for n in SIZES:
+        x = (rng.random(n) + 1j * rng.random(n)).astype(np.complex64)
+        for d in (FWD, BWD):
+            assert np.array_equal(orc.fft(x, C2C, d), ref.fft(x, C2C, d)), (n, d)
+        xr = rng.standard_normal(n).astype(np.float32)
+        assert np.array_equal(orc.fft(xr, R2C), ref.fft(xr, R2C)), n
+        if n <= 1024:
+            X = np.fft.rfft(xr).astype(np.complex64)
+            assert np.array_equal(orc.fft(X, C2R, BWD, n=n), ref.fft(X, C2R, BWD, n=n)), n
+
+
+def test_oracle_stft_hilbert_dct_fir_bitexact(orc, ref):
+    rng = np.random.default_rng(12)
+    x = rng.uniform(-1, 1, 20000).astype(np.float32)
+    for nfft, hop in [(1024, 256), (512, 128), (64, 64), (256, 1), (100, 30)]:
+        assert np.array_equal(orc.spectrogram(x[:5000], nfft, hop), ref.spectrogram(x[:5000], nfft, hop))
+    for n in [1, 2, 7, 8, 255, 256, 1024]:
+        s = rng.standard_normal(n).astype(np.float32)
+        assert np.array_equal(orc.hilbert(s), ref.hilbert(s)), n
+        for t in (2, 3, 4):
+            for inv in (False, True):
+                assert np.array_equal(orc.dct(s, t, inv), ref.dct(s, t, inv)), (n, t, inv)
+    for taps in [1, 2, 7, 33, 257]:
+        for wk in (0, 1, 2, 3):
+            a, b = orc.fir_design_lowpass(taps, 0.25, wk), ref.fir_design_lowpass(taps, 0.25, wk)
+            assert np.array_equal(a, b, equal_nan=True), (taps, wk)
+        h = orc.fir_design_lowpass(taps, 0.25, 2)
+        assert np.array_equal(orc.fir_apply(h, x[:3000]), ref.fir_apply(h, x[:3000]), equal_nan=True)
+        assert np.array_equal(orc.fir_apply(h, x[:400], fft=True), ref.fir_apply(h, x[:400], fft=True),
+                              equal_nan=True)
+
+
+def test_oracle_matches_golden(orc, golden):
+    g = golden("fft_testpy_n1024")
+    assert np.array_equal(orc.fft(g["x"], C2C, FWD), g["c2c_fwd_kiss"])
+    assert np.array_equal(orc.fft(g["x"], C2C, BWD), g["c2c_bwd_kiss"])
+    assert np.array_equal(orc.fft(g["xr"], R2C), g["r2c_kiss"])
+    assert np.array_equal(orc.fft(g["X"], C2R, BWD, n=1024), g["c2r_kiss"])
+    g = golden("fft_batch64_n1024")
+    for i in range(0, 64, 9):
+        assert np.array_equal(orc.fft(g["x"][i], C2C, FWD), g["kiss"][i])
+    g = golden("stft_48000_n1024_h256")
+    assert np.array_equal(orc.window(1, 1024), g["window"])
+    assert np.array_equal(orc.spectrogram(g["x"], 1024, 256), g["kiss"])
+    for n in (1024, 255):
+        g = golden(f"hilbert_n{n}")
+        assert np.array_equal(orc.hilbert(g["x"]), g["kiss"])
+    for n in (64, 1024):
+        g = golden(f"dct2_n{n}")
+        assert np.array_equal(orc.dct(g["x"], 2, False), g["kiss"])
+        assert np.array_equal(orc.dct(g["kiss"], 2, True), g["inv_kiss"])
+    g = golden("fir_257_n16384")
+    assert np.array_equal(orc.fir_design_lowpass(257, 0.25, 2), g["h"])
+    assert np.array_equal(orc.fir_apply(g["h"], g["x"]), g["kiss"])
+    g = golden("firfft_257_n1500")
+    assert np.array_equal(orc.fir_apply(g["h"], g["x"], fft=True), g["kiss"])
+
+
+def _err_over_tol(y, ref, rtol, atol):
+    return float(np.max(np.abs(y - ref) / (atol + rtol * np.abs(ref))))
+
+
+def test_golden_kiss_accuracy_profile(golden):
+    """The reference's own accuracy vs f64: C2C/R2C pass the
+    harness tolerance at n=1024, its O(n^2) C2R does not (1.22x)."""
+    g = golden("fft_testpy_n1024")
+    assert _err_over_tol(g["c2c_fwd_kiss"], g["c2c_fwd_np64"], 5e-5, 5e-5) < 1.0
+    assert _err_over_tol(g["r2c_kiss"], g["r2c_np64"], 5e-5, 5e-5) < 1.0
+    assert _err_over_tol(g["c2r_kiss"], g["c2r_np64"], 5e-5, 5e-5) > 1.0
+    g = golden("fft_testpy_n16")
+    for k in ("c2c_fwd", "c2c_bwd", "r2c", "c2r"):
+        assert _err_over_tol(g[k + "_kiss"], g[k + "_np64"], 5e-5, 5e-5) < 1.0, k
+    g = golden("stft_48000_n1024_h256")
+    assert _err_over_tol(g["kiss"], g["np64"], 5e-5, 5e-5) < 1.0
+    g = golden("fir_257_n16384")
+    np.testing.assert_allclose(g["kiss"], g["np64"], rtol=3e-3, atol=3e-3)
+    for n in (1024, 255):
+        g = golden(f"hilbert_n{n}")
+        assert np.max(np.abs(g["kiss"] - g["np64"])) < 1e-4

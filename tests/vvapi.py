@@ -1,0 +1,282 @@
+"""ctypes binding of the vv-dsp public C API (the reference's names and ABI).
+
+The same binding drives two libraries that export the identical C99 surface:
+  * oracle/_ref/libvvref.so  -- the reference's own sources (parity checker), and
+  * vv-dsp_amd/lib/libvvdsp_amd.so -- our MI355X drop-in (HIP backend).
+so the parity tests read like the reference's own C tests
+(tests/fft_backend_tests.c, tests/spectral_tests.c in the reference tree).
+
+ABI follows include/vv_dsp/vv_dsp_types.h:70-128 (float real, {re,im} complex,
+int status enum) and include/vv_dsp/spectral/{fft,stft,dct,hilbert}.h,
+include/vv_dsp/filter/fir.h of the reference.
+"""
+import ctypes as C
+import numpy as np
+
+OK = 0
+ERR_NULL, ERR_SIZE, ERR_RANGE, ERR_INTERNAL, ERR_NAN, ERR_UNSUPPORTED = 1, 2, 3, 4, 5, 6
+C2C, R2C, C2R = 0, 1, 2
+FWD, BWD = 1, -1
+KISS, FFTW, FFTS, HIP = 0, 1, 2, 3
+WIN_BOXCAR, WIN_HANN, WIN_HAMMING = 0, 1, 2
+FIRWIN_RECT, FIRWIN_HAMMING, FIRWIN_HANNING, FIRWIN_BLACKMAN = 0, 1, 2, 3
+DCT_II, DCT_III, DCT_IV = 2, 3, 4
+
+_f32p = C.POINTER(C.c_float)
+_vp = C.c_void_p
+
+
+class StftParams(C.Structure):
+    _fields_ = [("fft_size", C.c_size_t), ("hop_size", C.c_size_t), ("window", C.c_int)]
+
+
+class FirState(C.Structure):
+    _fields_ = [("history", _f32p), ("history_size", C.c_size_t),
+                ("history_idx", C.c_size_t), ("num_taps", C.c_size_t)]
+
+
+def _fp(a):
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_f32p)
+
+
+def _cplx_view(a):
+    """complex64 ndarray -> float32 view (interleaved re,im)."""
+    a = np.ascontiguousarray(a, dtype=np.complex64)
+    return a.view(np.float32)
+
+
+class VvDsp:
+    """Thin wrapper around a library exporting the vv_dsp_* API."""
+
+    def __init__(self, path):
+        self.path = path
+        self.lib = L = C.CDLL(path)
+        L.vv_dsp_fft_make_plan.argtypes = [C.c_size_t, C.c_int, C.c_int, C.POINTER(_vp)]
+        L.vv_dsp_fft_execute.argtypes = [_vp, _vp, _vp]
+        L.vv_dsp_fft_destroy.argtypes = [_vp]
+        L.vv_dsp_fft_set_backend.argtypes = [C.c_int]
+        L.vv_dsp_fft_get_backend.restype = C.c_int
+        L.vv_dsp_fft_is_backend_available.argtypes = [C.c_int]
+        L.vv_dsp_stft_create.argtypes = [C.POINTER(StftParams), C.POINTER(_vp)]
+        L.vv_dsp_stft_destroy.argtypes = [_vp]
+        L.vv_dsp_stft_process.argtypes = [_vp, _f32p, _f32p]
+        L.vv_dsp_stft_reconstruct.argtypes = [_vp, _f32p, _f32p, _f32p]
+        L.vv_dsp_stft_spectrogram.argtypes = [_vp, _f32p, C.c_size_t, _f32p, C.POINTER(C.c_size_t)]
+        L.vv_dsp_hilbert_analytic.argtypes = [_f32p, C.c_size_t, _f32p]
+        L.vv_dsp_dct_forward.argtypes = [C.c_size_t, C.c_int, _f32p, _f32p]
+        L.vv_dsp_dct_inverse.argtypes = [C.c_size_t, C.c_int, _f32p, _f32p]
+        L.vv_dsp_fir_design_lowpass.argtypes = [_f32p, C.c_size_t, C.c_float, C.c_int]
+        L.vv_dsp_fir_state_init.argtypes = [C.POINTER(FirState), C.c_size_t]
+        L.vv_dsp_fir_state_free.argtypes = [C.POINTER(FirState)]
+        L.vv_dsp_fir_state_free.restype = None
+        L.vv_dsp_fir_apply.argtypes = [C.POINTER(FirState), _f32p, _f32p, _f32p, C.c_size_t]
+        L.vv_dsp_fir_apply_fft.argtypes = [C.POINTER(FirState), _f32p, _f32p, _f32p, C.c_size_t]
+        if hasattr(L, "vv_dsp_window_hann"):
+            L.vv_dsp_window_hann.argtypes = [C.c_size_t, _f32p]
+        if hasattr(L, "vvhip_available"):
+            L.vvhip_available.restype = C.c_int
+            L.vvhip_last_error.restype = C.c_char_p
+
+    def _err(self):
+        if hasattr(self.lib, "vvhip_last_error"):
+            return ": " + self.lib.vvhip_last_error().decode(errors="replace")
+        return ""
+
+    # ---- FFT ------------------------------------------------------------
+    def make_plan(self, n, kind, direction):
+        p = _vp()
+        st = self.lib.vv_dsp_fft_make_plan(n, kind, direction, C.byref(p))
+        return st, p
+
+    def fft(self, x, kind=C2C, direction=FWD, n=None):
+        """Execute one transform with the reference's buffer conventions (fft.h:169-177)."""
+        if kind == C2C:
+            xin = _cplx_view(x)
+            n = len(x) if n is None else n
+            out = np.zeros(2 * n, np.float32)
+        elif kind == R2C:
+            xin = np.ascontiguousarray(x, np.float32)
+            n = len(x) if n is None else n
+            out = np.zeros(2 * (n // 2 + 1), np.float32)
+        else:
+            xin = _cplx_view(x)
+            assert n is not None
+            out = np.zeros(n, np.float32)
+        st, p = self.make_plan(n, kind, direction)
+        if st != OK:
+            raise RuntimeError(f"make_plan status {st}{self._err()}")
+        try:
+            st = self.lib.vv_dsp_fft_execute(p, xin.ctypes.data, out.ctypes.data)
+            if st != OK:
+                raise RuntimeError(f"execute status {st}{self._err()}")
+        finally:
+            self.lib.vv_dsp_fft_destroy(p)
+        return out.view(np.complex64) if kind != C2R else out
+
+    # ---- STFT -----------------------------------------------------------
+    def stft_create(self, nfft, hop, window=WIN_HANN):
+        prm = StftParams(nfft, hop, window)
+        h = _vp()
+        st = self.lib.vv_dsp_stft_create(C.byref(prm), C.byref(h))
+        return st, h
+
+    def spectrogram(self, x, nfft, hop, window=WIN_HANN):
+        st, h = self.stft_create(nfft, hop, window)
+        if st != OK:
+            raise RuntimeError(f"stft_create status {st}")
+        x = np.ascontiguousarray(x, np.float32)
+        n = len(x)
+        frames = 1 if n < nfft else 1 + (n - nfft + hop) // hop
+        out = np.zeros(frames * nfft, np.float32)
+        nf = C.c_size_t(0)
+        try:
+            st = self.lib.vv_dsp_stft_spectrogram(h, _fp(x), n, _fp(out), C.byref(nf))
+            if st != OK:
+                raise RuntimeError(f"spectrogram status {st}")
+        finally:
+            self.lib.vv_dsp_stft_destroy(h)
+        assert nf.value == frames
+        return out.reshape(frames, nfft)
+
+    def stft_process(self, h, frame, nfft):
+        spec = np.zeros(2 * nfft, np.float32)
+        st = self.lib.vv_dsp_stft_process(h, _fp(np.ascontiguousarray(frame, np.float32)), _fp(spec))
+        if st != OK:
+            raise RuntimeError(f"stft_process status {st}")
+        return spec.view(np.complex64)
+
+    # ---- Hilbert / DCT / FIR -------------------------------------------
+    def hilbert(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        z = np.zeros(2 * len(x), np.float32)
+        st = self.lib.vv_dsp_hilbert_analytic(_fp(x), len(x), _fp(z))
+        if st != OK:
+            raise RuntimeError(f"hilbert status {st}")
+        return z.view(np.complex64)
+
+    def dct(self, x, dct_type=DCT_II, inverse=False):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros_like(x)
+        f = self.lib.vv_dsp_dct_inverse if inverse else self.lib.vv_dsp_dct_forward
+        st = f(len(x), dct_type, _fp(x), _fp(y))
+        if st != OK:
+            raise RuntimeError(f"dct status {st}")
+        return y
+
+    def fir_design_lowpass(self, taps, fc, wkind=FIRWIN_HANNING):
+        h = np.zeros(taps, np.float32)
+        st = self.lib.vv_dsp_fir_design_lowpass(_fp(h), taps, fc, wkind)
+        if st != OK:
+            raise RuntimeError(f"fir_design status {st}")
+        return h
+
+    def fir_apply(self, h, x, fft=False, state=None):
+        """Zero-state (fresh) FIR unless a FirState is supplied."""
+        h = np.ascontiguousarray(h, np.float32)
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros_like(x)
+        own = state is None
+        if own:
+            state = FirState()
+            assert self.lib.vv_dsp_fir_state_init(C.byref(state), len(h)) == OK
+        try:
+            f = self.lib.vv_dsp_fir_apply_fft if fft else self.lib.vv_dsp_fir_apply
+            st = f(C.byref(state), _fp(h), _fp(x), _fp(y), len(x))
+            if st != OK:
+                raise RuntimeError(f"fir status {st}")
+        finally:
+            if own:
+                self.lib.vv_dsp_fir_state_free(C.byref(state))
+        return y
+
+    def hann(self, n):
+        w = np.zeros(n, np.float32)
+        assert self.lib.vv_dsp_window_hann(n, _fp(w)) == OK
+        return w
+
+
+class Oracle:
+    """Binding of oracle/liboracle.so (our C restatement; test infrastructure)."""
+
+    def __init__(self, path):
+        self.lib = L = C.CDLL(path)
+        L.orc_fft_c2c.argtypes = [_f32p, _f32p, C.c_size_t, C.c_int]
+        L.orc_fft_r2c.argtypes = [_f32p, _f32p, C.c_size_t]
+        L.orc_fft_c2r.argtypes = [_f32p, _f32p, C.c_size_t]
+        L.orc_window.argtypes = [C.c_int, C.c_size_t, _f32p]
+        L.orc_stft_spectrogram.argtypes = [_f32p, C.c_size_t, C.c_size_t, _f32p, C.c_size_t,
+                                           _f32p, C.POINTER(C.c_size_t)]
+        L.orc_stft_num_frames.argtypes = [C.c_size_t] * 3
+        L.orc_stft_num_frames.restype = C.c_size_t
+        L.orc_stft_process.argtypes = [_f32p, C.c_size_t, _f32p, _f32p]
+        L.orc_stft_reconstruct.argtypes = [_f32p, C.c_size_t, _f32p, _f32p, _f32p]
+        L.orc_hilbert_analytic.argtypes = [_f32p, C.c_size_t, _f32p]
+        L.orc_dct.argtypes = [_f32p, _f32p, C.c_size_t, C.c_int, C.c_int]
+        L.orc_fir_design_lowpass.argtypes = [_f32p, C.c_size_t, C.c_float, C.c_int]
+        L.orc_fir_apply.argtypes = [_f32p, C.c_size_t, _f32p, C.POINTER(C.c_size_t), _f32p,
+                                    _f32p, C.c_size_t]
+        L.orc_fir_apply_fft.argtypes = [_f32p, C.c_size_t, _f32p, _f32p, C.c_size_t]
+
+    def fft(self, x, kind=C2C, direction=FWD, n=None):
+        if kind == C2C:
+            xin = _cplx_view(x)
+            n = len(x)
+            out = np.zeros(2 * n, np.float32)
+            assert self.lib.orc_fft_c2c(_fp(xin), _fp(out), n, direction) == 0
+            return out.view(np.complex64)
+        if kind == R2C:
+            xin = np.ascontiguousarray(x, np.float32)
+            n = len(x)
+            out = np.zeros(2 * (n // 2 + 1), np.float32)
+            assert self.lib.orc_fft_r2c(_fp(xin), _fp(out), n) == 0
+            return out.view(np.complex64)
+        xin = _cplx_view(x)
+        out = np.zeros(n, np.float32)
+        assert self.lib.orc_fft_c2r(_fp(xin), _fp(out), n) == 0
+        return out
+
+    def window(self, kind, n):
+        w = np.zeros(n, np.float32)
+        assert self.lib.orc_window(kind, n, _fp(w)) == 0
+        return w
+
+    def spectrogram(self, x, nfft, hop, window=WIN_HANN):
+        w = self.window(window, nfft)
+        x = np.ascontiguousarray(x, np.float32)
+        frames = self.lib.orc_stft_num_frames(len(x), nfft, hop)
+        out = np.zeros(frames * nfft, np.float32)
+        nf = C.c_size_t(0)
+        assert self.lib.orc_stft_spectrogram(_fp(w), nfft, hop, _fp(x), len(x), _fp(out),
+                                             C.byref(nf)) == 0
+        return out.reshape(frames, nfft)
+
+    def hilbert(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        z = np.zeros(2 * len(x), np.float32)
+        assert self.lib.orc_hilbert_analytic(_fp(x), len(x), _fp(z)) == 0
+        return z.view(np.complex64)
+
+    def dct(self, x, dct_type=DCT_II, inverse=False):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros_like(x)
+        assert self.lib.orc_dct(_fp(x), _fp(y), len(x), dct_type, -1 if inverse else 1) == 0
+        return y
+
+    def fir_design_lowpass(self, taps, fc, wkind=FIRWIN_HANNING):
+        h = np.zeros(taps, np.float32)
+        assert self.lib.orc_fir_design_lowpass(_fp(h), taps, fc, wkind) == 0
+        return h
+
+    def fir_apply(self, h, x, fft=False):
+        h = np.ascontiguousarray(h, np.float32)
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros_like(x)
+        if fft:
+            assert self.lib.orc_fir_apply_fft(_fp(h), len(h), _fp(x), _fp(y), len(x)) == 0
+        else:
+            hist = np.zeros(max(len(h) - 1, 1), np.float32)
+            idx = C.c_size_t(0)
+            assert self.lib.orc_fir_apply(_fp(h), len(h), _fp(hist), C.byref(idx), _fp(x),
+                                          _fp(y), len(x)) == 0
+        return y

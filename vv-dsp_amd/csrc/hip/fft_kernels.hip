@@ -1,0 +1,471 @@
+// fft_kernels.hip -- batched C2C / R2C / C2R kernels for gfx950.
+//
+// Power-of-two lengths use the persistent register/LDS Stockham kernels of
+// fft_core.hpp: each wave (or workgroup, for N >= 2048) loops over transforms,
+// keeping its per-thread twiddles in VGPRs, reading one transform with
+// lane-contiguous loads and writing it with lane-contiguous stores: one HBM
+// read + one HBM write per transform (8 B/point each way for C2C).
+//
+// R2C of real length 2M runs an M-point complex FFT on z[m] = x[2m] + i x[2m+1]
+// followed by the split step  X[k] = Fe + W_{2M}^k (-i Fo)  in LDS; C2R runs the
+// inverse split step on the load path and an M-point inverse FFT, so real
+// transforms move 4 B/point.  Other lengths use an O(n^2) DFT kernel with f64
+// accumulation (the reference's own complexity for them: fft_kiss.c:76-92).
+#include "fft_core.hpp"
+#include "vvhip_internal.hpp"
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <vector>
+
+namespace vvh {
+
+// ------------------------------------------------------------------------
+// twiddle tables (host-side double -> f32, cached)
+// ------------------------------------------------------------------------
+namespace {
+std::mutex g_tab_mu;
+std::map<std::pair<int, int>, void*> g_tabs;   // (device, n) -> float2[n]
+std::map<std::pair<int, long long>, void*> g_tabs_d;   // (device, n) -> double2[n]
+}  // namespace
+
+const float2* twiddle_table(int n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    auto key = std::make_pair(dev, n);
+    auto it = g_tabs.find(key);
+    if (it != g_tabs.end()) return (const float2*)it->second;
+    std::vector<float2> h(n);
+    for (int k = 0; k < n; ++k) {
+        // exact argument reduction: angle = 2*pi*k/n computed from the reduced fraction
+        const double a = -2.0 * M_PI * (double)k / (double)n;
+        h[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, sizeof(float2) * n) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, h.data(), sizeof(float2) * n, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    g_tabs[key] = d;
+    return (const float2*)d;
+}
+
+static const double2* twiddle_table_d(long long n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    auto key = std::make_pair(dev, n);
+    auto it = g_tabs_d.find(key);
+    if (it != g_tabs_d.end()) return (const double2*)it->second;
+    std::vector<double2> h(n);
+    for (long long k = 0; k < n; ++k) {
+        const double a = -2.0 * M_PI * (double)k / (double)n;
+        h[k] = make_double2(std::cos(a), std::sin(a));
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, sizeof(double2) * n) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, h.data(), sizeof(double2) * n, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    g_tabs_d[key] = d;
+    return (const double2*)d;
+}
+
+int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 1;
+    long long g = (long long)cus * per_cu;
+    if (work_blocks < g) g = work_blocks;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+// ------------------------------------------------------------------------
+// C2C.  Persistent: each slot (wave, or the whole block for N >= 2048) loops
+// over transforms; the next transform's 16 points per lane are loaded into a
+// second register set before the current one is computed, so every wave
+// keeps its 8 KB (N = 1024) of HBM reads in flight while it works.  Twiddles
+// live in LDS, so vmcnt only ever waits on streamed data.
+// ------------------------------------------------------------------------
+template <int N, bool FWD>
+__global__ void __launch_bounds__(Wg<N>::value)
+k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
+      const float2* gtab, float scale) {
+    using G = Geo<N>;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
+    __shared__ float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, WG>(ltab, gtab);
+    __syncthreads();
+    const auto tw = twiddles_from<N>(ltab);
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    const long long stride = (long long)gridDim.x * F;
+    long long f = (long long)blockIdx.x * F + slot;
+    float2 nx[G::P];
+    if (f < batch) {
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(in + f * in_dist + t + r * G::T);
+    }
+    for (; f < batch; f += stride) {
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = nx[r];
+        const long long fn = f + stride;
+        if (fn < batch) {
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(in + fn * in_dist + t + r * G::T);
+        }
+        fft_regs<N, FWD>(v, t, my, tw);
+        float2* dst = out + f * out_dist;
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            float2 o = v[q];
+            if (!FWD) o = cscale(o, scale);
+            st_nt(o, dst + out_pos<N>(t, q));
+        }
+    }
+}
+
+template <int N, bool FWD>
+static hipError_t run_c2c(const float2* in, float2* out, long long batch, long long in_dist,
+                          long long out_dist, float scale, hipStream_t s) {
+    const float2* tab = twiddle_table(N);
+    if (!tab) return hipErrorOutOfMemory;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    static int grid_cap = 0;
+    if (!grid_cap) grid_cap = persistent_grid((const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
+    long long need = (batch + F - 1) / F;
+    int grid = (int)(need < grid_cap ? need : grid_cap);
+    if (grid < 1) return hipSuccess;
+    hipLaunchKernelGGL((k_c2c<N, FWD>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist,
+                       tab, scale);
+    return hipGetLastError();
+}
+
+bool c2c_supported(long long n) { return n >= 2 && n <= 4096 && (n & (n - 1)) == 0; }
+
+hipError_t launch_c2c(long long n, int fwd, const float2* in, float2* out, long long batch,
+                      long long in_dist, long long out_dist, float scale, hipStream_t s) {
+#define VVH_C2C(NN)                                                                           \
+    case NN:                                                                                  \
+        return fwd ? run_c2c<NN, true>(in, out, batch, in_dist, out_dist, scale, s)           \
+                   : run_c2c<NN, false>(in, out, batch, in_dist, out_dist, scale, s);
+    switch (n) {
+        VVH_C2C(2) VVH_C2C(4) VVH_C2C(8) VVH_C2C(16) VVH_C2C(32) VVH_C2C(64) VVH_C2C(128)
+        VVH_C2C(256) VVH_C2C(512) VVH_C2C(1024) VVH_C2C(2048) VVH_C2C(4096)
+        default: return hipErrorInvalidValue;
+    }
+#undef VVH_C2C
+}
+
+// ------------------------------------------------------------------------
+// R2C (real length 2M): M-point complex FFT of z[m] = x[2m] + i x[2m+1],
+// then the split step through LDS.  C2R: the inverse split step (reading the
+// prefetched half spectrum back from LDS for the k / M-k pairing), then an
+// M-point inverse FFT; x[2m] = Re z[m], x[2m+1] = Im z[m].
+// ------------------------------------------------------------------------
+template <int M>
+__global__ void __launch_bounds__(Wg<M>::value)
+k_r2c(const float* in, float2* out, long long batch, long long in_dist, long long out_dist,
+      const float2* gtabM, const float2* gtab2M) {
+    using G = Geo<M>;
+    constexpr int WG = Wg<M>::value, F = Wg<M>::F;
+    __shared__ float2 lds[F * G::LDS];
+    __shared__ float2 ltab[TwLayout<M>::ENTRIES];
+    __shared__ float2 lpost[PostLayout<M>::ENTRIES];
+    stage_twiddles<M, WG>(ltab, gtabM);
+    stage_post<M, WG>(lpost, gtab2M);
+    __syncthreads();
+    const auto tw = twiddles_from<M>(ltab);
+    const auto pw = post_from<M>(lpost);
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + slot * G::LDS;
+    const long long stride = (long long)gridDim.x * F;
+    long long f = (long long)blockIdx.x * F + slot;
+    float2 nx[G::P];
+    if (f < batch) {
+        const float2* src = reinterpret_cast<const float2*>(in + f * in_dist);
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(src + t + r * G::T);
+    }
+    for (; f < batch; f += stride) {
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = nx[r];
+        const long long fn = f + stride;
+        if (fn < batch) {
+            const float2* src = reinterpret_cast<const float2*>(in + fn * in_dist);
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(src + t + r * G::T);
+        }
+        fft_regs<M, true>(v, t, my, tw);
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
+        xsync<G::T>();
+        float2* dst = out + f * out_dist;
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int k = t + G::T * q;
+            const float2 A = my[G::pad(k)];
+            if (k == 0) {
+                st_nt(make_float2(A.x + A.y, 0.0f), dst);
+                st_nt(make_float2(A.x - A.y, 0.0f), dst + M);
+            } else {
+                st_nt(split_fwd(A, cconj(my[G::pad(M - k)]), pw(k)), dst + k);
+            }
+        }
+        xsync<G::T>();
+    }
+}
+
+template <int M>
+__global__ void __launch_bounds__(Wg<M>::value)
+k_c2r(const float2* in, float* out, long long batch, long long in_dist, long long out_dist,
+      const float2* gtabM, const float2* gtab2M, float scale) {
+    using G = Geo<M>;
+    constexpr int WG = Wg<M>::value, F = Wg<M>::F;
+    __shared__ float2 lds[F * G::LDS];
+    __shared__ float2 ltab[TwLayout<M>::ENTRIES];
+    __shared__ float2 lpost[PostLayout<M>::ENTRIES];
+    stage_twiddles<M, WG>(ltab, gtabM);
+    stage_post<M, WG>(lpost, gtab2M);
+    __syncthreads();
+    const auto tw = twiddles_from<M>(ltab);
+    const auto pw = post_from<M>(lpost);
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + slot * G::LDS;
+    const long long stride = (long long)gridDim.x * F;
+    long long f = (long long)blockIdx.x * F + slot;
+    float2 nx[G::P];
+    float2 nxm = make_float2(0.0f, 0.0f);
+    if (f < batch) {
+        const float2* src = in + f * in_dist;
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(src + t + r * G::T);
+        nxm = src[M];
+    }
+    for (; f < batch; f += stride) {
+        float2 xm = nxm;
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) my[G::pad(t + r * G::T)] = nx[r];
+        const long long fn = f + stride;
+        if (fn < batch) {
+            const float2* src = in + fn * in_dist;
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(src + t + r * G::T);
+            nxm = src[M];
+        }
+        xsync<G::T>();
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            const int k = t + r * G::T;
+            float2 A = my[G::pad(k)];
+            float2 B;
+            if (k == 0) {   // imag of DC and Nyquist ignored (fft_kiss.c:158-171 result)
+                A.y = 0.0f;
+                B = make_float2(xm.x, 0.0f);
+            } else {
+                B = my[G::pad(M - k)];
+            }
+            v[r] = split_inv(A, B, pw(k));
+        }
+        xsync<G::T>();
+        fft_regs<M, false>(v, t, my, tw);
+        float2* dst = reinterpret_cast<float2*>(out + f * out_dist);
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) st_nt(cscale(v[q], scale), dst + out_pos<M>(t, q));
+    }
+}
+
+template <int M>
+static hipError_t run_r2c(const float* in, float2* out, long long batch, long long in_dist,
+                          long long out_dist, hipStream_t s) {
+    const float2* tM = twiddle_table(M);
+    const float2* t2M = twiddle_table(2 * M);
+    if (!tM || !t2M) return hipErrorOutOfMemory;
+    constexpr int WG = Wg<M>::value, F = Wg<M>::F;
+    static int cap = 0;
+    if (!cap) cap = persistent_grid((const void*)k_r2c<M>, WG, 0, 1LL << 40);
+    long long need = (batch + F - 1) / F;
+    int grid = (int)(need < cap ? need : cap);
+    if (grid < 1) return hipSuccess;
+    hipLaunchKernelGGL(k_r2c<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, tM, t2M);
+    return hipGetLastError();
+}
+
+template <int M>
+static hipError_t run_c2r(const float2* in, float* out, long long batch, long long in_dist,
+                          long long out_dist, hipStream_t s) {
+    const float2* tM = twiddle_table(M);
+    const float2* t2M = twiddle_table(2 * M);
+    if (!tM || !t2M) return hipErrorOutOfMemory;
+    constexpr int WG = Wg<M>::value, F = Wg<M>::F;
+    static int cap = 0;
+    if (!cap) cap = persistent_grid((const void*)k_c2r<M>, WG, 0, 1LL << 40);
+    long long need = (batch + F - 1) / F;
+    int grid = (int)(need < cap ? need : cap);
+    if (grid < 1) return hipSuccess;
+    hipLaunchKernelGGL(k_c2r<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, tM, t2M,
+                       1.0f / (float)M);
+    return hipGetLastError();
+}
+
+bool r2c_supported(long long n) { return n >= 4 && n <= 8192 && (n & (n - 1)) == 0; }
+
+#define VVH_REAL_SWITCH(CALL)                                                                   \
+    switch (n / 2) {                                                                            \
+        case 2: return CALL(2); case 4: return CALL(4); case 8: return CALL(8);                 \
+        case 16: return CALL(16); case 32: return CALL(32); case 64: return CALL(64);           \
+        case 128: return CALL(128); case 256: return CALL(256); case 512: return CALL(512);     \
+        case 1024: return CALL(1024); case 2048: return CALL(2048); case 4096: return CALL(4096); \
+        default: return hipErrorInvalidValue;                                                   \
+    }
+
+hipError_t launch_r2c(long long n, const float* in, float2* out, long long batch, long long in_dist,
+                      long long out_dist, hipStream_t s) {
+#define CALL(MM) run_r2c<MM>(in, out, batch, in_dist, out_dist, s)
+    VVH_REAL_SWITCH(CALL)
+#undef CALL
+}
+
+hipError_t launch_c2r(long long n, const float2* in, float* out, long long batch, long long in_dist,
+                      long long out_dist, hipStream_t s) {
+#define CALL(MM) run_c2r<MM>(in, out, batch, in_dist, out_dist, s)
+    VVH_REAL_SWITCH(CALL)
+#undef CALL
+}
+
+// ------------------------------------------------------------------------
+// O(n^2) DFT for arbitrary n (f64 accumulation, exact index reduction)
+// ------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_dft_naive(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
+            long long in_dist, long long out_dist, float scale, const double2* __restrict__ tab,
+            long long kblocks) {
+    __shared__ double2 tile[256];
+    const long long f = (long long)blockIdx.x / kblocks;
+    const long long k = ((long long)blockIdx.x % kblocks) * 256 + threadIdx.x;
+    const float* rin = reinterpret_cast<const float*>(in) + (real_in ? f * in_dist : 0);
+    const float2* cin = reinterpret_cast<const float2*>(in) + (real_in ? 0 : f * in_dist);
+    double ar = 0.0, ai = 0.0;
+    long long idx = 0;   // (k * t) mod n, advanced incrementally
+    const long long kk = (k < n) ? k : 0;
+    for (long long t0 = 0; t0 < n; t0 += 256) {
+        const long long tt = t0 + threadIdx.x;
+        if (tt < n) {
+            if (real_in) tile[threadIdx.x] = make_double2((double)rin[tt], 0.0);
+            else { const float2 c = cin[tt]; tile[threadIdx.x] = make_double2((double)c.x, (double)c.y); }
+        }
+        __syncthreads();
+        const long long lim = (n - t0 < 256) ? (n - t0) : 256;
+        for (long long j = 0; j < lim; ++j) {
+            const double2 w = tab[idx];
+            const double wi = fwd ? w.y : -w.y;
+            const double2 x = tile[j];
+            ar += x.x * w.x - x.y * wi;
+            ai += x.x * wi + x.y * w.x;
+            idx += kk;
+            if (idx >= n) idx -= n;
+        }
+        __syncthreads();
+    }
+    if (k < nout) out[f * out_dist + k] = make_float2((float)(ar * scale), (float)(ai * scale));
+}
+
+hipError_t launch_dft_naive(long long n, int fwd, const void* in, int real_in, float2* out,
+                            long long nout, long long batch, long long in_dist, long long out_dist,
+                            float scale, hipStream_t s) {
+    const double2* tab = twiddle_table_d(n);
+    if (!tab) return hipErrorOutOfMemory;
+    const long long kblocks = (nout + 255) / 256;
+    if (kblocks * batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dft_naive, dim3((unsigned)(kblocks * batch)), dim3(256), 0, s, n, fwd, in,
+                       real_in, out, nout, in_dist, out_dist, scale, tab, kblocks);
+    return hipGetLastError();
+}
+
+__global__ void k_herm_expand(long long n, const float2* half, float2* full, long long half_dist,
+                              int zero_imag, long long total) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const long long f = i / n, k = i % n;
+    const long long nh = n / 2 + 1;
+    const float2* h = half + f * half_dist;
+    float2 v;
+    if (k < nh) {
+        v = h[k];
+        if (zero_imag && (k == 0 || (2 * k == n))) v.y = 0.0f;
+    } else {
+        const long long m = n - k;
+        v = (m > 0 && m < nh) ? cconj(h[m]) : make_float2(0.0f, 0.0f);
+    }
+    full[i] = v;
+}
+
+hipError_t launch_hermitian_expand(long long n, const float2* half, float2* full, long long batch,
+                                   long long half_dist, int zero_dc_nyq_imag, hipStream_t s) {
+    const long long total = n * batch;
+    hipLaunchKernelGGL(k_herm_expand, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, n, half,
+                       full, half_dist, zero_dc_nyq_imag, total);
+    return hipGetLastError();
+}
+
+__global__ void k_take_real(const float2* in, float* out, long long count) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) out[i] = in[i].x;
+}
+
+hipError_t launch_take_real(const float2* in, float* out, long long count, hipStream_t s) {
+    hipLaunchKernelGGL(k_take_real, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, in, out, count);
+    return hipGetLastError();
+}
+
+__global__ void k_zero_nyq(float2* out, long long n, long long batch, long long dist) {
+    const long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < batch) out[f * dist + n / 2].y = 0.0f;
+}
+
+hipError_t launch_zero_nyquist_imag(float2* out, long long n, long long batch, long long dist,
+                                    hipStream_t s) {
+    if (n % 2) return hipSuccess;
+    hipLaunchKernelGGL(k_zero_nyq, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, out, n, batch,
+                       dist);
+    return hipGetLastError();
+}
+
+__global__ void k_scale_r(float* p, long long count, float s) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) p[i] *= s;
+}
+__global__ void k_scale_c(float2* p, long long count, float s) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) p[i] = cscale(p[i], s);
+}
+hipError_t launch_scale_real(float* p, long long count, float s, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scale_r, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, p, count, s);
+    return hipGetLastError();
+}
+hipError_t launch_scale_cpx(float2* p, long long count, float s, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scale_c, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, p, count, s);
+    return hipGetLastError();
+}
+
+}  // namespace vvh

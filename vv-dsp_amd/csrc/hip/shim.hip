@@ -1,0 +1,693 @@
+// shim.hip -- the extern "C" HIP shim (include/vv_dsp_hip.h).
+//
+// Owns the device-side objects behind the C99 front-end: FFT plans (own stream,
+// lazily grown host-path staging buffers), STFT handles (device window), FIR
+// handles (device taps + per-block-size spectra H), and dispatches to the
+// kernel launchers of fft_kernels.hip / stft_kernels.hip / fir_kernels.hip /
+// spectral_kernels.hip.  There is no CPU compute path: every transform runs on
+// the GPU, and every entry point reports UNSUPPORTED/INTERNAL when no device is
+// present or a launch fails.
+#include "../../../include/vv_dsp_hip.h"
+#include "vvhip_internal.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+using namespace vvh;
+
+namespace {
+
+enum { ST_OK = 0, ST_NULL = 1, ST_SIZE = 2, ST_RANGE = 3, ST_INTERNAL = 4, ST_NAN = 5, ST_UNSUP = 6 };
+
+thread_local std::string g_err;
+
+int fail(int code, const char* what, hipError_t e = hipSuccess) {
+    g_err = what;
+    if (e != hipSuccess) {
+        g_err += ": ";
+        g_err += hipGetErrorString(e);
+    }
+    return code;
+}
+
+#define HIPCHK(expr, code)                                           \
+    do {                                                             \
+        hipError_t e__ = (expr);                                     \
+        if (e__ != hipSuccess) return fail((code), #expr, e__);      \
+    } while (0)
+
+int device_count() {
+    static int cnt = -1;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+        cnt = c;
+    });
+    return cnt;
+}
+
+bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
+
+// Growable device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// Stream-ordered scratch for multi-kernel paths on device pointers.
+struct Scratch {
+    void* p = nullptr;
+    hipStream_t s;
+    explicit Scratch(hipStream_t st) : s(st) {}
+    hipError_t alloc(size_t bytes) { return hipMallocAsync(&p, bytes ? bytes : 16, s); }
+    ~Scratch() {
+        if (p) (void)hipFreeAsync(p, s);
+    }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// FFT plans
+// ---------------------------------------------------------------------------
+struct vvhip_fft {
+    size_t n = 0;
+    int type = 0;   // 0 C2C 1 R2C 2 C2R
+    int dir = 1;
+    size_t batch = 1;
+    hipStream_t stream = nullptr;
+    DevBuf din, dout;
+};
+
+static size_t fft_in_elems_bytes(const vvhip_fft* p) {
+    switch (p->type) {
+        case 0: return p->n * 8;
+        case 1: return p->n * 4;
+        default: return (p->n / 2 + 1) * 8;
+    }
+}
+static size_t fft_out_elems_bytes(const vvhip_fft* p) {
+    switch (p->type) {
+        case 0: return p->n * 8;
+        case 1: return (p->n / 2 + 1) * 8;
+        default: return p->n * 4;
+    }
+}
+
+// Core device dispatch: `batch` transforms, contiguous, device pointers.
+static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_t batch, hipStream_t s) {
+    const long long N = (long long)n, B = (long long)batch;
+    if (B == 0) return ST_OK;
+    const int fwd = dir > 0;
+    if (type == 0) {
+        if (c2c_supported(N)) {
+            HIPCHK(launch_c2c(N, fwd, (const float2*)in, (float2*)out, B, N, N, 1.0f / (float)N, s), ST_INTERNAL);
+            return ST_OK;
+        }
+        if (n == 1) {
+            if (in != out) HIPCHK(hipMemcpyAsync(out, in, 8 * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+            return ST_OK;
+        }
+        if (is_pow2(n)) return fail(ST_UNSUP, "C2C power-of-two length > 4096 not supported yet");
+        const void* src = in;
+        Scratch tmp(s);
+        if (in == out) {
+            HIPCHK(tmp.alloc(8 * n * batch), ST_INTERNAL);
+            HIPCHK(hipMemcpyAsync(tmp.p, in, 8 * n * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+            src = tmp.p;
+        }
+        HIPCHK(launch_dft_naive(N, fwd, src, 0, (float2*)out, N, B, N, N, fwd ? 1.0f : 1.0f / (float)N, s),
+               ST_INTERNAL);
+        return ST_OK;
+    }
+    const long long NH = N / 2 + 1;
+    if (type == 1) {   // R2C: real[n] -> cpx[n/2+1]
+        if (r2c_supported(N)) {
+            HIPCHK(launch_r2c(N, (const float*)in, (float2*)out, B, N, NH, s), ST_INTERNAL);
+            return ST_OK;
+        }
+        if (is_pow2(n) && n > 8192) return fail(ST_UNSUP, "R2C power-of-two length > 8192 not supported yet");
+        HIPCHK(launch_dft_naive(N, 1, in, 1, (float2*)out, NH, B, N, NH, 1.0f, s), ST_INTERNAL);
+        HIPCHK(launch_zero_nyquist_imag((float2*)out, N, B, NH, s), ST_INTERNAL);
+        return ST_OK;
+    }
+    // C2R: cpx[n/2+1] -> real[n]
+    if (r2c_supported(N)) {
+        HIPCHK(launch_c2r(N, (const float2*)in, (float*)out, B, NH, N, s), ST_INTERNAL);
+        return ST_OK;
+    }
+    if (is_pow2(n) && n > 8192) return fail(ST_UNSUP, "C2R power-of-two length > 8192 not supported yet");
+    Scratch full(s), tim(s);
+    HIPCHK(full.alloc(8 * n * batch), ST_INTERNAL);
+    HIPCHK(tim.alloc(8 * n * batch), ST_INTERNAL);
+    HIPCHK(launch_hermitian_expand(N, (const float2*)in, (float2*)full.p, B, NH, 0, s), ST_INTERNAL);
+    HIPCHK(launch_dft_naive(N, 0, full.p, 0, (float2*)tim.p, N, B, N, N, 1.0f / (float)N, s), ST_INTERNAL);
+    HIPCHK(launch_take_real((const float2*)tim.p, (float*)out, N * B, s), ST_INTERNAL);
+    return ST_OK;
+}
+
+extern "C" {
+
+int vvhip_available(void) { return device_count(); }
+
+const char* vvhip_last_error(void) { return g_err.c_str(); }
+
+const char* vvhip_version(void) { return "vvhip gfx950 (CDNA4) ROCm 7.2"; }
+
+void* vvhip_malloc(size_t bytes) {
+    void* p = nullptr;
+    if (device_count() <= 0 || hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+    return p;
+}
+void vvhip_free(void* p) {
+    if (p) (void)hipFree(p);
+}
+int vvhip_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), ST_INTERNAL);
+    return ST_OK;
+}
+int vvhip_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), ST_INTERNAL);
+    return ST_OK;
+}
+int vvhip_memset(void* dst, int value, size_t bytes) {
+    HIPCHK(hipMemset(dst, value, bytes), ST_INTERNAL);
+    return ST_OK;
+}
+int vvhip_stream_sync(void* stream) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream), ST_INTERNAL);
+    return ST_OK;
+}
+int vvhip_device_sync(void) {
+    HIPCHK(hipDeviceSynchronize(), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_fft_plan_create(size_t n, int type, int dir, size_t batch, vvhip_fft** out) {
+    if (!out) return ST_NULL;
+    *out = nullptr;
+    if (n == 0 || batch == 0) return ST_SIZE;
+    if (type < 0 || type > 2 || (dir != 1 && dir != -1)) return ST_RANGE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    if (type == 0 && is_pow2(n) && n > 4096) return fail(ST_UNSUP, "C2C pow2 > 4096 not supported yet");
+    if (type != 0 && is_pow2(n) && n > 8192) return fail(ST_UNSUP, "real pow2 > 8192 not supported yet");
+    vvhip_fft* p = new (std::nothrow) vvhip_fft;
+    if (!p) return ST_INTERNAL;
+    p->n = n;
+    p->type = type;
+    p->dir = dir;
+    p->batch = batch;
+    *out = p;
+    return ST_OK;
+}
+
+int vvhip_fft_exec_device(vvhip_fft* p, const void* d_in, void* d_out, size_t batch, void* stream) {
+    if (!p || !d_in || !d_out) return ST_NULL;
+    return fft_run(p->n, p->type, p->dir, d_in, d_out, batch ? batch : p->batch, (hipStream_t)stream);
+}
+
+int vvhip_fft_exec_host(vvhip_fft* p, const void* in, void* out) {
+    if (!p || !in || !out) return ST_NULL;
+    if (!p->stream) HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking), ST_INTERNAL);
+    const size_t ib = fft_in_elems_bytes(p) * p->batch, ob = fft_out_elems_bytes(p) * p->batch;
+    HIPCHK(p->din.ensure(ib), ST_INTERNAL);
+    HIPCHK(p->dout.ensure(ob), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(p->din.p, in, ib, hipMemcpyHostToDevice, p->stream), ST_INTERNAL);
+    int st = fft_run(p->n, p->type, p->dir, p->din.p, p->dout.p, p->batch, p->stream);
+    if (st != ST_OK) return st;
+    HIPCHK(hipMemcpyAsync(out, p->dout.p, ob, hipMemcpyDeviceToHost, p->stream), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(p->stream), ST_INTERNAL);
+    return ST_OK;
+}
+
+void vvhip_fft_plan_destroy(vvhip_fft* p) {
+    if (!p) return;
+    if (p->stream) {
+        (void)hipStreamSynchronize(p->stream);
+        (void)hipStreamDestroy(p->stream);
+    }
+    p->din.release();
+    p->dout.release();
+    delete p;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// STFT
+// ---------------------------------------------------------------------------
+struct vvhip_stft {
+    size_t nfft = 0, hop = 0;
+    float* d_win = nullptr;
+    std::vector<float> h_win;
+    hipStream_t stream = nullptr;
+    DevBuf b0, b1, b2;
+};
+
+static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch, size_t ch_stride,
+                           void* out, size_t out_ch_stride, int complex_out, hipStream_t s) {
+    const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    const long long NF = (long long)h->nfft;
+    if (stft_fused_supported(NF)) {
+        HIPCHK(launch_stft(NF, (long long)h->hop, complex_out ? 1 : 0, sig, (long long)n, (long long)nch,
+                           (long long)ch_stride, (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
+               ST_INTERNAL);
+        return ST_OK;
+    }
+    // generic nfft: gather windowed complex frames, batched C2C, magnitude
+    if (is_pow2(h->nfft) && h->nfft > 4096) return fail(ST_UNSUP, "STFT nfft > 8192 not supported yet");
+    for (size_t c = 0; c < nch; ++c) {
+        Scratch fr(s);
+        const size_t cnt = frames * h->nfft;
+        HIPCHK(fr.alloc(8 * cnt), ST_INTERNAL);
+        HIPCHK(launch_frame_gather(NF, (long long)h->hop, sig + c * ch_stride, (long long)n, 1, 0,
+                                   (long long)frames, h->d_win, (float2*)fr.p, s),
+               ST_INTERNAL);
+        if (complex_out) {
+            int st = fft_run(h->nfft, 0, 1, fr.p, (float2*)out + c * out_ch_stride, frames, s);
+            if (st) return st;
+        } else {
+            int st = fft_run(h->nfft, 0, 1, fr.p, fr.p, frames, s);
+            if (st) return st;
+            HIPCHK(launch_magnitude((const float2*)fr.p, (float*)out + c * out_ch_stride, (long long)cnt, s),
+                   ST_INTERNAL);
+        }
+    }
+    return ST_OK;
+}
+
+extern "C" {
+
+size_t vvhip_stft_num_frames(size_t n, size_t nfft, size_t hop) {
+    if (hop == 0) return 0;
+    return (n < nfft) ? 1 : 1 + (n - nfft + hop) / hop;
+}
+
+int vvhip_stft_create(size_t nfft, size_t hop, const float* window, vvhip_stft** out) {
+    if (!out || !window) return ST_NULL;
+    *out = nullptr;
+    if (nfft == 0 || hop == 0 || hop > nfft) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    vvhip_stft* h = new (std::nothrow) vvhip_stft;
+    if (!h) return ST_INTERNAL;
+    h->nfft = nfft;
+    h->hop = hop;
+    h->h_win.assign(window, window + nfft);
+    if (hipMalloc(&h->d_win, sizeof(float) * (nfft + 2)) != hipSuccess ||
+        hipMemcpy(h->d_win, window, sizeof(float) * nfft, hipMemcpyHostToDevice) != hipSuccess) {
+        vvhip_stft_destroy(h);
+        return fail(ST_INTERNAL, "stft window upload");
+    }
+    *out = h;
+    return ST_OK;
+}
+
+void vvhip_stft_destroy(vvhip_stft* h) {
+    if (!h) return;
+    if (h->stream) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipStreamDestroy(h->stream);
+    }
+    if (h->d_win) (void)hipFree(h->d_win);
+    h->b0.release();
+    h->b1.release();
+    h->b2.release();
+    delete h;
+}
+
+static int stft_stream(vvhip_stft* h) {
+    if (!h->stream) HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
+                                  size_t ch_stride, void* d_out, size_t out_ch_stride, int complex_out,
+                                  void* stream) {
+    if (!h || !d_signal || !d_out) return ST_NULL;
+    if (nch == 0) return ST_OK;
+    return stft_frames_run(h, d_signal, n, nch, ch_stride, d_out, out_ch_stride, complex_out,
+                           (hipStream_t)stream);
+}
+
+int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, float* out_mag) {
+    if (!h || !signal || !out_mag) return ST_NULL;
+    if (int st = stft_stream(h)) return st;
+    const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    const size_t ob = sizeof(float) * frames * h->nfft;
+    HIPCHK(h->b0.ensure(sizeof(float) * (n ? n : 1)), ST_INTERNAL);
+    HIPCHK(h->b1.ensure(ob), ST_INTERNAL);
+    if (n) HIPCHK(hipMemcpyAsync(h->b0.p, signal, sizeof(float) * n, hipMemcpyHostToDevice, h->stream), ST_INTERNAL);
+    int st = stft_frames_run(h, (const float*)h->b0.p, n, 1, 0, h->b1.p, frames * h->nfft, 0, h->stream);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(out_mag, h->b1.p, ob, hipMemcpyDeviceToHost, h->stream), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(h->stream), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count, float* d_spec,
+                              void* stream) {
+    if (!h || !d_frames || !d_spec) return ST_NULL;
+    // explicit frames laid back to back: hop = nfft over a count*nfft signal
+    const size_t n = count * h->nfft;
+    const long long NF = (long long)h->nfft;
+    hipStream_t s = (hipStream_t)stream;
+    if (stft_fused_supported(NF)) {
+        HIPCHK(launch_stft(NF, NF, 1, d_frames, (long long)n, 1, 0, (long long)count, h->d_win, d_spec, 0, s),
+               ST_INTERNAL);
+        return ST_OK;
+    }
+    Scratch fr(s);
+    HIPCHK(fr.alloc(8 * n), ST_INTERNAL);
+    HIPCHK(launch_frame_gather(NF, NF, d_frames, (long long)n, 1, 0, (long long)count, h->d_win,
+                               (float2*)fr.p, s),
+           ST_INTERNAL);
+    return fft_run(h->nfft, 0, 1, fr.p, d_spec, count, s);
+}
+
+int vvhip_stft_process_host(vvhip_stft* h, const float* frame, float* spec_out) {
+    if (!h || !frame || !spec_out) return ST_NULL;
+    if (int st = stft_stream(h)) return st;
+    HIPCHK(h->b0.ensure(sizeof(float) * h->nfft), ST_INTERNAL);
+    HIPCHK(h->b1.ensure(8 * h->nfft), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(h->b0.p, frame, sizeof(float) * h->nfft, hipMemcpyHostToDevice, h->stream),
+           ST_INTERNAL);
+    int st = vvhip_stft_process_device(h, (const float*)h->b0.p, 1, (float*)h->b1.p, h->stream);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(spec_out, h->b1.p, 8 * h->nfft, hipMemcpyDeviceToHost, h->stream), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(h->stream), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t count, size_t hop,
+                                  float* d_out_add, float* d_norm_add, void* stream) {
+    if (!h || !d_spec || !d_out_add) return ST_NULL;
+    if (hop == 0) return ST_SIZE;
+    hipStream_t s = (hipStream_t)stream;
+    Scratch tf(s);
+    HIPCHK(tf.alloc(8 * h->nfft * count), ST_INTERNAL);
+    int st = fft_run(h->nfft, 0, -1, d_spec, tf.p, count, s);
+    if (st) return st;
+    HIPCHK(launch_ola((long long)h->nfft, (long long)hop, (const float2*)tf.p, (long long)count, h->d_win,
+                      d_out_add, d_norm_add, s),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_stft_reconstruct_host(vvhip_stft* h, const float* spec, float* out_add, float* norm_add) {
+    if (!h || !spec || !out_add) return ST_NULL;
+    if (int st = stft_stream(h)) return st;
+    const size_t nb = sizeof(float) * h->nfft;
+    HIPCHK(h->b0.ensure(2 * nb), ST_INTERNAL);
+    HIPCHK(h->b1.ensure(nb), ST_INTERNAL);
+    HIPCHK(h->b2.ensure(nb), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(h->b0.p, spec, 2 * nb, hipMemcpyHostToDevice, h->stream), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(h->b1.p, out_add, nb, hipMemcpyHostToDevice, h->stream), ST_INTERNAL);
+    if (norm_add) HIPCHK(hipMemcpyAsync(h->b2.p, norm_add, nb, hipMemcpyHostToDevice, h->stream), ST_INTERNAL);
+    int st = vvhip_stft_reconstruct_device(h, (const float*)h->b0.p, 1, h->nfft, (float*)h->b1.p,
+                                           norm_add ? (float*)h->b2.p : nullptr, h->stream);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(out_add, h->b1.p, nb, hipMemcpyDeviceToHost, h->stream), ST_INTERNAL);
+    if (norm_add) HIPCHK(hipMemcpyAsync(norm_add, h->b2.p, nb, hipMemcpyDeviceToHost, h->stream), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(h->stream), ST_INTERNAL);
+    return ST_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// FIR
+// ---------------------------------------------------------------------------
+struct vvhip_fir {
+    size_t taps = 0;
+    float* d_h = nullptr;
+    struct Spec {
+        size_t nfft;
+        float2* H;
+    };
+    std::vector<Spec> specs;   // H per overlap-save block size
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    DevBuf bx, by, bp;
+};
+
+static size_t fir_block(const vvhip_fir* f, size_t n) {
+    // smallest pow2 >= max(2*taps, 64); grown toward 8192 while the signal is longer
+    size_t nr = 64;
+    while (nr < 2 * f->taps) nr <<= 1;
+    while (nr < 8192 && nr < n + f->taps - 1) nr <<= 1;
+    return nr;
+}
+
+static int fir_spectrum(vvhip_fir* f, size_t nr, const float2** H, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(f->mu);
+    for (auto& sp : f->specs)
+        if (sp.nfft == nr) {
+            *H = sp.H;
+            return ST_OK;
+        }
+    float* hp = nullptr;
+    float2* Hd = nullptr;
+    HIPCHK(hipMalloc(&hp, sizeof(float) * nr), ST_INTERNAL);
+    HIPCHK(hipMalloc(&Hd, sizeof(float2) * (nr / 2 + 1)), ST_INTERNAL);
+    HIPCHK(hipMemsetAsync(hp, 0, sizeof(float) * nr, s), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(hp, f->d_h, sizeof(float) * f->taps, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+    HIPCHK(launch_r2c((long long)nr, hp, Hd, 1, (long long)nr, (long long)(nr / 2 + 1), s), ST_INTERNAL);
+    HIPCHK(launch_scale_cpx(Hd, (long long)(nr / 2 + 1), 2.0f / (float)nr, s), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(s), ST_INTERNAL);
+    (void)hipFree(hp);
+    f->specs.push_back({nr, Hd});
+    *H = Hd;
+    return ST_OK;
+}
+
+extern "C" {
+
+int vvhip_fir_create(const float* h, size_t taps, vvhip_fir** out) {
+    if (!out || !h) return ST_NULL;
+    *out = nullptr;
+    if (taps == 0) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    vvhip_fir* f = new (std::nothrow) vvhip_fir;
+    if (!f) return ST_INTERNAL;
+    f->taps = taps;
+    if (hipMalloc(&f->d_h, sizeof(float) * taps) != hipSuccess ||
+        hipMemcpy(f->d_h, h, sizeof(float) * taps, hipMemcpyHostToDevice) != hipSuccess) {
+        vvhip_fir_destroy(f);
+        return fail(ST_INTERNAL, "fir taps upload");
+    }
+    *out = f;
+    return ST_OK;
+}
+
+void vvhip_fir_destroy(vvhip_fir* f) {
+    if (!f) return;
+    if (f->stream) {
+        (void)hipStreamSynchronize(f->stream);
+        (void)hipStreamDestroy(f->stream);
+    }
+    if (f->d_h) (void)hipFree(f->d_h);
+    for (auto& sp : f->specs) (void)hipFree(sp.H);
+    f->bx.release();
+    f->by.release();
+    f->bp.release();
+    delete f;
+}
+
+size_t vvhip_fir_block_size(vvhip_fir* f, size_t n) { return f ? fir_block(f, n) : 0; }
+
+int vvhip_fir_apply_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n, size_t nch,
+                           size_t x_stride, size_t y_stride, const float* d_prefix, int mode,
+                           void* stream) {
+    if (!f || !d_x || !d_y) return ST_NULL;
+    if (n == 0 || nch == 0) return ST_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const long long L = (long long)f->taps;
+    if (mode == 0 && f->taps <= 4097) {
+        const size_t nr = fir_block(f, n);
+        const float2* H = nullptr;
+        if (int st = fir_spectrum(f, nr, &H, s)) return st;
+        HIPCHK(launch_fir_ols((long long)nr, L, H, d_x, d_y, (long long)n, (long long)nch, (long long)x_stride,
+                              (long long)y_stride, d_prefix, s),
+               ST_INTERNAL);
+        return ST_OK;
+    }
+    HIPCHK(launch_fir_direct(f->d_h, L, d_x, d_y, (long long)n, (long long)nch, (long long)x_stride,
+                             (long long)y_stride, d_prefix, s),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_fir_apply_host(vvhip_fir* f, const float* x, float* y, size_t n, const float* prefix, int mode) {
+    if (!f || !x || !y) return ST_NULL;
+    if (n == 0) return ST_OK;
+    if (!f->stream) HIPCHK(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking), ST_INTERNAL);
+    HIPCHK(f->bx.ensure(sizeof(float) * n), ST_INTERNAL);
+    HIPCHK(f->by.ensure(sizeof(float) * n), ST_INTERNAL);
+    const float* dp = nullptr;
+    if (prefix && f->taps > 1) {
+        HIPCHK(f->bp.ensure(sizeof(float) * (f->taps - 1)), ST_INTERNAL);
+        HIPCHK(hipMemcpyAsync(f->bp.p, prefix, sizeof(float) * (f->taps - 1), hipMemcpyHostToDevice, f->stream),
+               ST_INTERNAL);
+        dp = (const float*)f->bp.p;
+    }
+    HIPCHK(hipMemcpyAsync(f->bx.p, x, sizeof(float) * n, hipMemcpyHostToDevice, f->stream), ST_INTERNAL);
+    int st = vvhip_fir_apply_device(f, (const float*)f->bx.p, (float*)f->by.p, n, 1, n, n, dp, mode, f->stream);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(y, f->by.p, sizeof(float) * n, hipMemcpyDeviceToHost, f->stream), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(f->stream), ST_INTERNAL);
+    return ST_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Hilbert
+// ---------------------------------------------------------------------------
+int vvhip_hilbert_device(const float* d_x, size_t n, size_t batch, float* d_z, void* stream) {
+    if (!d_x || !d_z) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t nh = n / 2 + 1;
+    Scratch half(s);
+    HIPCHK(half.alloc(8 * nh * batch), ST_INTERNAL);
+    int st = fft_run(n, 1, 1, d_x, half.p, batch, s);
+    if (st) return st;
+    // mask straight into the output buffer, then inverse C2C in place
+    HIPCHK(launch_hilbert_mask((long long)n, (const float2*)half.p, (float2*)d_z, (long long)batch, (long long)nh, s),
+           ST_INTERNAL);
+    return fft_run(n, 0, -1, d_z, d_z, batch, s);
+}
+
+int vvhip_hilbert_host(const float* x, size_t n, float* z_out) {
+    if (!x || !z_out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), ST_INTERNAL);
+    float* dx = nullptr;
+    float* dz = nullptr;
+    int st = ST_OK;
+    if (hipMalloc(&dx, sizeof(float) * n) != hipSuccess || hipMalloc(&dz, 8 * n) != hipSuccess) {
+        st = fail(ST_INTERNAL, "hilbert alloc");
+    } else if (hipMemcpyAsync(dx, x, sizeof(float) * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+        st = fail(ST_INTERNAL, "hilbert h2d");
+    } else {
+        st = vvhip_hilbert_device(dx, n, 1, dz, s);
+        if (st == ST_OK && (hipMemcpyAsync(z_out, dz, 8 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                            hipStreamSynchronize(s) != hipSuccess))
+            st = fail(ST_INTERNAL, "hilbert d2h");
+    }
+    (void)hipStreamSynchronize(s);
+    if (dx) (void)hipFree(dx);
+    if (dz) (void)hipFree(dz);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+// ---------------------------------------------------------------------------
+// DCT
+// ---------------------------------------------------------------------------
+int vvhip_dct_device(const float* d_in, float* d_out, size_t n, size_t batch, int type, int dir,
+                     int nan_policy, void* stream) {
+    if (!d_in || !d_out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if ((type != 2 && type != 3 && type != 4) || (dir != 1 && dir != -1)) return ST_RANGE;
+    hipStream_t s = (hipStream_t)stream;
+    const long long N = (long long)n, B = (long long)batch;
+    Scratch xin(s), flag(s), v(s), V(s);
+    HIPCHK(xin.alloc(sizeof(float) * n * batch), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(xin.p, d_in, sizeof(float) * n * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+    int* dflag = nullptr;
+    if (nan_policy == 2) {
+        HIPCHK(flag.alloc(sizeof(int)), ST_INTERNAL);
+        dflag = (int*)flag.p;
+        HIPCHK(hipMemsetAsync(dflag, 0, sizeof(int), s), ST_INTERNAL);
+    }
+    HIPCHK(launch_nan_policy((float*)xin.p, N * B, nan_policy, dflag, s), ST_INTERNAL);
+    if (nan_policy == 2) {
+        int h = 0;
+        HIPCHK(hipMemcpyAsync(&h, dflag, sizeof(int), hipMemcpyDeviceToHost, s), ST_INTERNAL);
+        HIPCHK(hipStreamSynchronize(s), ST_INTERNAL);
+        if (h) return ST_NAN;
+    }
+    const bool fast = is_pow2(n) && n >= 4 && n <= 8192;
+    if (fast && type == 2 && dir > 0) {
+        const float2* tw4n = twiddle_table((int)(4 * n));
+        if (!tw4n) return fail(ST_INTERNAL, "dct twiddles");
+        HIPCHK(v.alloc(sizeof(float) * n * batch), ST_INTERNAL);
+        HIPCHK(V.alloc(8 * (n / 2 + 1) * batch), ST_INTERNAL);
+        HIPCHK(launch_dct2_pre(N, (const float*)xin.p, (float*)v.p, B, s), ST_INTERNAL);
+        int st = fft_run(n, 1, 1, v.p, V.p, batch, s);
+        if (st) return st;
+        HIPCHK(launch_dct2_post(N, (const float2*)V.p, d_out, B, tw4n, s), ST_INTERNAL);
+    } else if (fast && (type == 2 || type == 3) && dir < 0) {
+        const float2* tw4n = twiddle_table((int)(4 * n));
+        if (!tw4n) return fail(ST_INTERNAL, "dct twiddles");
+        HIPCHK(v.alloc(sizeof(float) * n * batch), ST_INTERNAL);
+        HIPCHK(V.alloc(8 * (n / 2 + 1) * batch), ST_INTERNAL);
+        HIPCHK(launch_dct3_pre(N, (const float*)xin.p, (float2*)V.p, B, tw4n, s), ST_INTERNAL);
+        int st = fft_run(n, 2, -1, V.p, v.p, batch, s);
+        if (st) return st;
+        HIPCHK(launch_dct3_post(N, (const float*)v.p, d_out, B, 1.0f, s), ST_INTERNAL);
+    } else {
+        HIPCHK(launch_dct_naive(N, type, dir, (const float*)xin.p, d_out, B, s), ST_INTERNAL);
+    }
+    if (nan_policy != 0) {
+        if (nan_policy == 2) HIPCHK(hipMemsetAsync(dflag, 0, sizeof(int), s), ST_INTERNAL);
+        HIPCHK(launch_nan_policy(d_out, N * B, nan_policy, dflag, s), ST_INTERNAL);
+        if (nan_policy == 2) {
+            int h = 0;
+            HIPCHK(hipMemcpyAsync(&h, dflag, sizeof(int), hipMemcpyDeviceToHost, s), ST_INTERNAL);
+            HIPCHK(hipStreamSynchronize(s), ST_INTERNAL);
+            if (h) return ST_NAN;
+        }
+    }
+    return ST_OK;
+}
+
+int vvhip_dct_host(const float* in, float* out, size_t n, int type, int dir, int nan_policy) {
+    if (!in || !out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), ST_INTERNAL);
+    float* di = nullptr;
+    float* dout = nullptr;
+    int st = ST_OK;
+    if (hipMalloc(&di, sizeof(float) * n) != hipSuccess || hipMalloc(&dout, sizeof(float) * n) != hipSuccess) {
+        st = fail(ST_INTERNAL, "dct alloc");
+    } else if (hipMemcpyAsync(di, in, sizeof(float) * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+        st = fail(ST_INTERNAL, "dct h2d");
+    } else {
+        st = vvhip_dct_device(di, dout, n, 1, type, dir, nan_policy, s);
+        // the reference writes the output buffer even when the output check fails
+        if ((st == ST_OK || st == ST_NAN) &&
+            (hipMemcpyAsync(out, dout, sizeof(float) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess))
+            st = fail(ST_INTERNAL, "dct d2h");
+    }
+    (void)hipStreamSynchronize(s);
+    if (di) (void)hipFree(di);
+    if (dout) (void)hipFree(dout);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+}  // extern "C"

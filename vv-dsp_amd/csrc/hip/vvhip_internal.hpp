@@ -1,0 +1,83 @@
+// vvhip_internal.hpp -- launchers shared between the kernel translation units
+// and the extern "C" shim (shim.hip).  Not part of the public C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace vvh {
+
+// Device-resident W_N^k = exp(-2*pi*i*k/N) table, k < N, f32 rounded from double.
+// Cached per N for the process lifetime (per device).
+const float2* twiddle_table(int n);
+
+// Persistent-grid sizing: resident blocks for `kernel` x CUs, capped by work.
+int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks);
+
+// ---- pow2 register/LDS FFTs (fft_kernels.hip) -----------------------------
+bool c2c_supported(long long n);           // pow2, 2..4096
+// batch transforms of length n; element e of transform f at in[f*in_dist + e]
+hipError_t launch_c2c(long long n, int fwd, const float2* in, float2* out, long long batch,
+                      long long in_dist, long long out_dist, float scale, hipStream_t s);
+bool r2c_supported(long long n);           // pow2 real length, 32..8192
+hipError_t launch_r2c(long long n, const float* in, float2* out, long long batch,
+                      long long in_dist, long long out_dist, hipStream_t s);
+hipError_t launch_c2r(long long n, const float2* in, float* out, long long batch,
+                      long long in_dist, long long out_dist, hipStream_t s);
+// Any n: O(n^2) DFT with f64 accumulation (the reference's non-pow2 path,
+// fft_kiss.c:76-92).  real_in: input is real[n] (R2C promotion); nout bins written.
+hipError_t launch_dft_naive(long long n, int fwd, const void* in, int real_in, float2* out,
+                            long long nout, long long batch, long long in_dist,
+                            long long out_dist, float scale, hipStream_t s);
+// Hermitian expansion used by C2R/Hilbert for non-pow2 n: half[n/2+1] -> full[n]
+hipError_t launch_hermitian_expand(long long n, const float2* half, float2* full, long long batch,
+                                   long long half_dist, int zero_dc_nyq_imag, hipStream_t s);
+hipError_t launch_take_real(const float2* in, float* out, long long count, hipStream_t s);
+hipError_t launch_zero_nyquist_imag(float2* out, long long n, long long batch, long long dist,
+                                    hipStream_t s);
+
+// ---- STFT (stft_kernels.hip) -------------------------------------------
+// mode 0: magnitude rows [frames][nfft] ; mode 1: complex rows [frames][nfft]
+bool stft_fused_supported(long long nfft);
+hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,
+                       long long nch, long long ch_stride, long long frames, const float* win,
+                       void* out, long long out_ch_stride, hipStream_t s);
+// Frames given explicitly (stft_process batch): in real[count][nfft] -> cpx[count][nfft]
+hipError_t launch_stft_frames(long long nfft, const float* frames_in, const float* win,
+                              float2* out, long long count, hipStream_t s);
+// Generic gather (any nfft): windowed complex frames for the generic FFT path
+hipError_t launch_frame_gather(long long nfft, long long hop, const float* sig, long long n,
+                               long long nch, long long ch_stride, long long frames,
+                               const float* win, float2* out, hipStream_t s);
+hipError_t launch_magnitude(const float2* in, float* out, long long count, hipStream_t s);
+// ISTFT accumulate (stft_reconstruct batch): out_add[i] += Re(t[f][i])*w[i] for frames at hop
+hipError_t launch_ola(long long nfft, long long hop, const float2* time_frames, long long count,
+                      const float* win, float* out_add, float* norm_add, hipStream_t s);
+
+// ---- FIR overlap-save (fir_kernels.hip) ---------------------------------
+bool fir_ols_supported(long long nfft);
+// H: nfft/2+1 complex, already scaled by 2/nfft.  prefix: [nch][taps-1] chronological or null.
+hipError_t launch_fir_ols(long long nfft, long long taps, const float2* H, const float* x,
+                          float* y, long long n, long long nch, long long x_stride,
+                          long long y_stride, const float* prefix, hipStream_t s);
+hipError_t launch_fir_direct(const float* h, long long taps, const float* x, float* y, long long n,
+                             long long nch, long long x_stride, long long y_stride,
+                             const float* prefix, hipStream_t s);
+hipError_t launch_scale_real(float* p, long long count, float s, hipStream_t st);
+hipError_t launch_scale_cpx(float2* p, long long count, float s, hipStream_t st);
+
+// ---- DCT / Hilbert helpers (spectral_kernels.hip) ----------------------
+hipError_t launch_hilbert_mask(long long n, const float2* half, float2* full, long long batch,
+                               long long half_dist, hipStream_t s);
+hipError_t launch_dct2_pre(long long n, const float* x, float* v, long long batch, hipStream_t s);
+hipError_t launch_dct2_post(long long n, const float2* V, float* X, long long batch,
+                            const float2* tw4n, hipStream_t s);
+hipError_t launch_dct3_pre(long long n, const float* X, float2* V, long long batch,
+                           const float2* tw4n, hipStream_t s);
+hipError_t launch_dct3_post(long long n, const float* v, float* x, long long batch, float scale,
+                            hipStream_t s);
+hipError_t launch_dct_naive(long long n, int type, int dir, const float* in, float* out,
+                            long long batch, hipStream_t s);
+hipError_t launch_nan_policy(float* p, long long count, int policy, int* flag, hipStream_t s);
+
+}  // namespace vvh

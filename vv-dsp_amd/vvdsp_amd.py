@@ -1,0 +1,206 @@
+"""ctypes binding of libvvdsp_amd.so's batched / device-pointer API (vv_dsp_amd.h).
+
+Device memory and streams come from PyTorch (plumbing only): tensors are
+passed as raw HBM pointers, streams as hipStream_t handles.  All compute runs
+in the library's hand-written gfx950 kernels; there is no Python or CPU
+fallback -- loading fails loudly when the library or a device is missing.
+
+`import torch` happens before the library is loaded so that one HIP runtime
+(torch's libamdhip64.so.7) serves both.
+"""
+import ctypes as C
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libvvdsp_amd.so")
+
+OK = 0
+C2C, R2C, C2R = 0, 1, 2
+FWD, BWD = 1, -1
+WIN_BOXCAR, WIN_HANN, WIN_HAMMING = 0, 1, 2
+
+_vp = C.c_void_p
+_sz = C.c_size_t
+_lib = None
+
+
+class StftParams(C.Structure):
+    _fields_ = [("fft_size", C.c_size_t), ("hop_size", C.c_size_t), ("window", C.c_int)]
+
+
+class VvError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the CDLL; raise if the native library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise VvError(f"native library missing: {LIB_PATH} (run `make -C vv-dsp_amd`)")
+    L = C.CDLL(LIB_PATH)
+    L.vvhip_available.restype = C.c_int
+    L.vvhip_last_error.restype = C.c_char_p
+    L.vvhip_version.restype = C.c_char_p
+    L.vv_dsp_fft_make_plan_many.argtypes = [_sz, C.c_int, C.c_int, _sz, C.POINTER(_vp)]
+    L.vv_dsp_fft_execute_device.argtypes = [_vp, _vp, _vp, _vp]
+    L.vv_dsp_fft_destroy.argtypes = [_vp]
+    L.vv_dsp_stft_create.argtypes = [C.POINTER(StftParams), C.POINTER(_vp)]
+    L.vv_dsp_stft_destroy.argtypes = [_vp]
+    L.vv_dsp_stft_spectrogram_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_stft_spectrum_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_stft_process_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.vv_dsp_stft_reconstruct_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp]
+    L.vv_dsp_fir_plan_create.argtypes = [_vp, _sz, C.POINTER(_vp)]
+    L.vv_dsp_fir_plan_destroy.argtypes = [_vp]
+    L.vv_dsp_fir_apply_fft_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]
+    L.vv_dsp_fir_apply_direct_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]
+    L.vv_dsp_hilbert_analytic_device.argtypes = [_vp, _sz, _sz, _vp, _vp]
+    L.vv_dsp_dct_make_plan.argtypes = [_sz, C.c_int, C.c_int, C.POINTER(_vp)]
+    L.vv_dsp_dct_execute_device.argtypes = [_vp, _vp, _vp, _sz, _vp]
+    L.vv_dsp_dct_destroy.argtypes = [_vp]
+    L.vvhip_fir_block_size.argtypes = [_vp, _sz]
+    L.vvhip_fir_block_size.restype = _sz
+    _lib = L
+    return L
+
+
+def _check(st, what):
+    if st != OK:
+        msg = lib().vvhip_last_error().decode(errors="replace")
+        raise VvError(f"{what} failed with status {st}: {msg}")
+
+
+def _ptr(t):
+    assert t.is_cuda and t.is_contiguous(), "device tensors must be contiguous CUDA(HIP) tensors"
+    return C.c_void_p(t.data_ptr())
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def device_count():
+    return lib().vvhip_available()
+
+
+class FftPlan:
+    """Batched FFT plan (vv_dsp_fft_make_plan_many) executed on device tensors."""
+
+    def __init__(self, n, kind=C2C, direction=FWD, batch=1):
+        self.n, self.kind, self.direction, self.batch = n, kind, direction, batch
+        self.h = _vp()
+        _check(lib().vv_dsp_fft_make_plan_many(n, kind, direction, batch, C.byref(self.h)), "make_plan_many")
+
+    def __call__(self, x, out=None, stream=None):
+        n, b = self.n, self.batch
+        if self.kind == C2C:
+            shape, dt = (b, n), torch.complex64
+        elif self.kind == R2C:
+            shape, dt = (b, n // 2 + 1), torch.complex64
+        else:
+            shape, dt = (b, n), torch.float32
+        if out is None:
+            out = torch.empty(shape, dtype=dt, device=x.device)
+        _check(lib().vv_dsp_fft_execute_device(self.h, _ptr(x), _ptr(out), _stream(stream)), "fft_execute_device")
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.vv_dsp_fft_destroy(self.h)
+            self.h = None
+
+
+class Stft:
+    """STFT handle: fused window + FFT + |X| (or complex) over many channels."""
+
+    def __init__(self, nfft, hop, window=WIN_HANN):
+        self.nfft, self.hop = nfft, hop
+        self.h = _vp()
+        prm = StftParams(nfft, hop, window)
+        _check(lib().vv_dsp_stft_create(C.byref(prm), C.byref(self.h)), "stft_create")
+
+    def frames(self, n):
+        return 1 if n < self.nfft else 1 + (n - self.nfft + self.hop) // self.hop
+
+    def spectrogram(self, sig, out=None, stream=None, complex_out=False):
+        """sig: (nch, n) or (n,) float32 device tensor -> (nch, frames, nfft)."""
+        sig2 = sig if sig.dim() == 2 else sig.unsqueeze(0)
+        nch, n = sig2.shape
+        fr = self.frames(n)
+        dt = torch.complex64 if complex_out else torch.float32
+        if out is None:
+            out = torch.empty((nch, fr, self.nfft), dtype=dt, device=sig.device)
+        nf = _sz(0)
+        f = lib().vv_dsp_stft_spectrum_device if complex_out else lib().vv_dsp_stft_spectrogram_device
+        _check(f(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * self.nfft, _stream(stream),
+                 C.byref(nf)), "stft_spectrogram_device")
+        assert nf.value == fr
+        return out if sig.dim() == 2 else out[0]
+
+    def process(self, frames, stream=None):
+        """frames: (count, nfft) float32 -> (count, nfft) complex64 (vv_dsp_stft_process batched)."""
+        out = torch.empty((frames.shape[0], self.nfft), dtype=torch.complex64, device=frames.device)
+        _check(lib().vv_dsp_stft_process_device(self.h, _ptr(frames), frames.shape[0], _ptr(out),
+                                                _stream(stream)), "stft_process_device")
+        return out
+
+    def reconstruct(self, spec, out_add, norm_add=None, stream=None):
+        _check(lib().vv_dsp_stft_reconstruct_device(self.h, _ptr(spec), spec.shape[0], _ptr(out_add),
+                                                    _ptr(norm_add) if norm_add is not None else None,
+                                                    _stream(stream)), "stft_reconstruct_device")
+        return out_add
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.vv_dsp_stft_destroy(self.h)
+            self.h = None
+
+
+class FirPlan:
+    def __init__(self, h):
+        h = h.detach().to("cpu", torch.float32).contiguous()
+        self.taps = h.numel()
+        self.h = _vp()
+        _check(lib().vv_dsp_fir_plan_create(C.c_void_p(h.data_ptr()), self.taps, C.byref(self.h)), "fir_plan_create")
+
+    def __call__(self, x, out=None, direct=False, stream=None):
+        """x: (nch, n) float32 device tensor -> y (nch, n)."""
+        x2 = x if x.dim() == 2 else x.unsqueeze(0)
+        nch, n = x2.shape
+        if out is None:
+            out = torch.empty_like(x2)
+        f = lib().vv_dsp_fir_apply_direct_device if direct else lib().vv_dsp_fir_apply_fft_device
+        _check(f(self.h, _ptr(x2), _ptr(out), n, nch, x2.stride(0), out.stride(0), _stream(stream)), "fir_apply")
+        return out if x.dim() == 2 else out[0]
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.vv_dsp_fir_plan_destroy(self.h)
+            self.h = None
+
+
+def hilbert(x, stream=None):
+    """x: (batch, N) or (N,) float32 device tensor -> complex64 analytic signal."""
+    x2 = x if x.dim() == 2 else x.unsqueeze(0)
+    b, n = x2.shape
+    z = torch.empty((b, n), dtype=torch.complex64, device=x.device)
+    _check(lib().vv_dsp_hilbert_analytic_device(_ptr(x2), n, b, _ptr(z), _stream(stream)), "hilbert_device")
+    return z if x.dim() == 2 else z[0]
+
+
+def dct(x, dct_type=2, inverse=False, stream=None):
+    x2 = x if x.dim() == 2 else x.unsqueeze(0)
+    b, n = x2.shape
+    p = _vp()
+    _check(lib().vv_dsp_dct_make_plan(n, dct_type, -1 if inverse else 1, C.byref(p)), "dct_make_plan")
+    try:
+        y = torch.empty_like(x2)
+        _check(lib().vv_dsp_dct_execute_device(p, _ptr(x2), _ptr(y), b, _stream(stream)), "dct_execute_device")
+    finally:
+        lib().vv_dsp_dct_destroy(p)
+    return y if x.dim() == 2 else y[0]
