@@ -5,17 +5,26 @@
 // as a chain of radix-16 passes (the last one radix 2/4/8 when log2 N is not a
 // multiple of 4).  Each pass is a Stockham autosort step:
 //
-//   butterfly b = t + T*i (i < P/R), inputs  b + r*N/R            (r < R)
-//   twiddle   W_{Ns*R}^{(b mod Ns)*r}                              (Ns = product of earlier radices)
+//   butterfly b (thread t owns P/R of them), inputs  b + r*N/R        (r < R)
+//   twiddle   W_{Ns*R}^{(b mod Ns)*r}                 (Ns = product of earlier radices)
 //   outputs   (b div Ns)*Ns*R + (b mod Ns) + r*Ns
 //
-// so the FIRST pass reads x[t + r*T] (lane-contiguous -> coalesced global loads)
-// and the LAST pass produces X[t + T*i + r*N/R] (lane-contiguous -> coalesced
-// global stores).  Between passes the points are exchanged through LDS with one
-// float2 of padding per 16 (conflict-free ds_write_b64/ds_read_b64 for the
-// strides that occur).  The in-register radix-R DFTs use exact constant
-// twiddles; the inter-pass twiddles come from a W_N^k table rounded from double
-// on the host and staged in LDS (see TwDirect / TwSplit).
+// With the standard ownership b = t + T*i the FIRST pass reads x[t + r*T]
+// (lane-contiguous, coalesced loads) and the LAST pass produces
+// X[t + T*i + r*N/R] (lane-contiguous stores).  Between passes the points go
+// through LDS with one float2 of padding per 16 (conflict-free b64 accesses).
+//
+// "Mirror-paired" last pass (PAIRED = true): the thread owns butterfly pairs
+// {b, NB - b} of the last pass (NB = N/R butterflies), so it ends holding both
+// X[k] and X[N-k] in registers.  Every real-signal split step (R2C, STFT of two
+// frames packed in one complex FFT, FIR spectrum multiply) then needs no LDS
+// round trip.  Available when the last pass leaves >= 2 butterflies per thread.
+//
+// Twiddles: in-register radix-R DFTs use exact constants; inter-pass twiddles
+// come from tables rounded from double on the host and staged in LDS.  For
+// N <= 2048 the table is pass-major (entry (r-1)*Ns + j of pass p holds
+// W_{Ns R}^{j r}) so that lanes with consecutive j read consecutive LDS words
+// (no bank conflicts); larger N use a two-level table W_N^k = lo[k%64]*hi[k/64].
 //
 // Semantics match the reference (src/spectral/fft_kiss.c:27-74): forward is
 // exp(-2*pi*i*k*n/N) unscaled; backward is exp(+...) and the caller applies 1/N.
@@ -124,7 +133,7 @@ struct Geo {
     static constexpr int P = N >= 16 ? 16 : N;          // points per thread
     static constexpr int T = N / P;                     // threads per transform
     static constexpr int NPASS = N >= 16 ? (LOG + 3) / 4 : 1;
-    static constexpr int LDS = N + (N >> 4);            // padded LDS floats2 per transform
+    static constexpr int LDS = N + (N >> 4);            // padded LDS float2 per transform
     __host__ __device__ static constexpr int radix(int p) {
         return N < 16 ? N : ((LOG - 4 * p) >= 4 ? 16 : (1 << (LOG - 4 * p)));
     }
@@ -134,7 +143,117 @@ struct Geo {
         return s;
     }
     __host__ __device__ static constexpr int pad(int e) { return e + (e >> 4); }
+    static constexpr int RL = radix(NPASS - 1);         // last radix
+    static constexpr int NB = N / RL;                   // butterflies in the last pass
+    static constexpr int NPT = P / RL;                  // last-pass butterflies per thread
+    // mirror pairing possible: single-thread transforms, or >= 2 last-pass butterflies per thread
+    static constexpr bool CAN_PAIR = (T == 1) || (NPT >= 2);
+    // pass-major twiddle table: offset of pass p, total entries
+    __host__ __device__ static constexpr int tw_off(int p) {
+        int o = 0;
+        for (int q = 1; q < p; ++q) o += (radix(q) - 1) * ns(q);
+        return o;
+    }
+    static constexpr int TW_PASS_ENTRIES = tw_off(NPASS) > 0 ? tw_off(NPASS) : 1;
 };
+
+// Butterfly owned by thread t in slot i of pass p.
+template <int N, int p, bool PAIRED>
+__device__ __forceinline__ int bfly(int t, int i) {
+    using G = Geo<N>;
+    if constexpr (PAIRED && G::T > 1 && p == G::NPASS - 1) {
+        const int b0 = t + G::T * (i >> 1);
+        if ((i & 1) == 0) return b0;
+        return b0 == 0 ? G::NB / 2 : G::NB - b0;
+    } else {
+        return t + G::T * i;
+    }
+}
+
+// Output position of register q after fft_regs (last-pass layout).
+template <int N, bool PAIRED = false>
+__device__ __forceinline__ int out_pos(int t, int q) {
+    using G = Geo<N>;
+    constexpr int R = G::RL;
+    return bfly<N, G::NPASS - 1, PAIRED>(t, q / R) + (q % R) * (N / R);
+}
+
+// In a PAIRED layout: register holding X[N - out_pos(t, q)].  Two candidates
+// (compile-time indices) selected by whether this is thread 0's self-mirrored
+// slots 0/1; callers pick with `t == 0 && q < 2R ? special : normal`.
+template <int N>
+struct Mirror {
+    using G = Geo<N>;
+    static constexpr int R = G::RL;
+    __host__ __device__ static constexpr int normal(int q) {
+        if (G::T == 1) return (N - q) % N;
+        const int i = q / R, r = q % R;
+        return (i ^ 1) * R + (R - 1 - r);
+    }
+    __host__ __device__ static constexpr int special(int q) {   // thread 0, slots 0 and 1
+        if (G::T == 1) return (N - q) % N;
+        const int i = q / R, r = q % R;
+        return i == 0 ? (R - r) % R : R + (R - 1 - r);
+    }
+};
+
+// Bitwise select between two register values.  A plain `c ? v[i] : v[j]` is
+// folded by LLVM into `v[c ? i : j]` -- a dynamic index that sends the whole
+// register array to scratch; masking the bits keeps both indices static.
+__device__ __forceinline__ float2 select2(bool c, float2 a, float2 b) {
+    const unsigned m = c ? 0xffffffffu : 0u;
+    return make_float2(__uint_as_float((__float_as_uint(a.x) & m) | (__float_as_uint(b.x) & ~m)),
+                       __uint_as_float((__float_as_uint(a.y) & m) | (__float_as_uint(b.y) & ~m)));
+}
+
+template <int N, bool PAIRED>
+__device__ __forceinline__ float2 mirror_of(const float2* v, int t, int q) {
+    using M = Mirror<N>;
+    if constexpr (Geo<N>::T == 1) {
+        return v[M::normal(q)];
+    } else {
+        if (q < 2 * M::R) return select2(t == 0, v[M::special(q)], v[M::normal(q)]);
+        return v[M::normal(q)];
+    }
+}
+
+// ---- inter-pass twiddle sources --------------------------------------------
+// Streaming kernels keep every table in LDS so that VMEM carries only the
+// streamed data (loads of the NEXT transform are prefetched; a table load at
+// use would sit behind them in the in-order vmcnt queue).
+template <int N>
+struct TwLayout {
+    static constexpr bool SPLIT = N > 2048;
+    static constexpr int ENTRIES = SPLIT ? 64 + N / 64 : Geo<N>::TW_PASS_ENTRIES;
+};
+
+template <int N>
+struct TwTab {
+    const float2* tab;   // LDS: pass-major table, or lo[64] ++ hi[N/64] when SPLIT
+    template <int p>
+    __device__ __forceinline__ float2 at(int j, int r) const {
+        using G = Geo<N>;
+        if constexpr (TwLayout<N>::SPLIT) {
+            const int k = j * r * (N / (G::ns(p) * G::radix(p)));
+            return cmul(tab[k & 63], tab[64 + (k >> 6)]);
+        } else {
+            return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
+        }
+    }
+};
+
+// Stage the global table into LDS (all NTHREADS threads of the block).
+//   gpass : pass-major table for N (host: pass_twiddles(N)), used when !SPLIT
+//   gtab  : W_N^k, k < N (host: twiddle_table(N)), used when SPLIT
+template <int N, int NTHREADS>
+__device__ __forceinline__ void stage_twiddles(float2* lds_tab, const float2* gpass, const float2* gtab) {
+    if constexpr (TwLayout<N>::SPLIT) {
+        for (int i = threadIdx.x; i < 64; i += NTHREADS) lds_tab[i] = gtab[i];
+        for (int i = threadIdx.x; i < N / 64; i += NTHREADS) lds_tab[64 + i] = gtab[64 * i];
+    } else {
+        for (int i = threadIdx.x; i < TwLayout<N>::ENTRIES; i += NTHREADS) lds_tab[i] = gpass[i];
+    }
+}
 
 // Barrier between LDS writes and reads of one transform.  A transform owned by
 // threads of a single wave needs no s_barrier: LDS ops of a wave execute in
@@ -150,62 +269,19 @@ __device__ __forceinline__ void xsync() {
     }
 }
 
-// ---- inter-pass twiddle sources -------------------------------------------
-// Streaming kernels keep every table in LDS so that VMEM carries only the
-// streamed data (loads of the NEXT transform are prefetched; a table load at
-// use would sit behind them in the in-order vmcnt queue).  Tables are staged
-// from the host-computed W_N^k (f32 rounded from double) at kernel start.
-//   TwDirect : W_N^k = tab[k]                          (N <= 2048: <= 16 KB)
-//   TwSplit  : W_N^k = lo[k & 63] * hi[k >> 6]          (N  > 2048: 64 + N/64 entries)
-struct TwDirect {
-    const float2* tab;
-    __device__ __forceinline__ float2 operator()(int k) const { return tab[k]; }
-};
-struct TwSplit {
-    const float2* lo;   // W_N^j, j < 64
-    const float2* hi;   // W_N^(64 i), i < N/64
-    __device__ __forceinline__ float2 operator()(int k) const { return cmul(lo[k & 63], hi[k >> 6]); }
-};
-
-// LDS footprint (float2 entries) of the twiddle source for a length-N transform.
-template <int N>
-struct TwLayout {
-    static constexpr bool SPLIT = N > 2048;
-    static constexpr int ENTRIES = SPLIT ? 64 + N / 64 : N;
-};
-
-// Cooperative copy of the W_N table into LDS (all threads of the block), then
-// returns the accessor.  `gtab` is the global W_N^k table (N entries).
-template <int N, int NTHREADS>
-__device__ __forceinline__ void stage_twiddles(float2* lds_tab, const float2* gtab) {
-    if constexpr (TwLayout<N>::SPLIT) {
-        for (int i = threadIdx.x; i < 64; i += NTHREADS) lds_tab[i] = gtab[i];
-        for (int i = threadIdx.x; i < N / 64; i += NTHREADS) lds_tab[64 + i] = gtab[64 * i];
-    } else {
-        for (int i = threadIdx.x; i < N; i += NTHREADS) lds_tab[i] = gtab[i];
-    }
-}
-
-template <int N>
-__device__ __forceinline__ auto twiddles_from(const float2* lds_tab) {
-    if constexpr (TwLayout<N>::SPLIT) return TwSplit{lds_tab, lds_tab + 64};
-    else return TwDirect{lds_tab};
-}
-
 // One Stockham pass p on the registers (twiddle + radix-R DFT), in place.
-// Twiddle W_{Ns*R}^{j*r} = W_N^{j*r*N/(Ns*R)}; a backward pass conjugates.
-template <int N, bool FWD, int p, class TW>
-__device__ __forceinline__ void pass_compute(float2* v, int t, const TW& tw) {
+template <int N, bool FWD, int p, bool PAIRED>
+__device__ __forceinline__ void pass_compute(float2* v, int t, const TwTab<N>& tw) {
     using G = Geo<N>;
     constexpr int R = G::radix(p);
     constexpr int Ns = G::ns(p);
 #pragma unroll
     for (int i = 0; i < G::P / R; ++i) {
         if constexpr (p > 0) {
-            const int j = (t + G::T * i) % Ns;
+            const int j = bfly<N, p, PAIRED>(t, i) % Ns;
 #pragma unroll
             for (int r = 1; r < R; ++r) {
-                const float2 w = tw(j * r * (N / (Ns * R)));
+                const float2 w = tw.template at<p>(j, r);
                 v[i * R + r] = cmul(v[i * R + r], FWD ? w : cconj(w));
             }
         }
@@ -214,13 +290,13 @@ __device__ __forceinline__ void pass_compute(float2* v, int t, const TW& tw) {
 }
 
 // Exchange after pass p: scatter outputs of pass p, gather inputs of pass p+1.
-template <int N, int p>
+template <int N, int p, bool PAIRED>
 __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
     using G = Geo<N>;
     constexpr int R = G::radix(p), Ns = G::ns(p), R2 = G::radix(p + 1);
 #pragma unroll
     for (int i = 0; i < G::P / R; ++i) {
-        const int b = t + G::T * i;
+        const int b = bfly<N, p, PAIRED>(t, i);
         const int base = (b / Ns) * Ns * R + (b % Ns);
 #pragma unroll
         for (int r = 0; r < R; ++r) lds[G::pad(base + r * Ns)] = v[i * R + r];
@@ -228,40 +304,47 @@ __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
     xsync<G::T>();
 #pragma unroll
     for (int i = 0; i < G::P / R2; ++i) {
-        const int b = t + G::T * i;
+        const int b = bfly<N, p + 1, PAIRED>(t, i);
 #pragma unroll
         for (int r = 0; r < R2; ++r) v[i * R2 + r] = lds[G::pad(b + r * (N / R2))];
     }
     if constexpr (G::T > 64) __syncthreads();   // next pass' writes must not race these reads
 }
 
-template <int N, bool FWD, int p, class TW>
+template <int N, bool FWD, int p, bool PAIRED>
 struct PassChain {
-    __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TW& tw) {
-        pass_compute<N, FWD, p>(v, t, tw);
+    __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TwTab<N>& tw) {
+        pass_compute<N, FWD, p, PAIRED>(v, t, tw);
         if constexpr (p + 1 < Geo<N>::NPASS) {
-            pass_exchange<N, p>(v, t, lds);
-            PassChain<N, FWD, p + 1, TW>::run(v, t, lds, tw);
+            pass_exchange<N, p, PAIRED>(v, t, lds);
+            PassChain<N, FWD, p + 1, PAIRED>::run(v, t, lds, tw);
         }
     }
 };
 
-// Full transform.  On entry v[r] = x[t + r*T] (r < P).  On exit, with R the
-// last radix, v[i*R + r] = X[t + T*i + r*(N/R)].
-template <int N, bool FWD, class TW>
-__device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TW& tw) {
-    PassChain<N, FWD, 0, TW>::run(v, t, lds, tw);
-}
-
-// Output position of register q after fft_regs (last-pass layout).
-template <int N>
-__device__ __forceinline__ constexpr int out_pos(int t, int q) {
-    using G = Geo<N>;
-    constexpr int R = G::radix(G::NPASS - 1);
-    return t + G::T * (q / R) + (q % R) * (N / R);
+// Full transform.  On entry v[r] = x[t + r*T] (r < P).  On exit register q
+// holds X[out_pos<N, PAIRED>(t, q)].
+template <int N, bool FWD, bool PAIRED = false>
+__device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TwTab<N>& tw) {
+    static_assert(!PAIRED || Geo<N>::CAN_PAIR, "mirror pairing needs >= 2 last-pass butterflies per thread");
+    PassChain<N, FWD, 0, PAIRED>::run(v, t, lds, tw);
 }
 
 // ---- shared pieces of the persistent streaming kernels ---------------------
+// A transform owned by >= 64 threads has one work item per wave: make the loop
+// state wave-uniform (SGPRs, scalar branches) so the compiler does not keep
+// exec-masked copies of the register arrays alive across the prefetch branch.
+template <int T>
+__device__ __forceinline__ long long uni(long long x) {
+    if constexpr (T >= 64) {
+        const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(x & 0xffffffffLL));
+        const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)((unsigned long long)x >> 32));
+        return (long long)(((unsigned long long)hi << 32) | lo);
+    } else {
+        return x;
+    }
+}
+
 // Workgroup geometry: 256 threads (several transforms per block) unless one
 // transform needs more threads.
 template <int N>
@@ -286,11 +369,20 @@ __device__ __forceinline__ float2 split_inv(float2 A, float2 B, float2 W) {
     return make_float2(E.x - O.y, E.y + O.x);
 }
 
-// W_{2M}^k for k < M (split-step twiddles), staged in LDS like TwLayout.
+// W_{2M}^k for k < M (split-step twiddles) staged in LDS: direct or two-level.
 template <int M>
 struct PostLayout {
     static constexpr bool SPLIT = 2 * M > 2048;
     static constexpr int ENTRIES = SPLIT ? 64 + M / 64 : M;
+};
+
+template <int M>
+struct PostTab {
+    const float2* tab;
+    __device__ __forceinline__ float2 operator()(int k) const {
+        if constexpr (PostLayout<M>::SPLIT) return cmul(tab[k & 63], tab[64 + (k >> 6)]);
+        else return tab[k];
+    }
 };
 
 template <int M, int NTHREADS>
@@ -301,12 +393,6 @@ __device__ __forceinline__ void stage_post(float2* lds_tab, const float2* g2M) {
     } else {
         for (int i = threadIdx.x; i < M; i += NTHREADS) lds_tab[i] = g2M[i];
     }
-}
-
-template <int M>
-__device__ __forceinline__ auto post_from(const float2* lds_tab) {
-    if constexpr (PostLayout<M>::SPLIT) return TwSplit{lds_tab, lds_tab + 64};
-    else return TwDirect{lds_tab};
 }
 
 }  // namespace vvh

@@ -1,121 +1,43 @@
 // fft_kernels.hip -- batched C2C / R2C / C2R kernels for gfx950.
 //
 // Power-of-two lengths use the persistent register/LDS Stockham kernels of
-// fft_core.hpp: each wave (or workgroup, for N >= 2048) loops over transforms,
-// keeping its per-thread twiddles in VGPRs, reading one transform with
-// lane-contiguous loads and writing it with lane-contiguous stores: one HBM
-// read + one HBM write per transform (8 B/point each way for C2C).
+// fft_core.hpp: each slot (a wave, or the whole block for N >= 2048) loops over
+// transforms with the NEXT transform's points prefetched into a second register
+// set, reading one transform with lane-contiguous loads and writing it with
+// lane-contiguous stores: one HBM read + one HBM write per transform
+// (8 B/point each way for C2C).  Twiddle tables live in LDS, so vmcnt only
+// waits on streamed data.
 //
 // R2C of real length 2M runs an M-point complex FFT on z[m] = x[2m] + i x[2m+1]
-// followed by the split step  X[k] = Fe + W_{2M}^k (-i Fo)  in LDS; C2R runs the
-// inverse split step on the load path and an M-point inverse FFT, so real
-// transforms move 4 B/point.  Other lengths use an O(n^2) DFT kernel with f64
-// accumulation (the reference's own complexity for them: fft_kiss.c:76-92).
+// and the split step X[k] = Fe + W_{2M}^k (-i Fo) with Z[k] and Z[M-k] held in
+// the same thread (mirror-paired last pass); C2R runs the inverse split step
+// and an M-point inverse FFT.  Real transforms move 4 B/point.  Lengths that
+// are not powers of two use an O(n^2) DFT kernel with f64 accumulation (the
+// reference's own complexity for them: fft_kiss.c:76-92).
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
-
-#include <cmath>
-#include <map>
-#include <mutex>
-#include <vector>
 
 namespace vvh {
 
 // ------------------------------------------------------------------------
-// twiddle tables (host-side double -> f32, cached)
-// ------------------------------------------------------------------------
-namespace {
-std::mutex g_tab_mu;
-std::map<std::pair<int, int>, void*> g_tabs;   // (device, n) -> float2[n]
-std::map<std::pair<int, long long>, void*> g_tabs_d;   // (device, n) -> double2[n]
-}  // namespace
-
-const float2* twiddle_table(int n) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(g_tab_mu);
-    auto key = std::make_pair(dev, n);
-    auto it = g_tabs.find(key);
-    if (it != g_tabs.end()) return (const float2*)it->second;
-    std::vector<float2> h(n);
-    for (int k = 0; k < n; ++k) {
-        // exact argument reduction: angle = 2*pi*k/n computed from the reduced fraction
-        const double a = -2.0 * M_PI * (double)k / (double)n;
-        h[k] = make_float2((float)std::cos(a), (float)std::sin(a));
-    }
-    void* d = nullptr;
-    if (hipMalloc(&d, sizeof(float2) * n) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, h.data(), sizeof(float2) * n, hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
-        return nullptr;
-    }
-    g_tabs[key] = d;
-    return (const float2*)d;
-}
-
-static const double2* twiddle_table_d(long long n) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(g_tab_mu);
-    auto key = std::make_pair(dev, n);
-    auto it = g_tabs_d.find(key);
-    if (it != g_tabs_d.end()) return (const double2*)it->second;
-    std::vector<double2> h(n);
-    for (long long k = 0; k < n; ++k) {
-        const double a = -2.0 * M_PI * (double)k / (double)n;
-        h[k] = make_double2(std::cos(a), std::sin(a));
-    }
-    void* d = nullptr;
-    if (hipMalloc(&d, sizeof(double2) * n) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, h.data(), sizeof(double2) * n, hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
-        return nullptr;
-    }
-    g_tabs_d[key] = d;
-    return (const double2*)d;
-}
-
-int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks) {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess ||
-        per_cu <= 0)
-        per_cu = 1;
-    long long g = (long long)cus * per_cu;
-    if (work_blocks < g) g = work_blocks;
-    if (g < 1) g = 1;
-    return (int)g;
-}
-
-// ------------------------------------------------------------------------
-// C2C.  Persistent: each slot (wave, or the whole block for N >= 2048) loops
-// over transforms; the next transform's 16 points per lane are loaded into a
-// second register set before the current one is computed, so every wave
-// keeps its 8 KB (N = 1024) of HBM reads in flight while it works.  Twiddles
-// live in LDS, so vmcnt only ever waits on streamed data.
+// C2C
 // ------------------------------------------------------------------------
 template <int N, bool FWD>
 __global__ void __launch_bounds__(Wg<N>::value)
 k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
-      const float2* gtab, float scale) {
+      const float2* gpass, const float2* gtab, float scale) {
     using G = Geo<N>;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
     __shared__ float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
-    stage_twiddles<N, WG>(ltab, gtab);
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
     __syncthreads();
-    const auto tw = twiddles_from<N>(ltab);
+    const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
     const long long stride = (long long)gridDim.x * F;
-    long long f = (long long)blockIdx.x * F + slot;
+    long long f = uni<G::T>((long long)blockIdx.x * F + slot);
     float2 nx[G::P];
     if (f < batch) {
 #pragma unroll
@@ -145,7 +67,8 @@ template <int N, bool FWD>
 static hipError_t run_c2c(const float2* in, float2* out, long long batch, long long in_dist,
                           long long out_dist, float scale, hipStream_t s) {
     const float2* tab = twiddle_table(N);
-    if (!tab) return hipErrorOutOfMemory;
+    const float2* pas = pass_twiddles(N);
+    if (!tab || !pas) return hipErrorOutOfMemory;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     static int grid_cap = 0;
     if (!grid_cap) grid_cap = persistent_grid((const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
@@ -153,7 +76,7 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     int grid = (int)(need < grid_cap ? need : grid_cap);
     if (grid < 1) return hipSuccess;
     hipLaunchKernelGGL((k_c2c<N, FWD>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist,
-                       tab, scale);
+                       pas, tab, scale);
     return hipGetLastError();
 }
 
@@ -174,29 +97,27 @@ hipError_t launch_c2c(long long n, int fwd, const float2* in, float2* out, long 
 }
 
 // ------------------------------------------------------------------------
-// R2C (real length 2M): M-point complex FFT of z[m] = x[2m] + i x[2m+1],
-// then the split step through LDS.  C2R: the inverse split step (reading the
-// prefetched half spectrum back from LDS for the k / M-k pairing), then an
-// M-point inverse FFT; x[2m] = Re z[m], x[2m+1] = Im z[m].
+// R2C / C2R (real length 2M)
 // ------------------------------------------------------------------------
 template <int M>
 __global__ void __launch_bounds__(Wg<M>::value)
 k_r2c(const float* in, float2* out, long long batch, long long in_dist, long long out_dist,
-      const float2* gtabM, const float2* gtab2M) {
+      const float2* gpass, const float2* gtabM, const float2* gtab2M) {
     using G = Geo<M>;
+    constexpr bool PAIR = G::CAN_PAIR;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     __shared__ float2 lds[F * G::LDS];
     __shared__ float2 ltab[TwLayout<M>::ENTRIES];
     __shared__ float2 lpost[PostLayout<M>::ENTRIES];
-    stage_twiddles<M, WG>(ltab, gtabM);
+    stage_twiddles<M, WG>(ltab, gpass, gtabM);
     stage_post<M, WG>(lpost, gtab2M);
     __syncthreads();
-    const auto tw = twiddles_from<M>(ltab);
-    const auto pw = post_from<M>(lpost);
+    const TwTab<M> tw{ltab};
+    const PostTab<M> pw{lpost};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
     const long long stride = (long long)gridDim.x * F;
-    long long f = (long long)blockIdx.x * F + slot;
+    long long f = uni<G::T>((long long)blockIdx.x * F + slot);
     float2 nx[G::P];
     if (f < batch) {
         const float2* src = reinterpret_cast<const float2*>(in + f * in_dist);
@@ -213,44 +134,58 @@ k_r2c(const float* in, float2* out, long long batch, long long in_dist, long lon
 #pragma unroll
             for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(src + t + r * G::T);
         }
-        fft_regs<M, true>(v, t, my, tw);
-#pragma unroll
-        for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
-        xsync<G::T>();
+        fft_regs<M, true, PAIR>(v, t, my, tw);
         float2* dst = out + f * out_dist;
+        if constexpr (PAIR) {
 #pragma unroll
-        for (int q = 0; q < G::P; ++q) {
-            const int k = t + G::T * q;
-            const float2 A = my[G::pad(k)];
-            if (k == 0) {
-                st_nt(make_float2(A.x + A.y, 0.0f), dst);
-                st_nt(make_float2(A.x - A.y, 0.0f), dst + M);
-            } else {
-                st_nt(split_fwd(A, cconj(my[G::pad(M - k)]), pw(k)), dst + k);
+            for (int q = 0; q < G::P; ++q) {
+                const int k = out_pos<M, true>(t, q);
+                const float2 A = v[q];
+                if (k == 0) {
+                    st_nt(make_float2(A.x + A.y, 0.0f), dst);
+                    st_nt(make_float2(A.x - A.y, 0.0f), dst + M);
+                } else {
+                    st_nt(split_fwd(A, cconj(mirror_of<M, true>(v, t, q)), pw(k)), dst + k);
+                }
             }
+        } else {
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
+            xsync<G::T>();
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                const int k = t + G::T * q;
+                const float2 A = my[G::pad(k)];
+                if (k == 0) {
+                    st_nt(make_float2(A.x + A.y, 0.0f), dst);
+                    st_nt(make_float2(A.x - A.y, 0.0f), dst + M);
+                } else {
+                    st_nt(split_fwd(A, cconj(my[G::pad(M - k)]), pw(k)), dst + k);
+                }
+            }
+            xsync<G::T>();
         }
-        xsync<G::T>();
     }
 }
 
 template <int M>
 __global__ void __launch_bounds__(Wg<M>::value)
 k_c2r(const float2* in, float* out, long long batch, long long in_dist, long long out_dist,
-      const float2* gtabM, const float2* gtab2M, float scale) {
+      const float2* gpass, const float2* gtabM, const float2* gtab2M, float scale) {
     using G = Geo<M>;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     __shared__ float2 lds[F * G::LDS];
     __shared__ float2 ltab[TwLayout<M>::ENTRIES];
     __shared__ float2 lpost[PostLayout<M>::ENTRIES];
-    stage_twiddles<M, WG>(ltab, gtabM);
+    stage_twiddles<M, WG>(ltab, gpass, gtabM);
     stage_post<M, WG>(lpost, gtab2M);
     __syncthreads();
-    const auto tw = twiddles_from<M>(ltab);
-    const auto pw = post_from<M>(lpost);
+    const TwTab<M> tw{ltab};
+    const PostTab<M> pw{lpost};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
     const long long stride = (long long)gridDim.x * F;
-    long long f = (long long)blockIdx.x * F + slot;
+    long long f = uni<G::T>((long long)blockIdx.x * F + slot);
     float2 nx[G::P];
     float2 nxm = make_float2(0.0f, 0.0f);
     if (f < batch) {
@@ -277,7 +212,7 @@ k_c2r(const float2* in, float* out, long long batch, long long in_dist, long lon
             const int k = t + r * G::T;
             float2 A = my[G::pad(k)];
             float2 B;
-            if (k == 0) {   // imag of DC and Nyquist ignored (fft_kiss.c:158-171 result)
+            if (k == 0) {   // imag of DC and Nyquist ignored (the fft_kiss.c:158-171 result)
                 A.y = 0.0f;
                 B = make_float2(xm.x, 0.0f);
             } else {
@@ -297,15 +232,16 @@ template <int M>
 static hipError_t run_r2c(const float* in, float2* out, long long batch, long long in_dist,
                           long long out_dist, hipStream_t s) {
     const float2* tM = twiddle_table(M);
+    const float2* pM = pass_twiddles(M);
     const float2* t2M = twiddle_table(2 * M);
-    if (!tM || !t2M) return hipErrorOutOfMemory;
+    if (!tM || !t2M || !pM) return hipErrorOutOfMemory;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     static int cap = 0;
     if (!cap) cap = persistent_grid((const void*)k_r2c<M>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < cap ? need : cap);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL(k_r2c<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, tM, t2M);
+    hipLaunchKernelGGL(k_r2c<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pM, tM, t2M);
     return hipGetLastError();
 }
 
@@ -313,15 +249,16 @@ template <int M>
 static hipError_t run_c2r(const float2* in, float* out, long long batch, long long in_dist,
                           long long out_dist, hipStream_t s) {
     const float2* tM = twiddle_table(M);
+    const float2* pM = pass_twiddles(M);
     const float2* t2M = twiddle_table(2 * M);
-    if (!tM || !t2M) return hipErrorOutOfMemory;
+    if (!tM || !t2M || !pM) return hipErrorOutOfMemory;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     static int cap = 0;
     if (!cap) cap = persistent_grid((const void*)k_c2r<M>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < cap ? need : cap);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL(k_c2r<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, tM, t2M,
+    hipLaunchKernelGGL(k_c2r<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pM, tM, t2M,
                        1.0f / (float)M);
     return hipGetLastError();
 }

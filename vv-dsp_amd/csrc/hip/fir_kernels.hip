@@ -43,31 +43,35 @@ __device__ __forceinline__ void ols_load(float2* nx, const float* xs, const floa
 }
 
 // LDS: exchange buffer + twiddles + split twiddles + H (M+1 complex).  The next
-// block's input is prefetched into registers during the current block.
+// block's input is prefetched into registers during the current block.  With a
+// mirror-paired forward FFT (M where Geo<M>::CAN_PAIR) each thread holds Z[k]
+// and Z[M-k], forms Y = X*H for both bins and the inverse split step in
+// registers, and one LDS scatter/gather re-orders Zi for the inverse FFT.
 template <int M>
 __global__ void __launch_bounds__(Wg<M>::value)
 k_fir_ols(long long taps, const float2* Hg, const float* x, float* y, long long n, long long nch,
           long long x_stride, long long y_stride, const float* prefix, long long nblk,
-          const float2* gtabM, const float2* gtab2M) {
+          const float2* gpass, const float2* gtabM, const float2* gtab2M) {
     using G = Geo<M>;
+    constexpr bool PAIR = G::CAN_PAIR;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     constexpr long long NR = 2 * M;
     __shared__ float2 lds[F * G::LDS];
     __shared__ float2 ltab[TwLayout<M>::ENTRIES];
     __shared__ float2 lpost[PostLayout<M>::ENTRIES];
     __shared__ float2 lH[M + 1];
-    stage_twiddles<M, WG>(ltab, gtabM);
+    stage_twiddles<M, WG>(ltab, gpass, gtabM);
     stage_post<M, WG>(lpost, gtab2M);
     for (int i = threadIdx.x; i <= M; i += WG) lH[i] = Hg[i];
     __syncthreads();
-    const auto tw = twiddles_from<M>(ltab);
-    const auto pw = post_from<M>(lpost);
+    const TwTab<M> tw{ltab};
+    const PostTab<M> pw{lpost};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
     const long long lm1 = taps - 1, lout = NR - lm1;
     const long long items = nch * nblk;
     const long long stride = (long long)gridDim.x * F;
-    long long it = (long long)blockIdx.x * F + slot;
+    long long it = uni<G::T>((long long)blockIdx.x * F + slot);
     float2 nx[G::P];
     if (it < items) {
         const long long c = it / nblk, j = it - c * nblk;
@@ -83,29 +87,55 @@ k_fir_ols(long long taps, const float2* Hg, const float* x, float* y, long long 
             const long long c2 = in_ / nblk, j2 = in_ - c2 * nblk;
             ols_load<M>(nx, x + c2 * x_stride, prefix ? prefix + c2 * lm1 : nullptr, j2 * lout - lm1, n, lm1, t);
         }
-        fft_regs<M, true>(v, t, my, tw);
+        fft_regs<M, true, PAIR>(v, t, my, tw);
+        if constexpr (PAIR) {
+            float2 zi[G::P];
 #pragma unroll
-        for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
-        xsync<G::T>();
-        // spectrum multiply + inverse split, bins k and M-k per thread
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) {
-            const int k = t + r * G::T;
-            const float2 A = my[G::pad(k)];
-            if (k == 0) {
-                const float y0 = (A.x + A.y) * lH[0].x;
-                const float ym = (A.x - A.y) * lH[M].x;
-                v[r] = make_float2((y0 + ym) * 0.5f, (y0 - ym) * 0.5f);
-            } else {
-                const float2 Bz = my[G::pad(M - k)];
-                const float2 W = pw(k);
-                const float2 Wm = make_float2(-W.x, W.y);       // W^(M-k) = -conj(W^k)
-                const float2 Yk = cmul(split_fwd(A, cconj(Bz), W), lH[k]);
-                const float2 Ym = cmul(split_fwd(Bz, cconj(A), Wm), lH[M - k]);
-                v[r] = split_inv(Yk, Ym, W);
+            for (int q = 0; q < G::P; ++q) {
+                const int k = out_pos<M, true>(t, q);
+                const float2 A = v[q];
+                if (k == 0) {
+                    const float y0 = (A.x + A.y) * lH[0].x;
+                    const float ym = (A.x - A.y) * lH[M].x;
+                    zi[q] = make_float2((y0 + ym) * 0.5f, (y0 - ym) * 0.5f);
+                } else {
+                    const float2 Bz = mirror_of<M, true>(v, t, q);
+                    const float2 W = pw(k);
+                    const float2 Wm = make_float2(-W.x, W.y);       // W^(M-k) = -conj(W^k)
+                    const float2 Yk = cmul(split_fwd(A, cconj(Bz), W), lH[k]);
+                    const float2 Ym = cmul(split_fwd(Bz, cconj(A), Wm), lH[M - k]);
+                    zi[q] = split_inv(Yk, Ym, W);
+                }
             }
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M, true>(t, q))] = zi[q];
+            xsync<G::T>();
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) v[r] = my[G::pad(t + r * G::T)];
+            xsync<G::T>();
+        } else {
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
+            xsync<G::T>();
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const int k = t + r * G::T;
+                const float2 A = my[G::pad(k)];
+                if (k == 0) {
+                    const float y0 = (A.x + A.y) * lH[0].x;
+                    const float ym = (A.x - A.y) * lH[M].x;
+                    v[r] = make_float2((y0 + ym) * 0.5f, (y0 - ym) * 0.5f);
+                } else {
+                    const float2 Bz = my[G::pad(M - k)];
+                    const float2 W = pw(k);
+                    const float2 Wm = make_float2(-W.x, W.y);
+                    const float2 Yk = cmul(split_fwd(A, cconj(Bz), W), lH[k]);
+                    const float2 Ym = cmul(split_fwd(Bz, cconj(A), Wm), lH[M - k]);
+                    v[r] = split_inv(Yk, Ym, W);
+                }
+            }
+            xsync<G::T>();
         }
-        xsync<G::T>();
         fft_regs<M, false>(v, t, my, tw);
         float* ys = y + c * y_stride;
         const long long ob = j * lout;
@@ -138,8 +168,9 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     if (lout <= 0) return hipErrorInvalidValue;
     const long long nblk = (n + lout - 1) / lout;
     const float2* tM = twiddle_table(M);
+    const float2* pM = pass_twiddles(M);
     const float2* t2M = twiddle_table(2 * M);
-    if (!tM || !t2M) return hipErrorOutOfMemory;
+    if (!tM || !t2M || !pM) return hipErrorOutOfMemory;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     static int cap = 0;
     if (!cap) cap = persistent_grid((const void*)k_fir_ols<M>, WG, 0, 1LL << 40);
@@ -147,7 +178,7 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     const int grid = (int)(need < cap ? need : cap);
     if (grid < 1) return hipSuccess;
     hipLaunchKernelGGL(k_fir_ols<M>, dim3(grid), dim3(WG), 0, s, taps, H, x, y, n, nch, x_stride, y_stride,
-                       prefix, nblk, tM, t2M);
+                       prefix, nblk, pM, tM, t2M);
     return hipGetLastError();
 }
 

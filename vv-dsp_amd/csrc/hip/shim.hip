@@ -12,6 +12,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -450,10 +451,18 @@ struct vvhip_fir {
 };
 
 static size_t fir_block(const vvhip_fir* f, size_t n) {
-    // smallest pow2 >= max(2*taps, 64); grown toward 8192 while the signal is longer
+    // smallest pow2 >= max(2*taps, 64); grown toward the preferred block (4096:
+    // M = 2048 runs the mirror-paired multiply, L2 re-read (L-1)/(4096-(L-1)))
+    // while the signal is longer.  VVHIP_FIR_BLOCK overrides the preferred size.
+    static size_t pref = 0;
+    if (!pref) {
+        const char* e = getenv("VVHIP_FIR_BLOCK");
+        pref = e ? (size_t)atol(e) : 4096;
+        if (pref < 64 || pref > 8192 || (pref & (pref - 1))) pref = 4096;
+    }
     size_t nr = 64;
     while (nr < 2 * f->taps) nr <<= 1;
-    while (nr < 8192 && nr < n + f->taps - 1) nr <<= 1;
+    while (nr < pref && nr < n + f->taps - 1) nr <<= 1;
     return nr;
 }
 

@@ -1,17 +1,25 @@
 // stft_kernels.hip -- fused STFT analysis for gfx950.
 //
-// One persistent kernel per power-of-two nfft (= 2M): for every (channel,
-// frame) it gathers the frame (zero past the end of the signal, as
-// stft.c:124-130), applies the window (vectorized_math_fallback.c:13-29), runs
-// the real FFT as an M-point complex Stockham FFT in VGPRs/LDS plus the split
-// step, and writes either magnitudes sqrtf(re^2+im^2) for all nfft bins
-// (stft.c:133-139) or the full complex spectrum (stft_process semantics,
-// stft.c:74-92) using X[nfft-k] = conj(X[k]).
+// For every (channel, frame) of the reference's spectrogram (stft.c:112-144):
+// gather the frame (zero past the end of the signal, stft.c:124-130), apply the
+// window (vectorized_math_fallback.c:13-29), FFT, and write either magnitudes
+// sqrtf(re^2+im^2) for all nfft bins (stft.c:133-139) or the full complex
+// spectrum (stft_process semantics, stft.c:74-92).
 //
-// Memory behaviour: the next frame's samples are prefetched into registers
-// while the current frame is transformed; window and twiddles live in LDS, so
-// the only VMEM traffic is the streamed signal (re-reads of the nfft-hop
-// overlap hit L2) and the output rows.
+// k_stft_pair<N>: TWO real frames a, b share one complex N-point FFT of
+// z = w*a + i*w*b.  With the mirror-paired last pass each thread holds Z[k]
+// and Z[N-k], so Xa[k] = (Z[k] + conj Z[N-k])/2 and Xb[k] = (Z[k] - conj Z[N-k])/2i
+// come straight from registers -- no split twiddles, no LDS post pass -- and
+// every bin 0..N-1 of both rows is produced in place (Hermitian symmetry is
+// automatic).  Used when Geo<N>::CAN_PAIR.
+// k_stft_half<M>: one frame per M = nfft/2 point complex FFT plus the real
+// split step (nfft = 256 and 4096, where N cannot be mirror-paired).
+//
+// Scheduling: each persistent slot walks a CONTIGUOUS chunk of frame pairs,
+// so the nfft-hop overlap of consecutive frames is re-read from L1/L2 of the
+// same CU, never from HBM by another XCD; the next pair's samples are
+// prefetched into registers while the current pair is transformed; window
+// values are per-thread constants in registers; twiddles live in LDS.
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
 
@@ -19,83 +27,184 @@
 
 namespace vvh {
 
-template <int M>
-__device__ __forceinline__ void stft_load(float2* nx, const float* s, long long start, long long n, int t) {
-    using G = Geo<M>;
-    constexpr int NR = 2 * M;
-    const float* base = s + start;
-    if (start + NR <= n && ((reinterpret_cast<uintptr_t>(base) & 7) == 0)) {
-        const float2* b2 = reinterpret_cast<const float2*>(base);
+// samples e = t + r*T of one frame (zero outside [0, n); all zero when !valid).
+// `s` must point at a real channel.  The tail path clamps the index and selects
+// instead of branching per element, so the loads stay branch-free.
+template <int N>
+__device__ __forceinline__ void frame_load(float* x, const float* s, long long start, long long n, int t,
+                                           bool valid) {
+    using G = Geo<N>;
+    if (start + N <= n) {
 #pragma unroll
-        for (int r = 0; r < G::P; ++r) nx[r] = b2[t + r * G::T];
+        for (int r = 0; r < G::P; ++r) x[r] = s[start + t + r * G::T];
     } else {
 #pragma unroll
         for (int r = 0; r < G::P; ++r) {
-            const long long e = 2 * (t + r * G::T);
-            nx[r] = make_float2((start + e < n) ? base[e] : 0.0f, (start + e + 1 < n) ? base[e + 1] : 0.0f);
+            const long long e = start + t + r * G::T;
+            const float val = s[e < n ? e : n - 1];
+            x[r] = e < n ? val : 0.0f;
+        }
+    }
+    if (!valid) {
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) x[r] = 0.0f;
+    }
+}
+
+// contiguous chunk [lo, hi) of `total` work items for persistent slot g of S
+__device__ __forceinline__ void chunk_of(long long total, long long g, long long S, long long* lo,
+                                         long long* hi) {
+    const long long per = total / S, rem = total % S;
+    *lo = g * per + (g < rem ? g : rem);
+    *hi = *lo + per + (g < rem ? 1 : 0);
+}
+
+template <int N, int MODE>
+__global__ void __launch_bounds__(Wg<N>::value)
+k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
+            long long hop, const float* win, void* out, long long out_ch_stride, const float2* gpass,
+            const float2* gtab) {
+    using G = Geo<N>;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
+    __shared__ float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    float w[G::P];
+#pragma unroll
+    for (int r = 0; r < G::P; ++r) w[r] = win[t + r * G::T];
+
+    // pairs never span channels (frames 2j, 2j+1 of one channel), so a
+    // channel's rows do not depend on how channels are grouped into calls/shards
+    const long long ppc = (frames + 1) / 2;
+    const long long pairs = nch * ppc;
+    long long p, p_end;
+    chunk_of(pairs, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &p, &p_end);
+    p = uni<G::T>(p);
+    p_end = uni<G::T>(p_end);
+    float xa[G::P], xb[G::P];
+    // pair q -> both frames' samples
+    auto load_pair = [&](long long q) {
+        const long long c = q / ppc, fa = 2 * (q - c * ppc);
+        const float* s = sig + c * ch_stride;
+        frame_load<N>(xa, s, fa * hop, n, t, true);
+        frame_load<N>(xb, s, (fa + 1 < frames ? fa + 1 : fa) * hop, n, t, fa + 1 < frames);
+    };
+    if (p < p_end) load_pair(p);
+    for (; p < p_end; ++p) {
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
+        if (p + 1 < p_end) load_pair(p + 1);
+        fft_regs<N, true, true>(v, t, my, tw);
+        const long long c = p / ppc, fa = 2 * (p - c * ppc);
+        const long long rowa = c * out_ch_stride + fa * (long long)N;
+        const long long rowb = rowa + N;
+        const bool has_b = fa + 1 < frames;
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int k = out_pos<N, true>(t, q);
+            const float2 Z = v[q];
+            const float2 Zm = mirror_of<N, true>(v, t, q);   // Z[N-k]
+            // 2*Xa = Z + conj(Zm) ; 2*Xb = -i (Z - conj(Zm))
+            const float ar = Z.x + Zm.x, ai = Z.y - Zm.y;
+            const float br = Z.y + Zm.y, bi = Zm.x - Z.x;
+            if (MODE == 0) {
+                float* o = reinterpret_cast<float*>(out);
+                __builtin_nontemporal_store(0.5f * sqrtf(ar * ar + ai * ai), o + rowa + k);
+                if (has_b) __builtin_nontemporal_store(0.5f * sqrtf(br * br + bi * bi), o + rowb + k);
+            } else {
+                float2* o = reinterpret_cast<float2*>(out);
+                st_nt(make_float2(0.5f * ar, 0.5f * ai), o + rowa + k);
+                if (has_b) st_nt(make_float2(0.5f * br, 0.5f * bi), o + rowb + k);
+            }
         }
     }
 }
 
-// MODE 0: out = float mags [ch][frame][2M]; MODE 1: out = float2 spectrum [ch][frame][2M]
 template <int M, int MODE>
 __global__ void __launch_bounds__(Wg<M>::value)
-k_stft(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
-       long long hop, const float* win, void* out, long long out_ch_stride, const float2* gtabM,
-       const float2* gtab2M) {
+k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
+            long long hop, const float* win, void* out, long long out_ch_stride, const float2* gpass,
+            const float2* gtabM, const float2* gtab2M) {
     using G = Geo<M>;
+    constexpr bool PAIR = G::CAN_PAIR;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     constexpr int NR = 2 * M;
     __shared__ float2 lds[F * G::LDS];
     __shared__ float2 ltab[TwLayout<M>::ENTRIES];
     __shared__ float2 lpost[PostLayout<M>::ENTRIES];
-    __shared__ float2 lwin[M];
-    stage_twiddles<M, WG>(ltab, gtabM);
+    stage_twiddles<M, WG>(ltab, gpass, gtabM);
     stage_post<M, WG>(lpost, gtab2M);
-    for (int i = threadIdx.x; i < M; i += WG) lwin[i] = make_float2(win[2 * i], win[2 * i + 1]);
     __syncthreads();
-    const auto tw = twiddles_from<M>(ltab);
-    const auto pw = post_from<M>(lpost);
+    const TwTab<M> tw{ltab};
+    const PostTab<M> pw{lpost};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
+    float2 w[G::P];
+#pragma unroll
+    for (int r = 0; r < G::P; ++r) w[r] = make_float2(win[2 * (t + r * G::T)], win[2 * (t + r * G::T) + 1]);
     const long long items = nch * frames;
-    const long long stride = (long long)gridDim.x * F;
-    long long it = (long long)blockIdx.x * F + slot;
+    long long it, it_end;
+    chunk_of(items, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &it, &it_end);
+    it = uni<G::T>(it);
+    it_end = uni<G::T>(it_end);
     float2 nx[G::P];
-    if (it < items) {
-        const long long c = it / frames, fr = it - c * frames;
-        stft_load<M>(nx, sig + c * ch_stride, fr * hop, n, t);
-    }
-    for (; it < items; it += stride) {
+    auto load = [&](long long i2) {
+        const long long c = i2 / frames, fr = i2 - c * frames;
+        const float* s = sig + c * ch_stride;
+        const long long start = fr * hop;
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            const long long e = start + 2 * (t + r * G::T);
+            nx[r] = make_float2(e < n ? s[e] : 0.0f, e + 1 < n ? s[e + 1] : 0.0f);
+        }
+    };
+    if (it < it_end) load(it);
+    for (; it < it_end; ++it) {
         const long long c = it / frames, fr = it - c * frames;
         float2 v[G::P];
 #pragma unroll
-        for (int r = 0; r < G::P; ++r) {
-            const float2 w = lwin[t + r * G::T];
-            v[r] = make_float2(nx[r].x * w.x, nx[r].y * w.y);
-        }
-        const long long in_ = it + stride;
-        if (in_ < items) {
-            const long long c2 = in_ / frames, fr2 = in_ - c2 * frames;
-            stft_load<M>(nx, sig + c2 * ch_stride, fr2 * hop, n, t);
-        }
-        fft_regs<M, true>(v, t, my, tw);
-#pragma unroll
-        for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
-        xsync<G::T>();
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(nx[r].x * w[r].x, nx[r].y * w[r].y);
+        if (it + 1 < it_end) load(it + 1);
+        fft_regs<M, true, PAIR>(v, t, my, tw);
         const long long row = c * out_ch_stride + fr * (long long)NR;
+        float2 A[G::P], B[G::P];
+        int K[G::P];
+        if constexpr (PAIR) {
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                K[q] = out_pos<M, true>(t, q);
+                A[q] = v[q];
+                B[q] = mirror_of<M, true>(v, t, q);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
+            xsync<G::T>();
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                K[q] = t + G::T * q;
+                A[q] = my[G::pad(K[q])];
+                B[q] = my[G::pad((M - K[q]) & (M - 1))];
+            }
+            xsync<G::T>();
+        }
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
-            const int k = t + G::T * q;
-            const float2 A = my[G::pad(k)];
+            const int k = K[q];
             if (MODE == 0) {
                 float* o = reinterpret_cast<float*>(out) + row;
                 if (k == 0) {
-                    const float x0 = A.x + A.y, xm = A.x - A.y;
+                    const float x0 = A[q].x + A[q].y, xm = A[q].x - A[q].y;
                     __builtin_nontemporal_store(sqrtf(x0 * x0), o);
                     __builtin_nontemporal_store(sqrtf(xm * xm), o + M);
                 } else {
-                    const float2 X = split_fwd(A, cconj(my[G::pad(M - k)]), pw(k));
+                    const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
                     const float mag = sqrtf(X.x * X.x + X.y * X.y);
                     __builtin_nontemporal_store(mag, o + k);
                     __builtin_nontemporal_store(mag, o + (NR - k));
@@ -103,58 +212,74 @@ k_stft(const float* sig, long long n, long long nch, long long ch_stride, long l
             } else {
                 float2* o = reinterpret_cast<float2*>(out) + row;
                 if (k == 0) {
-                    st_nt(make_float2(A.x + A.y, 0.0f), o);
-                    st_nt(make_float2(A.x - A.y, 0.0f), o + M);
+                    st_nt(make_float2(A[q].x + A[q].y, 0.0f), o);
+                    st_nt(make_float2(A[q].x - A[q].y, 0.0f), o + M);
                 } else {
-                    const float2 X = split_fwd(A, cconj(my[G::pad(M - k)]), pw(k));
+                    const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
                     st_nt(X, o + k);
                     st_nt(cconj(X), o + (NR - k));
                 }
             }
         }
-        xsync<G::T>();
     }
 }
 
-template <int M, int MODE>
+template <int N, int MODE>
 static hipError_t run_stft(const float* sig, long long n, long long nch, long long ch_stride,
                            long long frames, long long hop, const float* win, void* out,
                            long long out_ch_stride, hipStream_t s) {
-    const float2* tM = twiddle_table(M);
-    const float2* t2M = twiddle_table(2 * M);
-    if (!tM || !t2M) return hipErrorOutOfMemory;
-    constexpr int WG = Wg<M>::value, F = Wg<M>::F;
-    static int cap = 0;
-    if (!cap) cap = persistent_grid((const void*)k_stft<M, MODE>, WG, 0, 1LL << 40);
-    const long long need = (nch * frames + F - 1) / F;
-    const int grid = (int)(need < cap ? need : cap);
-    if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_stft<M, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
-                       hop, win, out, out_ch_stride, tM, t2M);
+    const long long items = nch * frames;
+    if constexpr (Geo<N>::CAN_PAIR) {
+        const float2* tN = twiddle_table(N);
+        const float2* pN = pass_twiddles(N);
+        if (!tN || !pN) return hipErrorOutOfMemory;
+        constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+        static int cap = 0;
+        if (!cap) cap = persistent_grid((const void*)k_stft_pair<N, MODE>, WG, 0, 1LL << 40);
+        const long long need = (nch * ((frames + 1) / 2) + F - 1) / F;
+        const int grid = (int)(need < cap ? need : cap);
+        if (grid < 1) return hipSuccess;
+        hipLaunchKernelGGL((k_stft_pair<N, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
+                           hop, win, out, out_ch_stride, pN, tN);
+    } else {
+        constexpr int M = N / 2;
+        const float2* tM = twiddle_table(M);
+        const float2* pM = pass_twiddles(M);
+        const float2* t2M = twiddle_table(N);
+        if (!tM || !pM || !t2M) return hipErrorOutOfMemory;
+        constexpr int WG = Wg<M>::value, F = Wg<M>::F;
+        static int cap = 0;
+        if (!cap) cap = persistent_grid((const void*)k_stft_half<M, MODE>, WG, 0, 1LL << 40);
+        const long long need = (items + F - 1) / F;
+        const int grid = (int)(need < cap ? need : cap);
+        if (grid < 1) return hipSuccess;
+        hipLaunchKernelGGL((k_stft_half<M, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
+                           hop, win, out, out_ch_stride, pM, tM, t2M);
+    }
     return hipGetLastError();
 }
 
 bool stft_fused_supported(long long nfft) {
-    return nfft >= 4 && nfft <= 8192 && (nfft & (nfft - 1)) == 0;
+    return nfft >= 2 && nfft <= 8192 && (nfft & (nfft - 1)) == 0;
 }
 
 hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,
                        long long nch, long long ch_stride, long long frames, const float* win,
                        void* out, long long out_ch_stride, hipStream_t s) {
-#define CALL(MM)                                                                                   \
-    (mode == 0 ? run_stft<MM, 0>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s)   \
-               : run_stft<MM, 1>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s))
-    switch (nfft / 2) {
-        case 2: return CALL(2); case 4: return CALL(4); case 8: return CALL(8);
-        case 16: return CALL(16); case 32: return CALL(32); case 64: return CALL(64);
-        case 128: return CALL(128); case 256: return CALL(256); case 512: return CALL(512);
-        case 1024: return CALL(1024); case 2048: return CALL(2048); case 4096: return CALL(4096);
+#define CALL(NN)                                                                                   \
+    (mode == 0 ? run_stft<NN, 0>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s)   \
+               : run_stft<NN, 1>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s))
+    switch (nfft) {
+        case 2: return CALL(2); case 4: return CALL(4); case 8: return CALL(8); case 16: return CALL(16);
+        case 32: return CALL(32); case 64: return CALL(64); case 128: return CALL(128);
+        case 256: return CALL(256); case 512: return CALL(512); case 1024: return CALL(1024);
+        case 2048: return CALL(2048); case 4096: return CALL(4096); case 8192: return CALL(8192);
         default: return hipErrorInvalidValue;
     }
 #undef CALL
 }
 
-// stft_process over explicit frames [count][nfft] (no overlap): same kernel, hop = nfft.
+// stft_process over explicit frames [count][nfft] (no overlap): same kernels, hop = nfft.
 hipError_t launch_stft_frames(long long nfft, const float* frames_in, const float* win, float2* out,
                               long long count, hipStream_t s) {
     return launch_stft(nfft, nfft, 1, frames_in, nfft * count, 1, 0, count, win, out, 0, s);

@@ -1,0 +1,125 @@
+// tables.hip -- device-resident twiddle tables (computed in double on the
+// host, rounded once to f32) and persistent-grid sizing.  Tables are cached per
+// (device, kind, n) for the process lifetime; kernels stage them into LDS.
+#include "fft_core.hpp"
+#include "vvhip_internal.hpp"
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+namespace vvh {
+
+namespace {
+std::mutex g_mu;
+std::map<std::tuple<int, int, long long>, void*> g_cache;   // (device, kind, n) -> device buffer
+
+enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2 };
+
+int current_device() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return dev;
+}
+
+// exp(-2*pi*i*num/den) in double, reduced exactly (num mod den) first
+void wn(long long num, long long den, double* c, double* s) {
+    const long long m = ((num % den) + den) % den;
+    const double a = -2.0 * M_PI * (double)m / (double)den;
+    *c = std::cos(a);
+    *s = std::sin(a);
+}
+
+template <class Fill>
+void* cached(Kind kind, long long n, size_t bytes, Fill fill) {
+    const auto key = std::make_tuple(current_device(), (int)kind, n);
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(key);
+    if (it != g_cache.end()) return it->second;
+    std::vector<unsigned char> h(bytes);
+    fill(h.data());
+    void* d = nullptr;
+    if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    g_cache[key] = d;
+    return d;
+}
+
+// Host mirror of Geo<N>::radix / ns (fft_core.hpp) for runtime N.
+int radix_of(int n, int p) {
+    const int lg = ilog2(n);
+    if (n < 16) return n;
+    return (lg - 4 * p) >= 4 ? 16 : (1 << (lg - 4 * p));
+}
+int npass_of(int n) { return n >= 16 ? (ilog2(n) + 3) / 4 : 1; }
+}  // namespace
+
+const float2* twiddle_table(int n) {
+    return (const float2*)cached(KIND_WN, n, sizeof(float2) * n, [n](unsigned char* b) {
+        float2* h = reinterpret_cast<float2*>(b);
+        for (int k = 0; k < n; ++k) {
+            double c, s;
+            wn(k, n, &c, &s);
+            h[k] = make_float2((float)c, (float)s);
+        }
+    });
+}
+
+const double2* twiddle_table_d(long long n) {
+    return (const double2*)cached(KIND_WN_D, n, sizeof(double2) * n, [n](unsigned char* b) {
+        double2* h = reinterpret_cast<double2*>(b);
+        for (long long k = 0; k < n; ++k) {
+            double c, s;
+            wn(k, n, &c, &s);
+            h[k] = make_double2(c, s);
+        }
+    });
+}
+
+// Pass-major inter-pass twiddles of a length-n Stockham FFT (fft_core.hpp):
+// for pass p >= 1 (radix R, stride Ns), entry (r-1)*Ns + j = W_{Ns*R}^{j*r}.
+const float2* pass_twiddles(int n) {
+    long long entries = 0;
+    for (int p = 1, ns = radix_of(n, 0); p < npass_of(n); ns *= radix_of(n, p), ++p)
+        entries += (long long)(radix_of(n, p) - 1) * ns;
+    if (entries == 0) entries = 1;
+    return (const float2*)cached(KIND_PASS, n, sizeof(float2) * entries, [n](unsigned char* b) {
+        float2* h = reinterpret_cast<float2*>(b);
+        h[0] = make_float2(1.0f, 0.0f);
+        long long o = 0;
+        for (int p = 1, ns = radix_of(n, 0); p < npass_of(n); ns *= radix_of(n, p), ++p) {
+            const int R = radix_of(n, p);
+            for (int r = 1; r < R; ++r)
+                for (int j = 0; j < ns; ++j) {
+                    double c, s;
+                    wn((long long)j * r, (long long)ns * R, &c, &s);
+                    h[o + (long long)(r - 1) * ns + j] = make_float2((float)c, (float)s);
+                }
+            o += (long long)(R - 1) * ns;
+        }
+    });
+}
+
+int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = current_device();
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 1;
+    long long g = (long long)cus * per_cu;
+    if (work_blocks < g) g = work_blocks;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace vvh

@@ -10,6 +10,9 @@ namespace vvh {
 // Device-resident W_N^k = exp(-2*pi*i*k/N) table, k < N, f32 rounded from double.
 // Cached per N for the process lifetime (per device).
 const float2* twiddle_table(int n);
+const double2* twiddle_table_d(long long n);
+// Pass-major inter-pass twiddles of the length-n Stockham FFT (fft_core.hpp TwTab).
+const float2* pass_twiddles(int n);
 
 // Persistent-grid sizing: resident blocks for `kernel` x CUs, capped by work.
 int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks);
