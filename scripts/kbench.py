@@ -69,7 +69,21 @@ def case_copy(nbytes):
     return (lambda: b.copy_(a)), 2 * nbytes, (a, b)
 
 
+def case_wr(mode, nt, rows=3600000, blocks=2048):
+    """store-pattern microbenchmark (scripts/membench.hip): rows x 4 KB"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libmembench.so"))
+    lib.membench_write.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_void_p]
+    out = torch.empty(rows, 1024, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    return (lambda: lib.membench_write(out.data_ptr(), rows, mode, nt, blocks, s)), rows * 4096, (out, lib)
+
+
 CASES = {
+    "wr4": lambda: case_wr(0, 0), "wr4nt": lambda: case_wr(0, 1),
+    "wrpat": lambda: case_wr(1, 0), "wrpatnt": lambda: case_wr(1, 1),
+    "wr8nt": lambda: case_wr(2, 1), "wr16": lambda: case_wr(3, 0), "wr16nt": lambda: case_wr(3, 1),
     "copy1G": lambda: case_copy(1 << 29),
     "c2c1024": lambda: case_c2c(1024, 65536),
     "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),
@@ -88,7 +102,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cases", default=",".join(CASES))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith("wr")))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

@@ -142,10 +142,10 @@ k_r2c(const float* in, float2* out, long long batch, long long in_dist, long lon
                 const int k = out_pos<M, true>(t, q);
                 const float2 A = v[q];
                 if (k == 0) {
-                    st_nt(make_float2(A.x + A.y, 0.0f), dst);
-                    st_nt(make_float2(A.x - A.y, 0.0f), dst + M);
+                    *(dst) = make_float2(A.x + A.y, 0.0f);
+                    *(dst + M) = make_float2(A.x - A.y, 0.0f);
                 } else {
-                    st_nt(split_fwd(A, cconj(mirror_of<M, true>(v, t, q)), pw(k)), dst + k);
+                    *(dst + k) = split_fwd(A, cconj(mirror_of<M, true>(v, t, q)), pw(k));
                 }
             }
         } else {
@@ -157,10 +157,10 @@ k_r2c(const float* in, float2* out, long long batch, long long in_dist, long lon
                 const int k = t + G::T * q;
                 const float2 A = my[G::pad(k)];
                 if (k == 0) {
-                    st_nt(make_float2(A.x + A.y, 0.0f), dst);
-                    st_nt(make_float2(A.x - A.y, 0.0f), dst + M);
+                    *(dst) = make_float2(A.x + A.y, 0.0f);
+                    *(dst + M) = make_float2(A.x - A.y, 0.0f);
                 } else {
-                    st_nt(split_fwd(A, cconj(my[G::pad(M - k)]), pw(k)), dst + k);
+                    *(dst + k) = split_fwd(A, cconj(my[G::pad(M - k)]), pw(k));
                 }
             }
             xsync<G::T>();

@@ -144,16 +144,16 @@ k_fir_ols(long long taps, const float2* Hg, const float* x, float* y, long long 
             for (int q = 0; q < G::P; ++q) {
                 const long long o0 = 2LL * out_pos<M>(t, q) - lm1;
                 const long long g = ob + o0;
-                if (o0 >= 0 && g + 1 < n) st_nt(v[q], reinterpret_cast<float2*>(ys + g));
-                else if (o0 >= 0 && g < n) __builtin_nontemporal_store(v[q].x, ys + g);
+                if (o0 >= 0 && g + 1 < n) *(reinterpret_cast<float2*>(ys + g)) = v[q];
+                else if (o0 >= 0 && g < n) *(ys + g) = v[q].x;
             }
         } else {
 #pragma unroll
             for (int q = 0; q < G::P; ++q) {
                 const long long o0 = 2LL * out_pos<M>(t, q) - lm1;
                 const long long g = ob + o0;
-                if (o0 >= 0 && g < n) __builtin_nontemporal_store(v[q].x, ys + g);
-                if (o0 + 1 >= 0 && g + 1 < n) __builtin_nontemporal_store(v[q].y, ys + g + 1);
+                if (o0 >= 0 && g < n) *(ys + g) = v[q].x;
+                if (o0 + 1 >= 0 && g + 1 < n) *(ys + g + 1) = v[q].y;
             }
         }
         xsync<G::T>();

@@ -59,13 +59,54 @@ __device__ __forceinline__ void chunk_of(long long total, long long g, long long
     *hi = *lo + per + (g < rem ? 1 : 0);
 }
 
-template <int N, int MODE>
+// |re + i im| with the hardware v_sqrt_f32 (<=1 ulp).  sqrtf's correctly
+// rounded IEEE expansion costs ~10 VALU per bin; the magnitude is compared at
+// the reference's float tolerance, never bit-exactly.
+__device__ __forceinline__ float cmag(float re, float im) {
+    return __builtin_amdgcn_sqrtf(__builtin_fmaf(re, re, im * im));
+}
+
+// Spectra of the two frames at bin k from Z = FFT(w/2 * (a + i b)):
+//   Xa[k] = Z[k] + conj Z[N-k],  Xb[k] = -i (Z[k] - conj Z[N-k]).
+// The 1/2 rides in the window (a power-of-two scale commutes with every
+// rounding, so this is bit-identical to halving at the end).  Packed f32 math.
+// MODE 0: A.x = |Xa[k]|, B.x = |Xb[k]|;  MODE 1: A = Xa[k], B = Xb[k].
+template <int MODE>
+__device__ __forceinline__ void pair_post(float2 Z, float2 Zm, float2* A, float2* B) {
+    const vf2_t z = {Z.x, Z.y}, zm = {Zm.x, Zm.y};
+    const vf2_t s = z + zm;   // (Re Xa, Re Xb)
+    const vf2_t d = z - zm;   // (-Im Xb, Im Xa)
+    if constexpr (MODE == 0) {
+        const vf2_t dd = d * d;
+        const vf2_t m2 = s * s + dd.yx;   // (|Xa|^2, |Xb|^2)
+        A->x = __builtin_amdgcn_sqrtf(m2.x);
+        B->x = __builtin_amdgcn_sqrtf(m2.y);
+        A->y = B->y = 0.0f;
+    } else {
+        *A = make_float2(s.x, d.y);
+        *B = make_float2(s.y, -d.x);
+    }
+}
+
+// bin k of an output row (MODE 0: float magnitudes, MODE 1: float2 spectrum)
+template <int MODE>
+__device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
+    if constexpr (MODE == 0) *(reinterpret_cast<float*>(row) + k) = X.x;
+    else *(reinterpret_cast<float2*>(row) + k) = X;
+}
+
+// Frame pairs (2j, 2j+1) of one channel, j in [pair0, pair0 + ppc): pairs never
+// span channels, so a channel's rows do not depend on how channels are grouped
+// into calls or shards.  !TAIL: both frames lie inside the signal (the bulk);
+// TAIL: the last few pairs, zero-padded past the end / odd last frame.
+template <int N, int MODE, bool TAIL>
 __global__ void __launch_bounds__(Wg<N>::value)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
-            long long hop, const float* win, void* out, long long out_ch_stride, const float2* gpass,
-            const float2* gtab) {
+            long long hop, long long pair0, long long ppc, const float* win, void* out,
+            long long out_ch_stride, const float2* gpass, const float2* gtab) {
     using G = Geo<N>;
-    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    using Mi = Mirror<N>;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
     __shared__ float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
@@ -76,53 +117,95 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
     float w[G::P];
 #pragma unroll
-    for (int r = 0; r < G::P; ++r) w[r] = win[t + r * G::T];
+    for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * G::T];
 
-    // pairs never span channels (frames 2j, 2j+1 of one channel), so a
-    // channel's rows do not depend on how channels are grouped into calls/shards
-    const long long ppc = (frames + 1) / 2;
     const long long pairs = nch * ppc;
     long long p, p_end;
     chunk_of(pairs, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &p, &p_end);
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
+    if (p >= p_end) return;   // uniform per transform (F == 1 whenever T > 64)
+    // (channel, first frame) of the current pair, advanced without divisions;
+    // this launch covers frames [f_lo, f_hi) of every channel
+    const long long f_lo = 2 * pair0, f_hi = 2 * (pair0 + ppc);
+    long long c = p / ppc, fa = f_lo + 2 * (p - c * ppc);
     float xa[G::P], xb[G::P];
-    // pair q -> both frames' samples
-    auto load_pair = [&](long long q) {
-        const long long c = q / ppc, fa = 2 * (q - c * ppc);
-        const float* s = sig + c * ch_stride;
-        frame_load<N>(xa, s, fa * hop, n, t, true);
-        frame_load<N>(xb, s, (fa + 1 < frames ? fa + 1 : fa) * hop, n, t, fa + 1 < frames);
+    auto load_pair = [&](long long cc, long long ff) {
+        if constexpr (TAIL) {
+            const float* s = sig + cc * ch_stride;
+            frame_load<N>(xa, s, ff * hop, n, t, true);
+            frame_load<N>(xb, s, (ff + 1 < frames ? ff + 1 : ff) * hop, n, t, ff + 1 < frames);
+        } else {   // both frames lie inside the signal: wave-uniform bases, plain loads
+            const float* sa = sig + cc * ch_stride + ff * hop;
+            const float* sb = sa + hop;
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = sa[t + r * G::T];
+                xb[r] = sb[t + r * G::T];
+            }
+        }
     };
-    if (p < p_end) load_pair(p);
+    load_pair(c, fa);
+    int kb[G::NPT];   // last-pass butterfly of each slot (loop invariant)
+#pragma unroll
+    for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
+    constexpr long long ES = MODE == 0 ? 4 : 8;
     for (; p < p_end; ++p) {
         float2 v[G::P];
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
-        if (p + 1 < p_end) load_pair(p + 1);
+        long long cn = c, fn = fa + 2;
+        if (fn >= f_hi) {
+            fn = f_lo;
+            ++cn;
+        }
+        const bool more = p + 1 < p_end;
+        if constexpr (TAIL) {
+            if (more) load_pair(cn, fn);
+        } else {
+            load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
+        }
         fft_regs<N, true, true>(v, t, my, tw);
-        const long long c = p / ppc, fa = 2 * (p - c * ppc);
-        const long long rowa = c * out_ch_stride + fa * (long long)N;
-        const long long rowb = rowa + N;
-        const bool has_b = fa + 1 < frames;
+        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * (long long)N) * ES;
+        char* rowb = rowa + N * ES;
+        const bool has_b = TAIL ? fa + 1 < frames : true;
+        if constexpr (G::T == 1) {
 #pragma unroll
-        for (int q = 0; q < G::P; ++q) {
-            const int k = out_pos<N, true>(t, q);
-            const float2 Z = v[q];
-            const float2 Zm = mirror_of<N, true>(v, t, q);   // Z[N-k]
-            // 2*Xa = Z + conj(Zm) ; 2*Xb = -i (Z - conj(Zm))
-            const float ar = Z.x + Zm.x, ai = Z.y - Zm.y;
-            const float br = Z.y + Zm.y, bi = Zm.x - Z.x;
-            if (MODE == 0) {
-                float* o = reinterpret_cast<float*>(out);
-                __builtin_nontemporal_store(0.5f * sqrtf(ar * ar + ai * ai), o + rowa + k);
-                if (has_b) __builtin_nontemporal_store(0.5f * sqrtf(br * br + bi * bi), o + rowb + k);
-            } else {
-                float2* o = reinterpret_cast<float2*>(out);
-                st_nt(make_float2(0.5f * ar, 0.5f * ai), o + rowa + k);
-                if (has_b) st_nt(make_float2(0.5f * br, 0.5f * bi), o + rowb + k);
+            for (int q = 0; q < G::P; ++q) {
+                float2 A, B;
+                pair_post<MODE>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                put_bin<MODE>(rowa, q, A);
+                if (has_b) put_bin<MODE>(rowb, q, B);
+            }
+        } else {
+            // even slots hold bins k, their partner slots hold N-k: one post
+            // per (k, N-k) pair, stored at both (real input -> mirror = conj)
+#pragma unroll
+            for (int i = 0; i < G::NPT; i += 2) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int q = i * R + r, qm = Mi::normal(q);
+                    float2 A, B;
+                    pair_post<MODE>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                    float2 Am = MODE == 0 ? A : cconj(A), Bm = MODE == 0 ? B : cconj(B);
+                    if (i == 0) {   // thread 0: slot 1 is butterfly NB/2, its own mirror
+                        float2 A2, B2;
+                        pair_post<MODE>(v[qm], v[Mi::special(qm)], &A2, &B2);
+                        Am = select2(t == 0, A2, Am);
+                        Bm = select2(t == 0, B2, Bm);
+                    }
+                    const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
+                    put_bin<MODE>(rowa, k, A);
+                    put_bin<MODE>(rowa, km, Am);
+                    if (has_b) {
+                        put_bin<MODE>(rowb, k, B);
+                        put_bin<MODE>(rowb, km, Bm);
+                    }
+                }
             }
         }
+        c = cn;
+        fa = fn;
     }
 }
 
@@ -201,23 +284,23 @@ k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, l
                 float* o = reinterpret_cast<float*>(out) + row;
                 if (k == 0) {
                     const float x0 = A[q].x + A[q].y, xm = A[q].x - A[q].y;
-                    __builtin_nontemporal_store(sqrtf(x0 * x0), o);
-                    __builtin_nontemporal_store(sqrtf(xm * xm), o + M);
+                    *(o) = fabsf(x0);
+                    *(o + M) = fabsf(xm);
                 } else {
                     const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
-                    const float mag = sqrtf(X.x * X.x + X.y * X.y);
-                    __builtin_nontemporal_store(mag, o + k);
-                    __builtin_nontemporal_store(mag, o + (NR - k));
+                    const float mag = cmag(X.x, X.y);
+                    *(o + k) = mag;
+                    *(o + (NR - k)) = mag;
                 }
             } else {
                 float2* o = reinterpret_cast<float2*>(out) + row;
                 if (k == 0) {
-                    st_nt(make_float2(A[q].x + A[q].y, 0.0f), o);
-                    st_nt(make_float2(A[q].x - A[q].y, 0.0f), o + M);
+                    *(o) = make_float2(A[q].x + A[q].y, 0.0f);
+                    *(o + M) = make_float2(A[q].x - A[q].y, 0.0f);
                 } else {
                     const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
-                    st_nt(X, o + k);
-                    st_nt(cconj(X), o + (NR - k));
+                    *(o + k) = X;
+                    *(o + (NR - k)) = cconj(X);
                 }
             }
         }
@@ -234,13 +317,27 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const float2* pN = pass_twiddles(N);
         if (!tN || !pN) return hipErrorOutOfMemory;
         constexpr int WG = Wg<N>::value, F = Wg<N>::F;
-        static int cap = 0;
-        if (!cap) cap = persistent_grid((const void*)k_stft_pair<N, MODE>, WG, 0, 1LL << 40);
-        const long long need = (nch * ((frames + 1) / 2) + F - 1) / F;
-        const int grid = (int)(need < cap ? need : cap);
-        if (grid < 1) return hipSuccess;
-        hipLaunchKernelGGL((k_stft_pair<N, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
-                           hop, win, out, out_ch_stride, pN, tN);
+        // pairs whose two frames lie inside the signal, then the zero-padded tail
+        const long long nfull = n >= N ? (n - N) / hop + 1 : 0;
+        const long long ppc = (frames + 1) / 2;
+        long long mpc = (nfull < frames ? nfull : frames) / 2;
+        if (mpc > ppc) mpc = ppc;
+        const long long tpc = ppc - mpc;
+        static int cap = 0, cap_t = 0;
+        if (!cap) cap = persistent_grid((const void*)k_stft_pair<N, MODE, false>, WG, 0, 1LL << 40);
+        if (!cap_t) cap_t = persistent_grid((const void*)k_stft_pair<N, MODE, true>, WG, 0, 1LL << 40);
+        if (mpc > 0) {
+            const long long need = (nch * mpc + F - 1) / F;
+            const int grid = (int)(need < cap ? need : cap);
+            hipLaunchKernelGGL((k_stft_pair<N, MODE, false>), dim3(grid), dim3(WG), 0, s, sig, n, nch,
+                               ch_stride, frames, hop, 0LL, mpc, win, out, out_ch_stride, pN, tN);
+        }
+        if (tpc > 0) {
+            const long long need = (nch * tpc + F - 1) / F;
+            const int grid = (int)(need < cap_t ? need : cap_t);
+            hipLaunchKernelGGL((k_stft_pair<N, MODE, true>), dim3(grid), dim3(WG), 0, s, sig, n, nch,
+                               ch_stride, frames, hop, mpc, tpc, win, out, out_ch_stride, pN, tN);
+        }
     } else {
         constexpr int M = N / 2;
         const float2* tM = twiddle_table(M);
@@ -316,7 +413,7 @@ __global__ void k_magnitude(const float2* in, float* out, long long count) {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count;
          i += (long long)gridDim.x * blockDim.x) {
         const float2 v = in[i];
-        out[i] = sqrtf(v.x * v.x + v.y * v.y);
+        out[i] = cmag(v.x, v.y);
     }
 }
 
