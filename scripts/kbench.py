@@ -80,7 +80,25 @@ def case_wr(mode, nt, rows=3600000, blocks=2048):
     return (lambda: lib.membench_write(out.data_ptr(), rows, mode, nt, blocks, s)), rows * 4096, (out, lib)
 
 
+def case_stft_exp(e, nch=32, seconds=600):
+    """STFT kernel with parts switched off (scripts/membench.hip k_stft_exp)"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libmembench.so"))
+    lib.membench_stft_exp.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_longlong,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    n = seconds * 48000
+    sig = torch.rand(nch, n, device="cuda") * 2 - 1
+    win = torch.hann_window(1024, periodic=False, device="cuda")
+    fr = (n - 1024) // 256 + 1
+    out = torch.empty(nch, fr, 1024, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    byts = nch * n * 4 + nch * fr * 1024 * 4
+    return (lambda: lib.membench_stft_exp(sig.data_ptr(), n, nch, 256, win.data_ptr(), out.data_ptr(), e, s)), \
+        byts, (sig, win, out, lib)
+
+
 CASES = {
+    **{f"ex{e}": (lambda e=e: case_stft_exp(e)) for e in range(8)},
     "wr4": lambda: case_wr(0, 0), "wr4nt": lambda: case_wr(0, 1),
     "wrpat": lambda: case_wr(1, 0), "wrpatnt": lambda: case_wr(1, 1),
     "wr8nt": lambda: case_wr(2, 1), "wr16": lambda: case_wr(3, 0), "wr16nt": lambda: case_wr(3, 1),
@@ -102,7 +120,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith("wr")))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

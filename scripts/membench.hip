@@ -66,3 +66,125 @@ extern "C" int membench_write(float* out, long long rows, int mode, int nt, int 
 #undef L
     return (int)hipGetLastError();
 }
+
+// ---- STFT bottleneck experiments: the product kernel's structure (nfft 1024,
+// magnitudes) with parts switched off.  E bit0: no FFT, bit1: no stores
+// (guarded by an impossible value), bit2: no loads (synthetic samples).
+#include "../vv-dsp_amd/csrc/hip/fft_core.hpp"
+#include <cmath>
+#include <vector>
+
+namespace vvh {
+template <int E>
+__global__ void __launch_bounds__(256) k_stft_exp(const float* sig, long long n, long long nch, long long ch_stride,
+                                                  long long hop, long long ppc, const float* win, float* out,
+                                                  long long out_ch_stride, const float2* gpass) {
+    constexpr int N = 1024;
+    using G = Geo<N>;
+    using Mi = Mirror<N>;
+    constexpr int F = Wg<N>::F, R = G::RL;
+    __shared__ float2 lds[F * G::LDS];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, 256>(ltab, gpass, gpass);
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + slot * G::LDS;
+    float w[G::P];
+#pragma unroll
+    for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * G::T];
+    const long long pairs = nch * ppc, S = (long long)gridDim.x * F, g = (long long)blockIdx.x * F + slot;
+    const long long per = pairs / S, rem = pairs % S;
+    long long p = g * per + (g < rem ? g : rem);
+    long long p_end = p + per + (g < rem ? 1 : 0);
+    p = uni<64>(p);
+    p_end = uni<64>(p_end);
+    if (p >= p_end) return;
+    long long c = p / ppc, fa = 2 * (p - c * ppc);
+    float xa[G::P], xb[G::P];
+    auto load_pair = [&](long long cc, long long ff) {
+        const float* sa = sig + cc * ch_stride + ff * hop;
+        const float* sb = sa + hop;
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            if (E & 4) {
+                xa[r] = (float)(ff + r) * 1e-3f + t;
+                xb[r] = (float)(cc - r) * 1e-3f - t;
+            } else {
+                xa[r] = sa[t + r * G::T];
+                xb[r] = sb[t + r * G::T];
+            }
+        }
+    };
+    load_pair(c, fa);
+    int kb[G::NPT];
+#pragma unroll
+    for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
+    for (; p < p_end; ++p) {
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
+        long long cn = c, fn = fa + 2;
+        if (fn >= 2 * ppc) {
+            fn = 0;
+            ++cn;
+        }
+        const bool more = p + 1 < p_end;
+        load_pair(more ? cn : c, more ? fn : fa);
+        if (!(E & 1)) fft_regs<N, true, true>(v, t, my, tw);
+        float* rowa = out + c * out_ch_stride + fa * (long long)N;
+        float* rowb = rowa + N;
+#pragma unroll
+        for (int i = 0; i < G::NPT; i += 2) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int q = i * R + r, qm = Mi::normal(q);
+                const float2 Z = v[q], Zm = mirror_of<N, true>(v, t, q);
+                const float ma = __builtin_amdgcn_sqrtf((Z.x + Zm.x) * (Z.x + Zm.x) + (Z.y - Zm.y) * (Z.y - Zm.y));
+                const float mb = __builtin_amdgcn_sqrtf((Z.y + Zm.y) * (Z.y + Zm.y) + (Z.x - Zm.x) * (Z.x - Zm.x));
+                const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
+                if (!(E & 2) || ma == 12345.678f) {
+                    rowa[k] = ma;
+                    rowa[km] = ma;
+                    rowb[k] = mb;
+                    rowb[km] = mb;
+                }
+                (void)qm;
+            }
+        }
+        c = cn;
+        fa = fn;
+    }
+}
+}  // namespace vvh
+
+extern "C" int membench_stft_exp(const float* sig, long long n, long long nch, long long hop, const float* win,
+                                 float* out, int e, void* stream) {
+    static float2* gpass = nullptr;
+    using G = vvh::Geo<1024>;
+    if (!gpass) {
+        std::vector<float2> h(G::TW_PASS_ENTRIES);
+        for (int p = 1; p < G::NPASS; ++p)
+            for (int r = 1; r < G::radix(p); ++r)
+                for (int j = 0; j < G::ns(p); ++j) {
+                    const double a = -2.0 * M_PI * j * r / (G::ns(p) * G::radix(p));
+                    h[G::tw_off(p) + (r - 1) * G::ns(p) + j] = make_float2((float)cos(a), (float)sin(a));
+                }
+        if (hipMalloc(&gpass, h.size() * sizeof(float2)) != hipSuccess) return -2;
+        if (hipMemcpy(gpass, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) return -3;
+    }
+    const long long frames = (n - 1024) / hop + 1;
+    const long long ppc = frames / 2;
+    hipStream_t s = (hipStream_t)stream;
+    const int grid = 512;
+#define L(EE)                                                                                                \
+    hipLaunchKernelGGL((vvh::k_stft_exp<EE>), dim3(grid), dim3(256), 0, s, sig, n, nch, n, hop, ppc, win, out, \
+                       frames * 1024, gpass)
+    switch (e) {
+        case 0: L(0); break; case 1: L(1); break; case 2: L(2); break; case 3: L(3); break;
+        case 4: L(4); break; case 5: L(5); break; case 6: L(6); break; case 7: L(7); break;
+        default: return -1;
+    }
+#undef L
+    return (int)hipGetLastError();
+}

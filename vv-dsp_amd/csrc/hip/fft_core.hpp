@@ -57,6 +57,7 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2
 
 // Streaming (non-temporal) global accesses: data touched exactly once.
 typedef float vf2_t __attribute__((ext_vector_type(2)));
+typedef float vf4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float2 ld_nt(const float2* p) {
     const vf2_t v = __builtin_nontemporal_load(reinterpret_cast<const vf2_t*>(p));
     return make_float2(v.x, v.y);
@@ -258,14 +259,18 @@ __device__ __forceinline__ void stage_twiddles(float2* lds_tab, const float2* gp
 // Barrier between LDS writes and reads of one transform.  A transform owned by
 // threads of a single wave needs no s_barrier: LDS ops of a wave execute in
 // order; only the compiler must not move them (wave_barrier + fence).
+// No memory fences: a fence makes hipcc drain vmcnt (outstanding global loads
+// AND stores) at every exchange, which serialises the streaming pipeline.  LDS
+// ordering needs only lgkmcnt + s_barrier across waves, and nothing but a
+// compiler barrier within one wave.
 template <int T>
 __device__ __forceinline__ void xsync() {
     if constexpr (T > 64) {
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        asm volatile("" ::: "memory");
     }
 }
 
@@ -308,7 +313,7 @@ __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
 #pragma unroll
         for (int r = 0; r < R2; ++r) v[i * R2 + r] = lds[G::pad(b + r * (N / R2))];
     }
-    if constexpr (G::T > 64) __syncthreads();   // next pass' writes must not race these reads
+    if constexpr (G::T > 64) xsync<G::T>();   // next pass' writes must not race these reads
 }
 
 template <int N, bool FWD, int p, bool PAIRED>

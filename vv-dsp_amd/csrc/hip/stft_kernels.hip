@@ -88,6 +88,32 @@ __device__ __forceinline__ void pair_post(float2 Z, float2 Zm, float2* A, float2
     }
 }
 
+// ---- hand-counted memory pipeline (LDS-DMA input spans) ---------------------
+// hipcc does not track inline-asm memory operations, so the kernel counts them
+// itself: vector-memory ops of a wave retire in issue order (loads, stores and
+// LDS-DMA alike), and the only ops in the loop are these.
+// 16 B per lane global -> LDS (dest = M0 + lane*16; M0 is written in the same
+// statement that uses it, as the compiler reserves it).
+__device__ __forceinline__ void glds16(const float* gsrc, float* lds_dst) {
+    const unsigned l = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(l)
+                 : "memory");
+}
+// The trailing s_nop covers the gfx9 hazard "VALU write of a >8-byte VMEM
+// store's data VGPRs right after the store", which hipcc does not model for asm.
+__device__ __forceinline__ void st16_nt_counted(vf4_t* p, vf4_t v) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+template <int CNT>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
+}
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
 // bin k of an output row (MODE 0: float magnitudes, MODE 1: float2 spectrum)
 template <int MODE>
 __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
@@ -97,19 +123,28 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
 
 // Frame pairs (2j, 2j+1) of one channel, j in [pair0, pair0 + ppc): pairs never
 // span channels, so a channel's rows do not depend on how channels are grouped
-// into calls or shards.  !TAIL: both frames lie inside the signal (the bulk);
-// TAIL: the last few pairs, zero-padded past the end / odd last frame.
-template <int N, int MODE, bool TAIL>
+// into calls or shards.
+//   VAR 0: bulk (both frames inside the signal), magnitude rows staged in LDS
+//          and written with 16 B/lane stores (16 B aligned output rows)
+//   VAR 1: bulk, stores straight from registers
+//   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
+template <int N, int MODE, int VAR>
 __global__ void __launch_bounds__(Wg<N>::value)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, const float2* gpass, const float2* gtab) {
     using G = Geo<N>;
     using Mi = Mirror<N>;
+    constexpr bool TAIL = VAR == 2;
+    constexpr bool STAGE = VAR == 0 && MODE == 0 && G::NPASS > 1 && G::T > 1;
+    constexpr bool GLDS = STAGE && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
+    constexpr int SPAN = GLDS ? N + N / 2 : 1;   // floats per transform: hop <= N/2
+    constexpr int NST = 2 * (G::P / 4);          // 16 B stores per pair (both rows)
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
     __shared__ float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    __shared__ float span_all[GLDS ? F * SPAN : 1];
     stage_twiddles<N, WG>(ltab, gpass, gtab);
     __syncthreads();
     const TwTab<N> tw{ltab};
@@ -130,8 +165,22 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     const long long f_lo = 2 * pair0, f_hi = 2 * (pair0 + ppc);
     long long c = p / ppc, fa = f_lo + 2 * (p - c * ppc);
     float xa[G::P], xb[G::P];
+    // GLDS: the pair's span [fa*hop, fa*hop + hop + N) goes HBM/L2 -> LDS by
+    // 16 B/lane LDS-DMA, issued right after the previous span was read, so it
+    // lands while that pair is transformed -- no VGPRs held across iterations.
+    float* span = span_all + (GLDS ? slot * SPAN : 0);
+    auto issue_span = [&](long long cc, long long ff) {
+        const float* s0 = sig + cc * ch_stride + ff * hop;
+        const int len = (int)(N + hop), lane = t & 63;
+        for (int u = t >> 6; u * 256 < len; u += G::T / 64) {
+            const int e = u * 256 + lane * 4;
+            glds16(s0 + (e < len ? e : 0), span + u * 256);
+        }
+    };
     auto load_pair = [&](long long cc, long long ff) {
-        if constexpr (TAIL) {
+        if constexpr (GLDS) {
+            issue_span(cc, ff);
+        } else if constexpr (TAIL) {
             const float* s = sig + cc * ch_stride;
             frame_load<N>(xa, s, ff * hop, n, t, true);
             frame_load<N>(xb, s, (ff + 1 < frames ? ff + 1 : ff) * hop, n, t, ff + 1 < frames);
@@ -146,21 +195,36 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         }
     };
     load_pair(c, fa);
+    if constexpr (GLDS) vm_wait<0>();
     int kb[G::NPT];   // last-pass butterfly of each slot (loop invariant)
 #pragma unroll
     for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
     constexpr long long ES = MODE == 0 ? 4 : 8;
     for (; p < p_end; ++p) {
-        float2 v[G::P];
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
         long long cn = c, fn = fa + 2;
         if (fn >= f_hi) {
             fn = f_lo;
             ++cn;
         }
         const bool more = p + 1 < p_end;
-        if constexpr (TAIL) {
+        if constexpr (GLDS) {
+            // younger than this span's DMA: only the previous pair's NST stores
+            vm_wait<NST>();
+            if constexpr (G::T > 64) lds_barrier();   // the other waves' pieces
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = span[t + r * G::T];
+                xb[r] = span[hop + t + r * G::T];
+            }
+            lgkm_wait0();   // span read before it is refilled
+            if constexpr (G::T > 64) lds_barrier();
+            if (more) load_pair(cn, fn);
+        }
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
+        if constexpr (GLDS) {
+        } else if constexpr (TAIL) {
             if (more) load_pair(cn, fn);
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
@@ -169,7 +233,47 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * (long long)N) * ES;
         char* rowb = rowa + N * ES;
         const bool has_b = TAIL ? fa + 1 < frames : true;
-        if constexpr (G::T == 1) {
+        if constexpr (STAGE) {
+            // both magnitude rows through the (now idle) exchange buffer, then
+            // full-line 16 B/lane streaming stores: 2N/(4T) instead of 2P per lane
+            float* sf = reinterpret_cast<float*>(my);
+#pragma unroll
+            for (int i = 0; i < G::NPT; i += 2) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int q = i * R + r, qm = Mi::normal(q);
+                    float2 A, B;
+                    pair_post<0>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                    float am = A.x, bm = B.x;
+                    if (i == 0) {
+                        float2 A2, B2;
+                        pair_post<0>(v[qm], v[Mi::special(qm)], &A2, &B2);
+                        am = t == 0 ? A2.x : am;
+                        bm = t == 0 ? B2.x : bm;
+                    }
+                    const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
+                    sf[k] = A.x;
+                    sf[km] = am;
+                    sf[N + k] = B.x;
+                    sf[N + km] = bm;
+                }
+            }
+            xsync<G::T>();
+#pragma unroll
+            for (int j = 0; j < G::P / 4; ++j) {
+                const int e = 4 * (t + G::T * j);
+                const vf4_t a = *reinterpret_cast<const vf4_t*>(sf + e);
+                const vf4_t b = *reinterpret_cast<const vf4_t*>(sf + N + e);
+                if constexpr (GLDS) {   // counted by the vm_wait<NST> above: exactly NST per pair
+                    st16_nt_counted(reinterpret_cast<vf4_t*>(rowa) + (t + G::T * j), a);
+                    st16_nt_counted(reinterpret_cast<vf4_t*>(rowb) + (t + G::T * j), b);
+                } else {
+                    __builtin_nontemporal_store(a, reinterpret_cast<vf4_t*>(rowa) + (t + G::T * j));
+                    __builtin_nontemporal_store(b, reinterpret_cast<vf4_t*>(rowb) + (t + G::T * j));
+                }
+            }
+            xsync<G::T>();   // the next transform's first exchange reuses `my`
+        } else if constexpr (G::T == 1) {
 #pragma unroll
             for (int q = 0; q < G::P; ++q) {
                 float2 A, B;
@@ -323,21 +427,24 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         long long mpc = (nfull < frames ? nfull : frames) / 2;
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
-        static int cap = 0, cap_t = 0;
-        if (!cap) cap = persistent_grid((const void*)k_stft_pair<N, MODE, false>, WG, 0, 1LL << 40);
-        if (!cap_t) cap_t = persistent_grid((const void*)k_stft_pair<N, MODE, true>, WG, 0, 1LL << 40);
+        static int cap[3] = {0, 0, 0};
+        auto launch = [&](auto kern, int var, long long pair0, long long cnt) {
+            if (!cap[var]) cap[var] = persistent_grid((const void*)kern, WG, 0, 1LL << 40);
+            const long long need = (nch * cnt + F - 1) / F;
+            const int grid = (int)(need < cap[var] ? need : cap[var]);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0, cnt,
+                               win, out, out_ch_stride, pN, tN);
+        };
+        // 16 B aligned output rows allow the staged 16 B/lane stores
+        bool aligned = ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0 && N >= 4;
+        // T >= 64: VAR 0 also reads its input spans by 16 B LDS-DMA
+        if (Geo<N>::T >= 64)
+            aligned = aligned && hop % 4 == 0 && hop <= N / 2 && ((uintptr_t)sig & 15) == 0 && (ch_stride & 3) == 0;
         if (mpc > 0) {
-            const long long need = (nch * mpc + F - 1) / F;
-            const int grid = (int)(need < cap ? need : cap);
-            hipLaunchKernelGGL((k_stft_pair<N, MODE, false>), dim3(grid), dim3(WG), 0, s, sig, n, nch,
-                               ch_stride, frames, hop, 0LL, mpc, win, out, out_ch_stride, pN, tN);
+            if (aligned) launch(k_stft_pair<N, MODE, 0>, 0, 0LL, mpc);
+            else launch(k_stft_pair<N, MODE, 1>, 1, 0LL, mpc);
         }
-        if (tpc > 0) {
-            const long long need = (nch * tpc + F - 1) / F;
-            const int grid = (int)(need < cap_t ? need : cap_t);
-            hipLaunchKernelGGL((k_stft_pair<N, MODE, true>), dim3(grid), dim3(WG), 0, s, sig, n, nch,
-                               ch_stride, frames, hop, mpc, tpc, win, out, out_ch_stride, pN, tN);
-        }
+        if (tpc > 0) launch(k_stft_pair<N, MODE, 2>, 2, mpc, tpc);
     } else {
         constexpr int M = N / 2;
         const float2* tM = twiddle_table(M);
