@@ -35,13 +35,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "vv-dsp_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import vvdsp_amd as vv  # noqa: E402
+import vvdsp_dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 NFFT, HOP = 1024, 256
 FS = 48000
 CH_PER_GPU = 32
 SAMPLES = 10 * 60 * FS        # 10 min per channel
-PUBLISHED_FPS = 24903.0       # STFT_size_1024, Ryzen 9 7950X 1 thread (stft_profile.json:29-34)
+PUBLISHED_CPU_FPS = 24903.0   # BASELINE.md §1 STFT_size_1024 (CPU, 1 thread) -- informational only:
+                              # BASELINE.json "published" is empty, so vs_baseline is null
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_bench_pmc.json")
 METRIC = "STFT frames/sec (1024-pt, hop 256) at 1/2/4/8 GPU; achieved HBM GB/s vs peak"
 
 
@@ -106,12 +109,13 @@ def fir_roofline(reps=10):
             "samples_per_s": round(nch * n / (avg * 1e-3), 1)}
 
 
-def cpu_baseline(threads=None):
-    """The reference's own vv_dsp_stft_spectrogram (KissFFT, oracle/_ref) on
-    this host: each thread runs 4 x 60 s mono (11,248 frames) signals."""
+def cpu_baseline(threads=None, seconds=15.0):
+    """The reference's own vv_dsp_stft_spectrogram (KissFFT, oracle/_ref = the
+    reference sources compiled in the build container) on this host's cores:
+    `threads` workers each run whole 60 s mono spectrograms back to back until
+    `seconds` have passed (a bounded sample of the same per-channel workload)."""
     from vvapi import VvDsp
     path = os.path.join(ROOT, "oracle", "_ref", "libvvref.so")
-    kind = "reference"
     if not os.path.exists(path):
         return {"value": None, "unit": "frames/s", "cores": 0, "kind": "reference",
                 "sample": "oracle/_ref/libvvref.so missing"}
@@ -120,34 +124,89 @@ def cpu_baseline(threads=None):
     n = 60 * FS
     rng = np.random.default_rng(3)
     sigs = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(threads)]
-    reps = 4
+    t_end = time.perf_counter() + seconds
 
     def work(i):
-        for _ in range(reps):
-            ref.spectrogram(sigs[i], NFFT, HOP)
-        return reps * frames_of(n)
+        done = 0
+        while time.perf_counter() < t_end:
+            ref.spectrogram(sigs[i], NFFT, HOP)   # ctypes releases the GIL
+            done += 1
+        return done
 
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(threads) as ex:
-        frames = sum(ex.map(work, range(threads)))
+        runs = sum(ex.map(work, range(threads)))
     dt = time.perf_counter() - t0
-    # single-thread reference point on one signal
+    frames = runs * frames_of(n)
     t1 = time.perf_counter()
     ref.spectrogram(sigs[0], NFFT, HOP)
     d1 = time.perf_counter() - t1
-    return {"value": round(frames / dt, 1), "unit": "frames/s", "cores": threads, "kind": kind,
-            "sample": f"{threads} threads x {reps} x vv_dsp_stft_spectrogram(60 s @ 48 kHz mono, 1024/256 Hann) "
-                      f"= {frames} frames in {dt:.2f} s",
+    return {"value": round(frames / dt, 1), "unit": "frames/s", "cores": threads, "kind": "reference",
+            "sample": f"{threads} threads x vv_dsp_stft_spectrogram(60 s @ 48 kHz mono, 1024 Hann, hop 256) "
+                      f"back to back for {seconds:.0f} s: {runs} runs = {frames} frames in {dt:.2f} s",
             "single_thread_frames_per_s": round(frames_of(n) / d1, 1)}
+
+
+def hbm_traffic(channels):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    command (scripts/gpu_prof.sh + scripts/pmc_summary.py --json): FETCH_SIZE x 2
+    (gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md §HBM) + WRITE_SIZE,
+    both in KiB, summed over the bulk and tail STFT launches of one step."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            prof = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC summary committed"
+    if prof.get("channels_per_gpu") != channels:
+        return None, f"PMC summary is for {prof.get('channels_per_gpu')} channels per GPU"
+    tot, names = 0.0, []
+    for k, c in prof["kernels"].items():
+        if k.startswith("vvh::k_stft_pair<1024, 0"):
+            tot += (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+            names.append(k)
+    if not names:
+        return None, "PMC summary has no k_stft_pair<1024,0,*> entries"
+    return round(tot), f"{os.path.relpath(TRAFFIC_JSON, ROOT)} ({prof.get('box', '?')}): " \
+                       f"(2*FETCH_SIZE + WRITE_SIZE) KiB x 1024 per dispatch over {', '.join(names)}"
+
+
+def gather_leg(out, total_ch, compute_s, frames_per_step, rank):
+    """One timed RCCL gather (torch.distributed nccl backend = RCCL, point to
+    point over xGMI) of every rank's [ch][frame][1024] rows to rank 0."""
+    try:
+        full = None
+        if rank == 0:
+            full = torch.empty((total_ch,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vvdsp_dist.gather_rows(out, total_ch, dst=0, out=full)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g = time.perf_counter() - t0
+        t = torch.tensor([g], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        g = float(t.item())
+        gathered = (total_ch - out.shape[0]) * out[0].numel() * out.element_size()
+        del full
+        return {"gather_s": round(g, 4), "bytes_into_rank0": gathered,
+                "xgmi_GBs_into_rank0": round(gathered / g / 1e9, 1),
+                "frames_per_s_with_gather": round(frames_per_step / (compute_s + g), 1),
+                "note": "one step of compute + one gather of the full magnitude rows to rank 0"}
+    except Exception as e:  # report, do not lose the bench line
+        return {"error": repr(e)[:300]}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=25)
     ap.add_argument("--channels", type=int, default=CH_PER_GPU, help="channels per GPU")
     ap.add_argument("--no-extras", action="store_true", help="skip config 2/4 and CPU baseline legs")
+    ap.add_argument("--gather", choices=["auto", "on", "off"], default="auto",
+                    help="after the timed steps, time one RCCL gather of all spectrogram rows to rank 0 "
+                         "(config 5 'with gather'; auto = on when N > 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -201,12 +260,17 @@ def main():
     bytes_per_launch = C_ * SAMPLES * 4 + C_ * nfr * NFFT * 4 + NFFT * 4
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
+    traffic, traffic_src = hbm_traffic(C_)
+
     # spot-check one frame row against NumPy f64 so a fast-but-wrong kernel cannot report
     fr = 12345
     x0 = sig[0, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
     w = np.array([0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(NFFT - 1) * np.float32(i))
                   for i in range(NFFT)], np.float64)
     ok = np.allclose(out[0, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * w)), rtol=5e-5, atol=5e-5)
+    gather = None
+    if world > 1 and (args.gather == "on" or args.gather == "auto"):
+        gather = gather_leg(out, C_ * world, elapsed / args.steps, frames_total / args.steps, rank)
     del sig, out, st
     torch.cuda.empty_cache()
 
@@ -220,8 +284,10 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / PUBLISHED_FPS, 1),
-        "vs_baseline_ref": "BASELINE.md STFT_size_1024 = 24,903 frames/s (Ryzen 9 7950X, 1 thread, KissFFT)",
+        "vs_baseline": None,
+        "published_cpu_reference": {"value": PUBLISHED_CPU_FPS, "unit": "frames/s",
+                                    "what": "BASELINE.md §1 STFT_size_1024, Ryzen 9 7950X, 1 thread, KissFFT "
+                                            "(informational; BASELINE.json publishes no number for this metric)"},
         "dtype": "f32",
         "data": "synthetic: uniform[-1,1) per channel, seed = global channel id, generated in HBM",
         "config": {
@@ -231,12 +297,17 @@ def main():
             "nfft": NFFT, "hop": HOP, "window": "hann (symmetric, window.c:25-36)",
             "output": "[ch][frame][1024] f32 magnitudes (stft.c:133-139)",
             "parallelism": f"dp{world} (channel shards, no data-path collective)"},
-        "roofline": {"kernel": "vvh::k_stft<512,0> (fused frame gather + Hann + 1024-pt real FFT + |X|)",
+        "roofline": {"kernel": "vvh::k_stft_pair<1024,0,0> (LDS-DMA frame spans + Hann + two frames per "
+                               "1024-pt complex FFT + |X| rows, 16 B stores) + its zero-padded tail launch "
+                               "k_stft_pair<1024,0,2>; kernel_ms = HIP events around both on the launch stream",
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "kernel_ms": round(kern_ms, 4)},
         "check_row_vs_numpy_f64": bool(ok),
     }
+    if gather is not None:
+        res["with_gather"] = gather
     if rank == 0 and not args.no_extras and world == 1:
         res["fft_c2c_1024"] = fft_c2c_roofline()
         torch.cuda.empty_cache()

@@ -1,0 +1,60 @@
+"""Multi-GPU layout of the batched STFT (BASELINE config 5).
+
+Channels are independent, so the path shards without any data-path exchange:
+rank r owns a contiguous channel range and runs the single-GPU kernels on it
+(one process per GPU, torch.distributed for rendezvous only).  The only
+collective is the optional gather of the spectrogram rows to one rank that
+config 5 asks for ("RCCL gather over xGMI"): on the nccl backend (= RCCL on
+ROCm) `dist.gather` is point-to-point over xGMI; on gloo it is the same call
+on CPU tensors, which is how the CPU test suite exercises this module.
+"""
+import torch
+import torch.distributed as dist
+
+
+def channel_shard(total, world, rank):
+    """Contiguous channel range [lo, hi) of `rank`; rank order == channel order,
+    sizes differ by at most one."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    base, rem = divmod(int(total), int(world))
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def shard_sizes(total, world):
+    return [b - a for a, b in (channel_shard(total, world, r) for r in range(world))]
+
+
+def gather_rows(local, total, dst=0, group=None, out=None):
+    """Gather every rank's [ch_r, ...] block into one [total, ...] tensor on
+    rank `dst` (None elsewhere).  Equal shards land directly in `out` (or a
+    new tensor) with no extra copy; uneven shards are padded to the largest
+    one for the collective and trimmed on the destination."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = shard_sizes(total, world)
+    if local.shape[0] != sizes[rank]:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} channels, layout says {sizes[rank]}")
+    cmax = max(sizes)
+    if min(sizes) == cmax and cmax > 0:
+        if rank == dst:
+            if out is None:
+                out = torch.empty((total,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+            dist.gather(local.contiguous(), gather_list=list(out.view((world, cmax) + tuple(local.shape[1:]))
+                                                              .unbind(0)), dst=dst, group=group)
+            return out
+        dist.gather(local.contiguous(), dst=dst, group=group)
+        return None
+    if local.shape[0] < cmax:
+        pad = torch.zeros((cmax - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+        send = torch.cat([local, pad], 0)
+    else:
+        send = local.contiguous()
+    if rank == dst:
+        bufs = [torch.empty_like(send) for _ in range(world)]
+        dist.gather(send, gather_list=bufs, dst=dst, group=group)
+        return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0)
+    dist.gather(send, dst=dst, group=group)
+    return None
