@@ -350,6 +350,16 @@ __device__ __forceinline__ long long uni(long long x) {
     }
 }
 
+// Contiguous chunk [lo, hi) of `total` work items for persistent slot g of S:
+// consecutive items of a slot share input lines in L1/L2 (overlapping frames,
+// overlap-save halos) instead of being fetched by another XCD.
+__device__ __forceinline__ void chunk_of(long long total, long long g, long long S, long long* lo,
+                                         long long* hi) {
+    const long long per = total / S, rem = total % S;
+    *lo = g * per + (g < rem ? g : rem);
+    *hi = *lo + per + (g < rem ? 1 : 0);
+}
+
 // Workgroup geometry: 256 threads (several transforms per block) unless one
 // transform needs more threads.
 template <int N>

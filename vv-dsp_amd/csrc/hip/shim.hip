@@ -450,19 +450,24 @@ struct vvhip_fir {
     DevBuf bx, by, bp;
 };
 
+// Overlap-save block N (= complex FFT size of k_fir_pair): the smallest power
+// of two >= max(4*(L-1), 64), so that at least 3/4 of every block is output,
+// grown toward the preferred size (1024: four transforms per 256-thread
+// workgroup, H and twiddles in 51 KB of LDS) while the signal is longer.
+// VVHIP_FIR_BLOCK overrides the preferred size.  0 = no OLS block (long
+// filters use the direct form).
 static size_t fir_block(const vvhip_fir* f, size_t n) {
-    // smallest pow2 >= max(2*taps, 64); grown toward the preferred block (4096:
-    // M = 2048 runs the mirror-paired multiply, L2 re-read (L-1)/(4096-(L-1)))
-    // while the signal is longer.  VVHIP_FIR_BLOCK overrides the preferred size.
     static size_t pref = 0;
     if (!pref) {
         const char* e = getenv("VVHIP_FIR_BLOCK");
-        pref = e ? (size_t)atol(e) : 4096;
-        if (pref < 64 || pref > 8192 || (pref & (pref - 1))) pref = 4096;
+        pref = e ? (size_t)atol(e) : 1024;
+        if (pref < 64 || pref > 8192 || (pref & (pref - 1))) pref = 1024;
     }
+    const size_t lm1 = f->taps - 1;
     size_t nr = 64;
-    while (nr < 2 * f->taps) nr <<= 1;
-    while (nr < pref && nr < n + f->taps - 1) nr <<= 1;
+    while (nr < 4 * lm1 && nr < 8192) nr <<= 1;
+    while (nr < pref && nr < n + lm1) nr <<= 1;
+    if (nr <= lm1 || nr - lm1 < nr / 4) return 0;
     return nr;
 }
 
@@ -473,16 +478,21 @@ static int fir_spectrum(vvhip_fir* f, size_t nr, const float2** H, hipStream_t s
             *H = sp.H;
             return ST_OK;
         }
+    // H = FFT(h zero-padded to nr) / nr over all nr bins (R2C, Hermitian expand)
     float* hp = nullptr;
+    float2* Hh = nullptr;
     float2* Hd = nullptr;
     HIPCHK(hipMalloc(&hp, sizeof(float) * nr), ST_INTERNAL);
-    HIPCHK(hipMalloc(&Hd, sizeof(float2) * (nr / 2 + 1)), ST_INTERNAL);
+    HIPCHK(hipMalloc(&Hh, sizeof(float2) * (nr / 2 + 1)), ST_INTERNAL);
+    HIPCHK(hipMalloc(&Hd, sizeof(float2) * nr), ST_INTERNAL);
     HIPCHK(hipMemsetAsync(hp, 0, sizeof(float) * nr, s), ST_INTERNAL);
     HIPCHK(hipMemcpyAsync(hp, f->d_h, sizeof(float) * f->taps, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
-    HIPCHK(launch_r2c((long long)nr, hp, Hd, 1, (long long)nr, (long long)(nr / 2 + 1), s), ST_INTERNAL);
-    HIPCHK(launch_scale_cpx(Hd, (long long)(nr / 2 + 1), 2.0f / (float)nr, s), ST_INTERNAL);
+    HIPCHK(launch_r2c((long long)nr, hp, Hh, 1, (long long)nr, (long long)(nr / 2 + 1), s), ST_INTERNAL);
+    HIPCHK(launch_hermitian_expand((long long)nr, Hh, Hd, 1, (long long)(nr / 2 + 1), 0, s), ST_INTERNAL);
+    HIPCHK(launch_scale_cpx(Hd, (long long)nr, 1.0f / (float)nr, s), ST_INTERNAL);
     HIPCHK(hipStreamSynchronize(s), ST_INTERNAL);
     (void)hipFree(hp);
+    (void)hipFree(Hh);
     f->specs.push_back({nr, Hd});
     *H = Hd;
     return ST_OK;
@@ -530,8 +540,8 @@ int vvhip_fir_apply_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n,
     if (n == 0 || nch == 0) return ST_OK;
     hipStream_t s = (hipStream_t)stream;
     const long long L = (long long)f->taps;
-    if (mode == 0 && f->taps <= 4097) {
-        const size_t nr = fir_block(f, n);
+    const size_t nr = mode == 0 ? fir_block(f, n) : 0;
+    if (nr) {
         const float2* H = nullptr;
         if (int st = fir_spectrum(f, nr, &H, s)) return st;
         HIPCHK(launch_fir_ols((long long)nr, L, H, d_x, d_y, (long long)n, (long long)nch, (long long)x_stride,

@@ -51,14 +51,6 @@ __device__ __forceinline__ void frame_load(float* x, const float* s, long long s
     }
 }
 
-// contiguous chunk [lo, hi) of `total` work items for persistent slot g of S
-__device__ __forceinline__ void chunk_of(long long total, long long g, long long S, long long* lo,
-                                         long long* hi) {
-    const long long per = total / S, rem = total % S;
-    *lo = g * per + (g < rem ? g : rem);
-    *hi = *lo + per + (g < rem ? 1 : 0);
-}
-
 // |re + i im| with the hardware v_sqrt_f32 (<=1 ulp).  sqrtf's correctly
 // rounded IEEE expansion costs ~10 VALU per bin; the magnitude is compared at
 // the reference's float tolerance, never bit-exactly.
