@@ -3,21 +3,32 @@
 // vv_dsp_fir_apply_fft (src/filter/fir.c:75-135) is "the first n samples of the
 // linear convolution with zero initial state"; vv_dsp_fir_apply (:160-196) is
 // the same convolution continued from a (taps-1)-sample history.  Both are
-// computed here as overlap-save with blocks of N real samples:
+// computed here as overlap-save with blocks of N real samples and an
+// effective history LE >= taps-1 (the filter read as zero-padded to LE+1 taps,
+// which changes nothing; LE is a multiple of 4 and >= N/4 so that block starts
+// are 16 B aligned and a pair's input span fits its LDS buffer):
 //
-//   block j of channel c covers input samples [j*Lout - (L-1), j*Lout + Lout)
-//   (Lout = N - (L-1)); samples before 0 come from `prefix` (history) or are 0;
+//   block j of channel c covers input samples [j*Lout - LE, j*Lout + Lout)
+//   (Lout = N - LE); samples before 0 come from `prefix` (history) or are 0;
 //   outputs j*Lout + [0, Lout) are the block's circular-convolution samples
-//   L-1 .. N-1.
+//   LE .. N-1.
 //
 // Two real blocks per complex FFT: z = a + i b (blocks j and j+1), then
 // Y = FFT(z) * H with H = FFT(h)/N over all N bins, and y = IFFT(Y) holds
 // a*h in its real part and b*h in its imaginary part (h is real, so the
-// product keeps the two convolutions separate -- no split step at all).
-// Per pair: forward N-pt FFT in registers/LDS, multiply by H (staged in LDS),
-// one LDS re-order into natural order, inverse N-pt FFT, lane-contiguous
-// stores.  The signal is read once from HBM (the L-1 overlap comes from L2)
-// and the output written once: 8 B per sample.
+// product keeps the two convolutions apart -- no split step).  After the
+// forward Stockham FFT thread t holds Z[t + T*m] for m < P, which is exactly
+// the input set of the inverse transform: the multiply by H re-indexes
+// registers and no LDS re-order is needed between the two transforms.
+//
+// k_fir_pair<N, true>  (bulk, T >= 64): the pair's input span comes HBM -> LDS
+//   by 16 B/lane LDS-DMA issued one pair ahead with a hand-counted vmcnt;
+//   outputs are dword stores of which lanes below LE go to a write sink, so
+//   every pair issues exactly 2P stores.
+// k_fir_pair<N, false> (edges and small N): register loads with the prefix /
+//   zero padding, predicated stores.
+// HBM traffic: the signal read once (the LE overlap comes from L2/LDS), the
+// output written once -- 8 B per sample.
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
 
@@ -25,7 +36,8 @@
 
 namespace vvh {
 
-// samples s0 + t + r*T of one block (prefix before 0, zero past n)
+// samples s0 + t + r*T of one block (prefix before 0 -- only its last lm1
+// samples exist, earlier ones meet zero taps -- and zero past n)
 template <int N>
 __device__ __forceinline__ void fir_blk_load(float* xr, const float* xs, const float* pre, long long s0,
                                              long long n, long long lm1, int t) {
@@ -40,7 +52,7 @@ __device__ __forceinline__ void fir_blk_load(float* xr, const float* xs, const f
             const long long i = s0 + t + r * G::T;
             float v = 0.0f;
             if (i < 0) {
-                if (pre) v = pre[lm1 + i];
+                if (pre && i >= -lm1) v = pre[lm1 + i];
             } else if (i < n) {
                 v = xs[i];
             }
@@ -49,95 +61,190 @@ __device__ __forceinline__ void fir_blk_load(float* xr, const float* xs, const f
     }
 }
 
+// Y = Z * H with the register re-index forward-output -> inverse-input
 template <int N>
+__device__ __forceinline__ void fir_multiply(const float2* v, float2* u, const float2* lH, int t) {
+    using G = Geo<N>;
+#pragma unroll
+    for (int q = 0; q < G::P; ++q) {
+        const int m = q / G::RL + G::NPT * (q % G::RL);   // out_pos<N>(t, q) = t + T*m
+        u[m] = cmul(v[q], lH[t + G::T * m]);
+    }
+}
+
+// Pairs of channel c handled by a launch: idx < qlo -> pair idx, else pair
+// qhi + (idx - qlo); cnt = pairs per channel in this launch.
+template <int N, bool BULK>
 __global__ void __launch_bounds__(Wg<N>::value)
-k_fir_pair(long long taps, const float2* Hg, const float* x, float* y, long long n, long long nch,
-           long long x_stride, long long y_stride, const float* prefix, long long nblk, const float2* gpass,
-           const float2* gtab) {
+k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float* y, long long n,
+           long long nch, long long x_stride, long long y_stride, const float* prefix, long long cnt,
+           long long qlo, long long qhi, const float2* gpass, const float2* gtab, float* sink) {
     using G = Geo<N>;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    constexpr int SPAN = BULK ? N + (3 * N) / 4 : 1;   // N + Lout, Lout <= 3N/4
+    constexpr int NST = 2 * G::P;                      // stores per pair (bulk)
+    static_assert(!BULK || G::T >= 64, "LDS-DMA spans need whole waves per transform");
     __shared__ float2 lds[F * G::LDS];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
     __shared__ float2 lH[N];
+    __shared__ float span_all[BULK ? F * SPAN : 1];
     stage_twiddles<N, WG>(ltab, gpass, gtab);
     for (int i = threadIdx.x; i < N; i += WG) lH[i] = Hg[i];
     __syncthreads();
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
-    const long long lm1 = taps - 1, lout = N - lm1;
-    const long long ppc = (nblk + 1) / 2;   // block pairs per channel
+    const long long lout = N - le;
     long long p, p_end;
-    chunk_of(nch * ppc, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &p, &p_end);
+    chunk_of(nch * cnt, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &p, &p_end);
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
     if (p >= p_end) return;   // uniform per transform (F == 1 whenever T > 64)
-    long long c = p / ppc, j = 2 * (p - c * ppc);
-    float xa[G::P], xb[G::P];
-    auto load_pair = [&](long long cc, long long jj) {
-        const float* xs = x + cc * x_stride;
-        const float* pre = prefix ? prefix + cc * lm1 : nullptr;
-        fir_blk_load<N>(xa, xs, pre, jj * lout - lm1, n, lm1, t);
-        fir_blk_load<N>(xb, xs, pre, (jj + 1) * lout - lm1, n, lm1, t);
-    };
-    load_pair(c, j);
-    for (; p < p_end; ++p) {
-        float2 v[G::P];
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
-        long long cn = c, jn = j + 2;
-        if (jn >= 2 * ppc) {
-            jn = 0;
-            ++cn;
-        }
-        if (p + 1 < p_end) load_pair(cn, jn);
-        fft_regs<N, true>(v, t, my, tw);
-        // Y = Z * H, re-ordered to natural order for the inverse transform
-#pragma unroll
-        for (int q = 0; q < G::P; ++q) {
-            const int k = out_pos<N>(t, q);
-            my[G::pad(k)] = cmul(v[q], lH[k]);
-        }
-        xsync<G::T>();
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) v[r] = my[G::pad(t + r * G::T)];
-        xsync<G::T>();
-        fft_regs<N, false>(v, t, my, tw);
-        // circular samples e >= L-1 are outputs: Re -> block j, Im -> block j+1
-        float* ys = y + c * y_stride;
-        const long long oa0 = j * lout - lm1;
-#pragma unroll
-        for (int q = 0; q < G::P; ++q) {
-            const long long e = out_pos<N>(t, q);
-            if (e >= lm1) {
-                const long long oa = oa0 + e, ob = oa + lout;
-                if (oa < n) ys[oa] = v[q].x;
-                if (ob < n) ys[ob] = v[q].y;
+    long long c = p / cnt, idx = p - c * cnt;
+    auto block_of = [&](long long i) { return 2 * (i < qlo ? i : qhi + (i - qlo)); };
+    long long j = block_of(idx);
+    if constexpr (BULK) {
+        float* span = span_all + slot * SPAN;
+        float* snk = sink + ((((long long)blockIdx.x * (WG / 64) + (lt >> 6)) * 64) % SINK_FLOATS) + (lt & 63);
+        auto issue_span = [&](long long cc, long long jj) {
+            const float* s0 = x + cc * x_stride + jj * lout - le;
+            const int len = (int)(N + lout), lane = t & 63;
+            for (int u = t >> 6; u * 256 < len; u += G::T / 64) {
+                const int e = u * 256 + lane * 4;
+                glds16(s0 + (e < len ? e : 0), span + u * 256);
             }
+        };
+        issue_span(c, j);
+        vm_wait<0>();
+        for (; p < p_end; ++p) {
+            long long cn = c, jn = j + 2;
+            if (jn >= 2 * (qhi + cnt)) {   // bulk launch: qlo == 0, pairs [qhi, qhi+cnt)
+                jn = 2 * qhi;
+                ++cn;
+            }
+            vm_wait<NST>();   // younger than this span's DMA: the previous pair's stores
+            if constexpr (G::T > 64) lds_barrier();
+            float2 v[G::P];
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) v[r] = make_float2(span[t + r * G::T], span[lout + t + r * G::T]);
+            lgkm_wait0();
+            if constexpr (G::T > 64) lds_barrier();
+            if (p + 1 < p_end) issue_span(cn, jn);
+            fft_regs<N, true>(v, t, my, tw);
+            float2 u[G::P];
+            fir_multiply<N>(v, u, lH, t);
+            fft_regs<N, false>(u, t, my, tw);
+            float* ya = y + c * y_stride + j * lout - le;   // + e: block j output (e >= le)
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                const long long e = out_pos<N>(t, q);
+                const bool ok = e >= le;
+                st4_counted(ok ? ya + e : snk, u[q].x);
+                st4_counted(ok ? ya + e + lout : snk, u[q].y);
+            }
+            c = cn;
+            j = jn;
         }
-        c = cn;
-        j = jn;
+    } else {
+        float xa[G::P], xb[G::P];
+        auto load_pair = [&](long long cc, long long jj) {
+            const float* xs = x + cc * x_stride;
+            const float* pre = prefix ? prefix + cc * lm1 : nullptr;
+            fir_blk_load<N>(xa, xs, pre, jj * lout - le, n, lm1, t);
+            fir_blk_load<N>(xb, xs, pre, (jj + 1) * lout - le, n, lm1, t);
+        };
+        load_pair(c, j);
+        for (; p < p_end; ++p) {
+            float2 v[G::P];
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
+            long long cn = c, in = idx + 1;
+            if (in >= cnt) {
+                in = 0;
+                ++cn;
+            }
+            const long long jn = block_of(in);
+            if (p + 1 < p_end) load_pair(cn, jn);
+            fft_regs<N, true>(v, t, my, tw);
+            float2 u[G::P];
+            fir_multiply<N>(v, u, lH, t);
+            fft_regs<N, false>(u, t, my, tw);
+            float* ys = y + c * y_stride;
+            const long long oa0 = j * lout - le;
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                const long long e = out_pos<N>(t, q);
+                if (e >= le) {
+                    const long long oa = oa0 + e, ob = oa + lout;
+                    if (oa < n) ys[oa] = u[q].x;
+                    if (ob < n) ys[ob] = u[q].y;
+                }
+            }
+            c = cn;
+            idx = in;
+            j = jn;
+        }
     }
 }
+
+// Effective history of the block geometry (see the header comment).
+long long fir_effective_history(long long nfft, long long taps) {
+    long long le = taps - 1;
+    if (le < nfft / 4) le = nfft / 4;
+    return (le + 3) & ~3LL;
+}
+
+// LDS-DMA bulk variant: one wave per transform, where span + exchange + H +
+// twiddles (80 KB per 4 transforms) still leave two workgroups per CU
+template <int N>
+constexpr bool FIR_BULK = Geo<N>::T == 64;
 
 template <int N>
 static hipError_t run_fir(long long taps, const float2* H, const float* x, float* y, long long n,
                           long long nch, long long x_stride, long long y_stride, const float* prefix,
                           hipStream_t s) {
-    const long long lout = (long long)N - (taps - 1);
-    if (lout <= 0) return hipErrorInvalidValue;
-    const long long nblk = (n + lout - 1) / lout;
+    const long long lm1 = taps - 1, le = fir_effective_history(N, taps), lout = N - le;
+    if (lout < N / 4) return hipErrorInvalidValue;
+    const long long nblk = (n + lout - 1) / lout, ppc = (nblk + 1) / 2;
     const float2* tN = twiddle_table(N);
     const float2* pN = pass_twiddles(N);
-    if (!tN || !pN) return hipErrorOutOfMemory;
+    float* sink = store_sink();
+    if (!tN || !pN || !sink) return hipErrorOutOfMemory;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
-    static int cap = 0;
-    if (!cap) cap = persistent_grid((const void*)k_fir_pair<N>, WG, 0, 1LL << 40);
-    const long long need = (nch * ((nblk + 1) / 2) + F - 1) / F;
-    const int grid = (int)(need < cap ? need : cap);
-    if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL(k_fir_pair<N>, dim3(grid), dim3(WG), 0, s, taps, H, x, y, n, nch, x_stride, y_stride,
-                       prefix, nblk, pN, tN);
+    // bulk pairs [qf, ql): span start (2q*lout - le) >= 0 and both blocks'
+    // outputs (2q+2)*lout <= n; aligned channels only
+    long long qf = ppc, ql = ppc;
+    if constexpr (FIR_BULK<N>) {
+        const bool aligned = ((uintptr_t)x & 15) == 0 && (x_stride & 3) == 0;
+        if (aligned) {
+            qf = (le + 2 * lout - 1) / (2 * lout);
+            ql = n / (2 * lout);   // (2q+2)*lout <= n  <=>  q < n/(2 lout)
+            if (ql > ppc) ql = ppc;
+            if (qf >= ql) qf = ql = ppc;
+        }
+    }
+    // the bulk kernel reads spans [2q*lout - le, (2q+2)*lout) and writes outputs
+    // below (2q+2)*lout without bounds checks: verify the range on the host
+    if (ql > qf && (2 * qf * lout < le || 2 * ql * lout > n || N + lout > N + (3 * N) / 4))
+        return hipErrorInvalidValue;
+    static int cap_b = 0, cap_e = 0;
+    if (ql > qf) {
+        if constexpr (FIR_BULK<N>) {
+            if (!cap_b) cap_b = persistent_grid((const void*)k_fir_pair<N, true>, WG, 0, 1LL << 40);
+            const long long cnt = ql - qf, need = (nch * cnt + F - 1) / F;
+            const int grid = (int)(need < cap_b ? need : cap_b);
+            hipLaunchKernelGGL((k_fir_pair<N, true>), dim3(grid), dim3(WG), 0, s, lm1, le, H, x, y, n, nch,
+                               x_stride, y_stride, prefix, cnt, 0LL, qf, pN, tN, sink);
+        }
+    }
+    const long long ecnt = qf + (ppc - ql);   // edge pairs per channel: [0, qf) and [ql, ppc)
+    if (ecnt > 0) {
+        if (!cap_e) cap_e = persistent_grid((const void*)k_fir_pair<N, false>, WG, 0, 1LL << 40);
+        const long long need = (nch * ecnt + F - 1) / F;
+        const int grid = (int)(need < cap_e ? need : cap_e);
+        hipLaunchKernelGGL((k_fir_pair<N, false>), dim3(grid), dim3(WG), 0, s, lm1, le, H, x, y, n, nch,
+                           x_stride, y_stride, prefix, ecnt, qf, ql, pN, tN, sink);
+    }
     return hipGetLastError();
 }
 

@@ -80,32 +80,6 @@ __device__ __forceinline__ void pair_post(float2 Z, float2 Zm, float2* A, float2
     }
 }
 
-// ---- hand-counted memory pipeline (LDS-DMA input spans) ---------------------
-// hipcc does not track inline-asm memory operations, so the kernel counts them
-// itself: vector-memory ops of a wave retire in issue order (loads, stores and
-// LDS-DMA alike), and the only ops in the loop are these.
-// 16 B per lane global -> LDS (dest = M0 + lane*16; M0 is written in the same
-// statement that uses it, as the compiler reserves it).
-__device__ __forceinline__ void glds16(const float* gsrc, float* lds_dst) {
-    const unsigned l = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_dst);
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(l)
-                 : "memory");
-}
-// The trailing s_nop covers the gfx9 hazard "VALU write of a >8-byte VMEM
-// store's data VGPRs right after the store", which hipcc does not model for asm.
-__device__ __forceinline__ void st16_nt_counted(vf4_t* p, vf4_t v) {
-    asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-template <int CNT>
-__device__ __forceinline__ void vm_wait() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
-}
-__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
 // bin k of an output row (MODE 0: float magnitudes, MODE 1: float2 spectrum)
 template <int MODE>
 __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {

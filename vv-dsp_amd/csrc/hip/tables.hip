@@ -16,7 +16,7 @@ namespace {
 std::mutex g_mu;
 std::map<std::tuple<int, int, long long>, void*> g_cache;   // (device, kind, n) -> device buffer
 
-enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2 };
+enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2, KIND_SINK = 3 };
 
 int current_device() {
     int dev = 0;
@@ -78,6 +78,14 @@ const double2* twiddle_table_d(long long n) {
             wn(k, n, &c, &s);
             h[k] = make_double2(c, s);
         }
+    });
+}
+
+// Write sink for lanes whose store has no destination in a kernel that keeps
+// its count of memory instructions fixed (SINK_FLOATS floats, never read).
+float* store_sink() {
+    return (float*)cached(KIND_SINK, 0, sizeof(float) * SINK_FLOATS, [](unsigned char* b) {
+        for (size_t i = 0; i < sizeof(float) * SINK_FLOATS; ++i) b[i] = 0;
     });
 }
 

@@ -14,6 +14,11 @@ const double2* twiddle_table_d(long long n);
 // Pass-major inter-pass twiddles of the length-n Stockham FFT (fft_core.hpp TwTab).
 const float2* pass_twiddles(int n);
 
+// Write sink (SINK_FLOATS floats): destination of lanes that must issue a store
+// with nothing to write, in kernels that hand-count their memory operations.
+constexpr size_t SINK_FLOATS = 1u << 18;   // 1 MiB = 4096 waves x 64 lanes
+float* store_sink();
+
 // Persistent-grid sizing: resident blocks for `kernel` x CUs, capped by work.
 int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks);
 
