@@ -97,8 +97,22 @@ def case_stft_exp(e, nch=32, seconds=600):
         byts, (sig, win, out, lib)
 
 
+def case_rw(w, in_bytes=3686400000):
+    """streaming read 1 : write w (scripts/membench.hip k_rw), 16 B/lane, nt"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libmembench.so"))
+    lib.membench_rw.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_void_p]
+    n4 = in_bytes // 16
+    a = torch.empty(n4 * 4, device="cuda")
+    b = torch.empty(n4 * 4 * w, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    return (lambda: lib.membench_rw(a.data_ptr(), b.data_ptr(), n4, w, 4096, s)), in_bytes * (1 + w), (a, b, lib)
+
+
 CASES = {
     **{f"ex{e}": (lambda e=e: case_stft_exp(e)) for e in range(8)},
+    "rw1": lambda: case_rw(1), "rw4": lambda: case_rw(4),
     "wr4": lambda: case_wr(0, 0), "wr4nt": lambda: case_wr(0, 1),
     "wrpat": lambda: case_wr(1, 0), "wrpatnt": lambda: case_wr(1, 1),
     "wr8nt": lambda: case_wr(2, 1), "wr16": lambda: case_wr(3, 0), "wr16nt": lambda: case_wr(3, 1),
@@ -120,7 +134,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

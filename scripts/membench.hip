@@ -188,3 +188,23 @@ extern "C" int membench_stft_exp(const float* sig, long long n, long long nch, l
 #undef L
     return (int)hipGetLastError();
 }
+
+// ---- mixed read/write streaming: each lane reads 1 float4 and writes W float4
+// (W = 4: the STFT's 1:4 read:write byte mix; W = 1: copy).
+template <int W>
+__global__ void __launch_bounds__(256) k_rw(const vf4* __restrict__ in, vf4* __restrict__ out, long long n4) {
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+        const vf4 v = __builtin_nontemporal_load(in + i);
+#pragma unroll
+        for (int w = 0; w < W; ++w) __builtin_nontemporal_store(v, out + (long long)w * n4 + i);   // W planes
+    }
+}
+
+extern "C" int membench_rw(const float* in, float* out, long long n4, int w, int blocks, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (w == 1) hipLaunchKernelGGL((k_rw<1>), dim3(blocks), dim3(256), 0, s, (const vf4*)in, (vf4*)out, n4);
+    else if (w == 4) hipLaunchKernelGGL((k_rw<4>), dim3(blocks), dim3(256), 0, s, (const vf4*)in, (vf4*)out, n4);
+    else return -1;
+    return (int)hipGetLastError();
+}

@@ -392,6 +392,26 @@ __device__ __forceinline__ void chunk_of(long long total, long long g, long long
     *hi = *lo + per + (g < rem ? 1 : 0);
 }
 
+// Work sequence of persistent slot `slot` (of F per block) over items [0, total):
+// the block groups blockIdx % 8 (the blocks sharing one XCD and its L2) each
+// take a contiguous share, and inside a group consecutive slots take
+// consecutive items, so a group sweeps its share as one front.  Items that
+// share input lines (overlapping frames, overlap-save halos) are then fetched
+// once into that XCD's L2, and the DRAM sees few open pages at a time.
+// A slot visits first, first + step, ... < end.
+__device__ __forceinline__ void xcd_walk(long long total, int F, int slot, long long* first, long long* end,
+                                         long long* step) {
+    const long long nb = gridDim.x, b = blockIdx.x;
+    const long long ng = nb < 8 ? nb : 8;
+    const long long grp = b % ng;
+    const long long nbg = (nb - grp + ng - 1) / ng;   // blocks in this group
+    long long lo, hi;
+    chunk_of(total, grp, ng, &lo, &hi);
+    *first = lo + (b / ng) * F + slot;
+    *end = hi;
+    *step = nbg * F;
+}
+
 // Workgroup geometry: 256 threads (several transforms per block) unless one
 // transform needs more threads.
 template <int N>

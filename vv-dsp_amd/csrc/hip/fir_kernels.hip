@@ -95,14 +95,20 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
     const long long lout = N - le;
-    long long p, p_end;
-    chunk_of(nch * cnt, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &p, &p_end);
+    long long p, p_end, p_step;
+    xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
+    p_step = uni<G::T>(p_step);
     if (p >= p_end) return;   // uniform per transform (F == 1 whenever T > 64)
-    long long c = p / cnt, idx = p - c * cnt;
-    auto block_of = [&](long long i) { return 2 * (i < qlo ? i : qhi + (i - qlo)); };
-    long long j = block_of(idx);
+    // item -> (channel, first block of the pair)
+    auto locate = [&](long long it, long long* cc, long long* jj) {
+        *cc = it / cnt;
+        const long long i = it - *cc * cnt;
+        *jj = 2 * (i < qlo ? i : qhi + (i - qlo));
+    };
+    long long c, j;
+    locate(p, &c, &j);
     if constexpr (BULK) {
         float* span = span_all + slot * SPAN;
         float* snk = sink + ((((long long)blockIdx.x * (WG / 64) + (lt >> 6)) * 64) % SINK_FLOATS) + (lt & 63);
@@ -116,12 +122,10 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
         };
         issue_span(c, j);
         vm_wait<0>();
-        for (; p < p_end; ++p) {
-            long long cn = c, jn = j + 2;
-            if (jn >= 2 * (qhi + cnt)) {   // bulk launch: qlo == 0, pairs [qhi, qhi+cnt)
-                jn = 2 * qhi;
-                ++cn;
-            }
+        for (; p < p_end; p += p_step) {
+            const bool more = p + p_step < p_end;
+            long long cn = c, jn = j;
+            if (more) locate(p + p_step, &cn, &jn);
             vm_wait<NST>();   // younger than this span's DMA: the previous pair's stores
             if constexpr (G::T > 64) lds_barrier();
             float2 v[G::P];
@@ -129,7 +133,7 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
             for (int r = 0; r < G::P; ++r) v[r] = make_float2(span[t + r * G::T], span[lout + t + r * G::T]);
             lgkm_wait0();
             if constexpr (G::T > 64) lds_barrier();
-            if (p + 1 < p_end) issue_span(cn, jn);
+            if (more) issue_span(cn, jn);
             fft_regs<N, true>(v, t, my, tw);
             float2 u[G::P];
             fir_multiply<N>(v, u, lH, t);
@@ -154,17 +158,16 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
             fir_blk_load<N>(xb, xs, pre, (jj + 1) * lout - le, n, lm1, t);
         };
         load_pair(c, j);
-        for (; p < p_end; ++p) {
+        for (; p < p_end; p += p_step) {
             float2 v[G::P];
 #pragma unroll
             for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
-            long long cn = c, in = idx + 1;
-            if (in >= cnt) {
-                in = 0;
-                ++cn;
+            const bool more = p + p_step < p_end;
+            long long cn = c, jn = j;
+            if (more) {
+                locate(p + p_step, &cn, &jn);
+                load_pair(cn, jn);
             }
-            const long long jn = block_of(in);
-            if (p + 1 < p_end) load_pair(cn, jn);
             fft_regs<N, true>(v, t, my, tw);
             float2 u[G::P];
             fir_multiply<N>(v, u, lH, t);
@@ -181,7 +184,6 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
                 }
             }
             c = cn;
-            idx = in;
             j = jn;
         }
     }

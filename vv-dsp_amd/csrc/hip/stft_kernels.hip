@@ -121,15 +121,20 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * G::T];
 
     const long long pairs = nch * ppc;
-    long long p, p_end;
-    chunk_of(pairs, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &p, &p_end);
+    long long p, p_end, p_step;
+    xcd_walk(pairs, F, slot, &p, &p_end, &p_step);
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
+    p_step = uni<G::T>(p_step);
     if (p >= p_end) return;   // uniform per transform (F == 1 whenever T > 64)
-    // (channel, first frame) of the current pair, advanced without divisions;
-    // this launch covers frames [f_lo, f_hi) of every channel
-    const long long f_lo = 2 * pair0, f_hi = 2 * (pair0 + ppc);
-    long long c = p / ppc, fa = f_lo + 2 * (p - c * ppc);
+    // (channel, first frame) of a pair; this launch covers frames
+    // [2*pair0, 2*(pair0 + ppc)) of every channel
+    auto locate = [&](long long q, long long* cc, long long* ff) {
+        *cc = q / ppc;
+        *ff = 2 * (pair0 + q - *cc * ppc);
+    };
+    long long c, fa;
+    locate(p, &c, &fa);
     float xa[G::P], xb[G::P];
     // GLDS: the pair's span [fa*hop, fa*hop + hop + N) goes HBM/L2 -> LDS by
     // 16 B/lane LDS-DMA, issued right after the previous span was read, so it
@@ -166,13 +171,10 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
 #pragma unroll
     for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
     constexpr long long ES = MODE == 0 ? 4 : 8;
-    for (; p < p_end; ++p) {
-        long long cn = c, fn = fa + 2;
-        if (fn >= f_hi) {
-            fn = f_lo;
-            ++cn;
-        }
-        const bool more = p + 1 < p_end;
+    for (; p < p_end; p += p_step) {
+        const bool more = p + p_step < p_end;
+        long long cn = c, fn = fa;
+        if (more) locate(p + p_step, &cn, &fn);
         if constexpr (GLDS) {
             // younger than this span's DMA: only the previous pair's NST stores
             vm_wait<NST>();
@@ -302,10 +304,11 @@ k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, l
 #pragma unroll
     for (int r = 0; r < G::P; ++r) w[r] = make_float2(win[2 * (t + r * G::T)], win[2 * (t + r * G::T) + 1]);
     const long long items = nch * frames;
-    long long it, it_end;
-    chunk_of(items, (long long)blockIdx.x * F + slot, (long long)gridDim.x * F, &it, &it_end);
+    long long it, it_end, it_step;
+    xcd_walk(items, F, slot, &it, &it_end, &it_step);
     it = uni<G::T>(it);
     it_end = uni<G::T>(it_end);
+    it_step = uni<G::T>(it_step);
     float2 nx[G::P];
     auto load = [&](long long i2) {
         const long long c = i2 / frames, fr = i2 - c * frames;
@@ -318,12 +321,12 @@ k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, l
         }
     };
     if (it < it_end) load(it);
-    for (; it < it_end; ++it) {
+    for (; it < it_end; it += it_step) {
         const long long c = it / frames, fr = it - c * frames;
         float2 v[G::P];
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = make_float2(nx[r].x * w[r].x, nx[r].y * w[r].y);
-        if (it + 1 < it_end) load(it + 1);
+        if (it + it_step < it_end) load(it + it_step);
         fft_regs<M, true, PAIR>(v, t, my, tw);
         const long long row = c * out_ch_stride + fr * (long long)NR;
         float2 A[G::P], B[G::P];
