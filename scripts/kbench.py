@@ -97,7 +97,7 @@ def case_stft_exp(e, nch=32, seconds=600):
         byts, (sig, win, out, lib)
 
 
-def case_rw(w, in_bytes=3686400000):
+def case_rw(w, in_bytes=3686400000, blocks=4096):
     """streaming read 1 : write w (scripts/membench.hip k_rw), 16 B/lane, nt"""
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libmembench.so"))
@@ -107,12 +107,13 @@ def case_rw(w, in_bytes=3686400000):
     a = torch.empty(n4 * 4, device="cuda")
     b = torch.empty(n4 * 4 * w, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    return (lambda: lib.membench_rw(a.data_ptr(), b.data_ptr(), n4, w, 4096, s)), in_bytes * (1 + w), (a, b, lib)
+    return (lambda: lib.membench_rw(a.data_ptr(), b.data_ptr(), n4, w, blocks, s)), in_bytes * (1 + w), (a, b, lib)
 
 
 CASES = {
     **{f"ex{e}": (lambda e=e: case_stft_exp(e)) for e in range(8)},
     "rw1": lambda: case_rw(1), "rw4": lambda: case_rw(4),
+    **{f"rw{w}b{b}": (lambda w=w, b=b: case_rw(w, blocks=b)) for w in (1, 4) for b in (256, 512, 1024, 2048, 16384)},
     "wr4": lambda: case_wr(0, 0), "wr4nt": lambda: case_wr(0, 1),
     "wrpat": lambda: case_wr(1, 0), "wrpatnt": lambda: case_wr(1, 1),
     "wr8nt": lambda: case_wr(2, 1), "wr16": lambda: case_wr(3, 0), "wr16nt": lambda: case_wr(3, 1),

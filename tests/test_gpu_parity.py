@@ -74,6 +74,54 @@ def test_r2c_c2r_vs_numpy(amd, orc, n):
     kiss_check(X, orc.fft(xr, R2C), np.fft.rfft(xr.astype(np.float64)), n)
 
 
+def _normwise(y, ref):
+    return float(np.max(np.abs(y - ref)) / np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("n", [8192, 16384, 1 << 16, 1 << 20])
+def test_c2c_large_pow2(amd, n):
+    """Power-of-two lengths above one workgroup's FFT (four-step path).  The
+    reference's radix-2 Kiss covers every power of two (fft_kiss.c:27-74) but is
+    itself outside the harness bound from n = 4096, so the bound
+    here is normwise: within 4x the error of an f32 FFT (scipy.fft, single
+    precision) against f64, and a round trip back to the input."""
+    import scipy.fft
+    rng = np.random.default_rng(n)
+    x = (rng.random(n) - 0.5 + 1j * (rng.random(n) - 0.5)).astype(np.complex64)
+    ref = np.fft.fft(x.astype(np.complex128))
+    y = amd.fft(x, C2C, FWD)
+    e32 = _normwise(scipy.fft.fft(x), ref)
+    assert _normwise(y, ref) <= max(4 * e32, 1e-6), (_normwise(y, ref), e32)
+    xb = amd.fft(y, C2C, BWD)
+    assert _normwise(xb, x) <= 1e-5
+    refb = np.fft.ifft(x.astype(np.complex128))
+    assert _normwise(amd.fft(x, C2C, BWD), refb) <= max(4 * _normwise(scipy.fft.ifft(x), refb), 1e-6)
+
+
+@pytest.mark.parametrize("n", [16384, 1 << 18])
+def test_real_large_pow2(amd, n):
+    import scipy.fft
+    rng = np.random.default_rng(n + 7)
+    xr = (rng.random(n) - 0.5).astype(np.float32)
+    ref = np.fft.rfft(xr.astype(np.float64))
+    X = amd.fft(xr, R2C)
+    assert X.shape == (n // 2 + 1,) and X[-1].imag == 0.0
+    assert _normwise(X, ref) <= max(4 * _normwise(scipy.fft.rfft(xr), ref), 1e-6)
+    y = amd.fft(X, C2R, BWD, n=n)
+    assert _normwise(y, xr) <= 1e-5
+
+
+def test_large_pow2_batched_device(vdev):
+    import torch
+    rng = np.random.default_rng(9)
+    n, b = 16384, 3
+    x = (rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)
+    plan = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)
+    y = plan(torch.from_numpy(x).cuda()).cpu().numpy()
+    ref = np.fft.fft(x.astype(np.complex128), axis=1)
+    assert _normwise(y, ref) <= 2e-6
+
+
 def test_impulse_known_answer(amd):
     """tests/fft_backend_tests.c:70-99 and spectral_tests.c:14-35 of the reference."""
     for n in (8, 16, 1024):
@@ -158,6 +206,19 @@ def test_stft_vs_oracle(amd, orc, nfft, hop):
         pad = np.concatenate([x.astype(np.float64), np.zeros(nfft, np.float64)])
         np_mag = np.abs(np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1))
         close(mag, np_mag, factor=1.0 if nfft <= 1024 else 4.0)
+
+
+def test_stft_large_nfft(amd, orc):
+    """nfft above the fused kernels (16384: frame gather + four-step FFT)."""
+    nfft, hop = 16384, 4096
+    x = np.random.default_rng(77).uniform(-1, 1, 3 * nfft + 11).astype(np.float32)
+    mag = amd.spectrogram(x, nfft, hop)
+    ref = orc.spectrogram(x, nfft, hop)
+    assert mag.shape == ref.shape
+    w = orc.window(1, nfft).astype(np.float64)
+    pad = np.concatenate([x.astype(np.float64), np.zeros(nfft)])
+    np_mag = np.abs(np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(ref.shape[0])]) * w, axis=1))
+    assert _normwise(mag, np_mag) <= 2e-6
 
 
 def test_stft_process_and_reconstruct(amd, orc):

@@ -128,7 +128,11 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
             if (in != out) HIPCHK(hipMemcpyAsync(out, in, 8 * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
             return ST_OK;
         }
-        if (is_pow2(n)) return fail(ST_UNSUP, "C2C power-of-two length > 4096 not supported yet");
+        if (is_pow2(n)) {
+            if (!c2c_large_supported(N)) return fail(ST_UNSUP, "C2C power-of-two length > 2^24 not supported");
+            HIPCHK(launch_c2c_large(N, fwd, (const float2*)in, (float2*)out, B, s), ST_INTERNAL);
+            return ST_OK;
+        }
         const void* src = in;
         Scratch tmp(s);
         if (in == out) {
@@ -146,7 +150,17 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
             HIPCHK(launch_r2c(N, (const float*)in, (float2*)out, B, N, NH, s), ST_INTERNAL);
             return ST_OK;
         }
-        if (is_pow2(n) && n > 8192) return fail(ST_UNSUP, "R2C power-of-two length > 8192 not supported yet");
+        if (is_pow2(n) && n > 8192) {   // promote, four-step C2C, keep bins 0..n/2 (fft_kiss.c:120-147)
+            if (!c2c_large_supported(N)) return fail(ST_UNSUP, "R2C power-of-two length > 2^24 not supported");
+            Scratch z(s), Z(s);
+            HIPCHK(z.alloc(8 * n * batch), ST_INTERNAL);
+            HIPCHK(Z.alloc(8 * n * batch), ST_INTERNAL);
+            HIPCHK(launch_promote_real((const float*)in, (float2*)z.p, N * B, s), ST_INTERNAL);
+            HIPCHK(launch_c2c_large(N, 1, (const float2*)z.p, (float2*)Z.p, B, s), ST_INTERNAL);
+            HIPCHK(hipMemcpy2DAsync(out, 8 * NH, Z.p, 8 * n, 8 * NH, batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+            HIPCHK(launch_zero_nyquist_imag((float2*)out, N, B, NH, s), ST_INTERNAL);
+            return ST_OK;
+        }
         HIPCHK(launch_dft_naive(N, 1, in, 1, (float2*)out, NH, B, N, NH, 1.0f, s), ST_INTERNAL);
         HIPCHK(launch_zero_nyquist_imag((float2*)out, N, B, NH, s), ST_INTERNAL);
         return ST_OK;
@@ -156,12 +170,16 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
         HIPCHK(launch_c2r(N, (const float2*)in, (float*)out, B, NH, N, s), ST_INTERNAL);
         return ST_OK;
     }
-    if (is_pow2(n) && n > 8192) return fail(ST_UNSUP, "C2R power-of-two length > 8192 not supported yet");
+    if (is_pow2(n) && n > 8192 && !c2c_large_supported(N))
+        return fail(ST_UNSUP, "C2R power-of-two length > 2^24 not supported");
     Scratch full(s), tim(s);
     HIPCHK(full.alloc(8 * n * batch), ST_INTERNAL);
     HIPCHK(tim.alloc(8 * n * batch), ST_INTERNAL);
     HIPCHK(launch_hermitian_expand(N, (const float2*)in, (float2*)full.p, B, NH, 0, s), ST_INTERNAL);
-    HIPCHK(launch_dft_naive(N, 0, full.p, 0, (float2*)tim.p, N, B, N, N, 1.0f / (float)N, s), ST_INTERNAL);
+    if (is_pow2(n) && n > 8192)   // Hermitian expand (fft_kiss.c:149-174), four-step inverse
+        HIPCHK(launch_c2c_large(N, 0, (const float2*)full.p, (float2*)tim.p, B, s), ST_INTERNAL);
+    else
+        HIPCHK(launch_dft_naive(N, 0, full.p, 0, (float2*)tim.p, N, B, N, N, 1.0f / (float)N, s), ST_INTERNAL);
     HIPCHK(launch_take_real((const float2*)tim.p, (float*)out, N * B, s), ST_INTERNAL);
     return ST_OK;
 }
@@ -209,8 +227,7 @@ int vvhip_fft_plan_create(size_t n, int type, int dir, size_t batch, vvhip_fft**
     if (n == 0 || batch == 0) return ST_SIZE;
     if (type < 0 || type > 2 || (dir != 1 && dir != -1)) return ST_RANGE;
     if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
-    if (type == 0 && is_pow2(n) && n > 4096) return fail(ST_UNSUP, "C2C pow2 > 4096 not supported yet");
-    if (type != 0 && is_pow2(n) && n > 8192) return fail(ST_UNSUP, "real pow2 > 8192 not supported yet");
+    if (is_pow2(n) && n > (1u << 24)) return fail(ST_UNSUP, "power-of-two length > 2^24 not supported");
     vvhip_fft* p = new (std::nothrow) vvhip_fft;
     if (!p) return ST_INTERNAL;
     p->n = n;
@@ -275,7 +292,6 @@ static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch
         return ST_OK;
     }
     // generic nfft: gather windowed complex frames, batched C2C, magnitude
-    if (is_pow2(h->nfft) && h->nfft > 4096) return fail(ST_UNSUP, "STFT nfft > 8192 not supported yet");
     for (size_t c = 0; c < nch; ++c) {
         Scratch fr(s);
         const size_t cnt = frames * h->nfft;

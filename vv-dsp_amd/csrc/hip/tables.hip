@@ -16,7 +16,7 @@ namespace {
 std::mutex g_mu;
 std::map<std::tuple<int, int, long long>, void*> g_cache;   // (device, kind, n) -> device buffer
 
-enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2, KIND_SINK = 3 };
+enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2, KIND_SINK = 3, KIND_SPLIT = 4 };
 
 int current_device() {
     int dev = 0;
@@ -77,6 +77,28 @@ const double2* twiddle_table_d(long long n) {
             double c, s;
             wn(k, n, &c, &s);
             h[k] = make_double2(c, s);
+        }
+    });
+}
+
+// Two-level W_n^k for large n: lo[j] = W_n^j (j < 2^lo_bits), then
+// hi[j] = W_n^(j << lo_bits) (j < n >> lo_bits); W_n^k = lo[k & mask] * hi[k >> lo_bits].
+const float2* twiddle_split(long long n, int* lo_bits) {
+    int lg = 0;
+    while ((1LL << lg) < n) ++lg;
+    const int lb = (lg + 1) / 2;
+    *lo_bits = lb;
+    const long long nlo = 1LL << lb, nhi = n >> lb;
+    return (const float2*)cached(KIND_SPLIT, n, sizeof(float2) * (nlo + nhi), [=](unsigned char* b) {
+        float2* h = reinterpret_cast<float2*>(b);
+        double c, s;
+        for (long long j = 0; j < nlo; ++j) {
+            wn(j, n, &c, &s);
+            h[j] = make_float2((float)c, (float)s);
+        }
+        for (long long j = 0; j < nhi; ++j) {
+            wn(j << lb, n, &c, &s);
+            h[nlo + j] = make_float2((float)c, (float)s);
         }
     });
 }

@@ -14,6 +14,16 @@ const double2* twiddle_table_d(long long n);
 // Pass-major inter-pass twiddles of the length-n Stockham FFT (fft_core.hpp TwTab).
 const float2* pass_twiddles(int n);
 
+// Two-level table for large n (large_fft.hip): lo[2^lo_bits] ++ hi[n >> lo_bits].
+const float2* twiddle_split(long long n, int* lo_bits);
+
+// ---- large power-of-two C2C (large_fft.hip): four-step over the fused kernels
+bool c2c_large_supported(long long n);     // pow2, 8192 .. 2^24
+hipError_t launch_c2c_large(long long n, int fwd, const float2* in, float2* out, long long batch,
+                            hipStream_t s);
+// real[batch][n] -> complex[batch][n] (imaginary 0)
+hipError_t launch_promote_real(const float* in, float2* out, long long count, hipStream_t s);
+
 // Write sink (SINK_FLOATS floats): destination of lanes that must issue a store
 // with nothing to write, in kernels that hand-count their memory operations.
 constexpr size_t SINK_FLOATS = 1u << 18;   // 1 MiB = 4096 waves x 64 lanes
