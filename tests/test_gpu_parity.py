@@ -111,6 +111,36 @@ def test_real_large_pow2(amd, n):
     assert _normwise(y, xr) <= 1e-5
 
 
+@pytest.mark.parametrize("n", [1025, 3000, 48000, 100003])
+def test_c2c_bluestein(amd, orc, n):
+    """Non-power-of-two lengths from 1025 on run Bluestein over the power-of-two
+    kernels (the reference: an O(n^2) f32 DFT, fft_kiss.c:76-92).  Normwise
+    within 8x an f32 FFT's error vs f64, and for the lengths the CPU oracle
+    finishes quickly, at least as close to f64 as the reference's own result."""
+    import scipy.fft
+    rng = np.random.default_rng(n)
+    x = (rng.random(n) - 0.5 + 1j * (rng.random(n) - 0.5)).astype(np.complex64)
+    for d, npf, spf in ((FWD, np.fft.fft, scipy.fft.fft), (BWD, np.fft.ifft, scipy.fft.ifft)):
+        ref = npf(x.astype(np.complex128))
+        y = amd.fft(x, C2C, d)
+        e, e32 = _normwise(y, ref), _normwise(spf(x), ref)
+        assert e <= max(8 * e32, 2e-6), (d, e, e32)
+        if n <= 3000:
+            assert e <= _normwise(orc.fft(x, C2C, d), ref)
+    assert _normwise(amd.fft(amd.fft(x, C2C, FWD), C2C, BWD), x) <= 1e-5
+
+
+@pytest.mark.parametrize("n", [1500, 48000])
+def test_real_bluestein(amd, n):
+    import scipy.fft
+    rng = np.random.default_rng(n + 3)
+    xr = (rng.random(n) - 0.5).astype(np.float32)
+    ref = np.fft.rfft(xr.astype(np.float64))
+    X = amd.fft(xr, R2C)
+    assert _normwise(X, ref) <= max(8 * _normwise(scipy.fft.rfft(xr), ref), 2e-6)
+    assert _normwise(amd.fft(X, C2R, BWD, n=n), xr) <= 1e-5
+
+
 def test_large_pow2_batched_device(vdev):
     import torch
     rng = np.random.default_rng(9)

@@ -114,6 +114,15 @@ static size_t fft_out_elems_bytes(const vvhip_fft* p) {
     }
 }
 
+// Non-power-of-two DFT: the exact-angle f64 O(n^2) kernel for short lengths,
+// Bluestein over the power-of-two kernels from BLUESTEIN_MIN on.
+static hipError_t dft_any(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
+                          long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s) {
+    if (n >= BLUESTEIN_MIN && bluestein_supported(n))
+        return launch_bluestein(n, fwd, in, real_in, out, nout, batch, in_dist, out_dist, scale, s);
+    return launch_dft_naive(n, fwd, in, real_in, out, nout, batch, in_dist, out_dist, scale, s);
+}
+
 // Core device dispatch: `batch` transforms, contiguous, device pointers.
 static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_t batch, hipStream_t s) {
     const long long N = (long long)n, B = (long long)batch;
@@ -140,7 +149,7 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
             HIPCHK(hipMemcpyAsync(tmp.p, in, 8 * n * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
             src = tmp.p;
         }
-        HIPCHK(launch_dft_naive(N, fwd, src, 0, (float2*)out, N, B, N, N, fwd ? 1.0f : 1.0f / (float)N, s),
+        HIPCHK(dft_any(N, fwd, src, 0, (float2*)out, N, B, N, N, fwd ? 1.0f : 1.0f / (float)N, s),
                ST_INTERNAL);
         return ST_OK;
     }
@@ -161,7 +170,7 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
             HIPCHK(launch_zero_nyquist_imag((float2*)out, N, B, NH, s), ST_INTERNAL);
             return ST_OK;
         }
-        HIPCHK(launch_dft_naive(N, 1, in, 1, (float2*)out, NH, B, N, NH, 1.0f, s), ST_INTERNAL);
+        HIPCHK(dft_any(N, 1, in, 1, (float2*)out, NH, B, N, NH, 1.0f, s), ST_INTERNAL);
         HIPCHK(launch_zero_nyquist_imag((float2*)out, N, B, NH, s), ST_INTERNAL);
         return ST_OK;
     }
@@ -179,7 +188,7 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
     if (is_pow2(n) && n > 8192)   // Hermitian expand (fft_kiss.c:149-174), four-step inverse
         HIPCHK(launch_c2c_large(N, 0, (const float2*)full.p, (float2*)tim.p, B, s), ST_INTERNAL);
     else
-        HIPCHK(launch_dft_naive(N, 0, full.p, 0, (float2*)tim.p, N, B, N, N, 1.0f / (float)N, s), ST_INTERNAL);
+        HIPCHK(dft_any(N, 0, full.p, 0, (float2*)tim.p, N, B, N, N, 1.0f / (float)N, s), ST_INTERNAL);
     HIPCHK(launch_take_real((const float2*)tim.p, (float*)out, N * B, s), ST_INTERNAL);
     return ST_OK;
 }

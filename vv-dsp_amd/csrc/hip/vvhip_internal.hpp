@@ -21,6 +21,12 @@ const float2* twiddle_split(long long n, int* lo_bits);
 bool c2c_large_supported(long long n);     // pow2, 8192 .. 2^24
 hipError_t launch_c2c_large(long long n, int fwd, const float2* in, float2* out, long long batch,
                             hipStream_t s);
+// Bluestein (chirp-z) for any n with pow2(2n-1) <= 2^24; same contract as
+// launch_dft_naive (real_in promotes real input; nout bins written).
+constexpr long long BLUESTEIN_MIN = 1025;   // below: the f64 O(n^2) DFT (exact-angle, faster at small n)
+bool bluestein_supported(long long n);
+hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
+                            long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s);
 // real[batch][n] -> complex[batch][n] (imaginary 0)
 hipError_t launch_promote_real(const float* in, float2* out, long long count, hipStream_t s);
 
