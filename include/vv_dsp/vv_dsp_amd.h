@@ -11,6 +11,7 @@
 #include "vv_dsp/spectral/stft.h"
 #include "vv_dsp/spectral/dct.h"
 #include "vv_dsp/filter/fir.h"
+#include "vv_dsp/features/mel.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -37,6 +38,12 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_spectrum_device(vv_dsp_stft* h, const
                                                            size_t n, size_t nch, size_t ch_stride,
                                                            vv_dsp_cpx* d_out, size_t out_ch_stride,
                                                            void* stream, size_t* out_frames);
+/* power spectrogram [ch][frame][fft_size/2+1] = re^2 + im^2 of bins 0..fft_size/2
+ * (the input of vv_dsp_compute_log_mel_spectrogram / vv_dsp_mfcc_process) */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_power_device(vv_dsp_stft* h, const vv_dsp_real* d_signal,
+                                                        size_t n, size_t nch, size_t ch_stride,
+                                                        vv_dsp_real* d_out_power, size_t out_ch_stride,
+                                                        void* stream, size_t* out_frames);
 /* count frames real[count][fft_size] -> cpx[count][fft_size] (vv_dsp_stft_process batched) */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_process_device(vv_dsp_stft* h, const vv_dsp_real* d_frames,
                                                           size_t count, vv_dsp_cpx* d_spec, void* stream);
@@ -64,6 +71,14 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_hilbert_analytic_device(const vv_dsp_real*
 /* DCT of `batch` contiguous rows with the plan's type/direction */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dct_execute_device(const vv_dsp_dct_plan* plan, const vv_dsp_real* d_in,
                                                          vv_dsp_real* d_out, size_t batch, void* stream);
+
+/* MFCC plan (vv_dsp_mfcc_init) on device rows: power [frames][n_fft/2+1]
+ * (e.g. vv_dsp_stft_power_device) -> MFCC [frames][num_mfcc_coeffs], or ->
+ * log-mel [frames][n_mels]; one fused kernel, the spectrogram read once. */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_mfcc_process_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
+                                                          size_t num_frames, vv_dsp_real* d_out_mfcc, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_log_mel_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
+                                                     size_t num_frames, vv_dsp_real* d_out_log_mel, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,6 +37,7 @@ extern "C" {
 typedef struct vvhip_fft vvhip_fft;
 typedef struct vvhip_stft vvhip_stft;
 typedef struct vvhip_fir vvhip_fir;
+typedef struct vvhip_mel vvhip_mel;
 
 /* Number of usable HIP devices (0 when none: every other call then fails). */
 int vvhip_available(void);
@@ -69,11 +70,14 @@ void vvhip_stft_destroy(vvhip_stft* h);
 /* frames = n < nfft ? 1 : 1 + (n - nfft + hop) / hop   (stft.c:119) */
 size_t vvhip_stft_num_frames(size_t n, size_t nfft, size_t hop);
 int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, float* out_mag);
-/* nch channels at ch_stride floats; magnitudes [ch][frame][nfft] at out_ch_stride floats.
- * complex_out != 0 writes the full complex spectrum rows (float pairs) instead. */
+/* nch channels at ch_stride floats; rows [ch][frame][...] at out_ch_stride elements.
+ * out_kind 0: magnitudes sqrtf(re^2+im^2) of all nfft bins (stft.c:133-139);
+ *          1: the full complex spectrum (float pairs, stft_process semantics);
+ *          2: power re^2+im^2 of bins 0..nfft/2 (nfft/2+1 floats per row; the
+ *             power spectrogram vv_dsp_compute_log_mel_spectrogram consumes). */
 int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
                                   size_t ch_stride, void* d_out, size_t out_ch_stride,
-                                  int complex_out, void* stream);
+                                  int out_kind, void* stream);
 int vvhip_stft_process_host(vvhip_stft* h, const float* frame, float* spec_out);
 int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count, float* d_spec,
                               void* stream);
@@ -95,6 +99,19 @@ int vvhip_fir_apply_host(vvhip_fir* f, const float* x, float* y, size_t n, const
 int vvhip_fir_apply_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n, size_t nch,
                            size_t x_stride, size_t y_stride, const float* d_prefix, int mode,
                            void* stream);
+/* ---- Mel / MFCC (src/features/mel.c:204-309) ----
+ * fb: dense filterbank [n_mels][nbins] (vv_dsp_mel_filterbank_create), or NULL
+ * for a plan that only maps log-mel rows to MFCC (kind 2).  n_coeffs: MFCC
+ * coefficients (0 = log-mel only); lifter as mel.c:298-304; eps added before log. */
+int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coeffs, float lifter, float eps,
+                     vvhip_mel** out);
+void vvhip_mel_destroy(vvhip_mel* m);
+/* kind 0: power rows [frames][nbins] -> log-mel [frames][n_mels]
+ *      1: power rows -> MFCC [frames][n_coeffs]
+ *      2: log-mel rows [frames][n_mels] -> MFCC [frames][n_coeffs] */
+int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_out, int kind, void* stream);
+int vvhip_mel_host(vvhip_mel* m, const float* in, size_t frames, float* out, int kind);
+
 /* Block length (real FFT size) the overlap-save path uses for a signal of n samples. */
 size_t vvhip_fir_block_size(vvhip_fir* f, size_t n);
 

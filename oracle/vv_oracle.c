@@ -378,3 +378,96 @@ int orc_fir_apply_fft(const float* h, size_t taps, const float* x, float* y, siz
     free(xb); free(hb); free(X); free(H); free(Y);
     return 0;
 }
+
+/* ---- mel / MFCC (src/features/mel.c) ------------------------------------- */
+/* mel.c:14-20 */
+float orc_hz_to_mel(float hz) {
+    if (hz < 0.0f) return 0.0f;
+    return 2595.0f * log10f(1.0f + hz / 700.0f);
+}
+
+/* mel.c:22-28 (VV_DSP_POW = powf, vv_dsp_math.h:48) */
+float orc_mel_to_hz(float mel) {
+    if (mel < 0.0f) return 0.0f;
+    return 700.0f * (powf(10.0f, mel / 2595.0f) - 1.0f);
+}
+
+/* mel.c:51-62 */
+static size_t orc_searchsorted(const float* a, size_t n, float v) {
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+        const size_t mid = lo + (hi - lo) / 2;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* mel.c:66-193 (HTK only, as the reference).  fb: n_mels x (n_fft/2+1), caller-owned. */
+int orc_mel_filterbank(size_t n_fft, size_t n_mels, float sample_rate, float fmin, float fmax, float* fb) {
+    if (!fb) return 1;
+    if (n_fft == 0 || n_mels == 0 || sample_rate <= 0.0f || fmin < 0.0f || fmax <= fmin) return 2;
+    if (fmax > sample_rate / 2.0f) return 3;
+    const size_t nb = n_fft / 2 + 1;
+    if (n_mels >= nb) return 2;
+    memset(fb, 0, n_mels * nb * sizeof(float));
+    const float mel_min = orc_hz_to_mel(fmin), mel_max = orc_hz_to_mel(fmax);
+    const size_t np = n_mels + 2;
+    float* mel = (float*)malloc(np * sizeof(float));
+    float* hz = (float*)malloc(np * sizeof(float));
+    float* ff = (float*)malloc(nb * sizeof(float));
+    if (!mel || !hz || !ff) { free(mel); free(hz); free(ff); return 4; }
+    const float step = (mel_max - mel_min) / (float)(np - 1);   /* linspace, mel.c:35-46 */
+    for (size_t i = 0; i < np; ++i) mel[i] = mel_min + step * (float)i;
+    for (size_t i = 0; i < np; ++i) hz[i] = orc_mel_to_hz(mel[i]);
+    for (size_t i = 0; i < nb; ++i) ff[i] = (float)i * sample_rate / (float)n_fft;
+    for (size_t m = 0; m < n_mels; ++m) {
+        const float left = hz[m], center = hz[m + 1], right = hz[m + 2];
+        const size_t li = orc_searchsorted(ff, nb, left), ci = orc_searchsorted(ff, nb, center),
+                     ri = orc_searchsorted(ff, nb, right);
+        float* row = fb + m * nb;
+        for (size_t k = li; k < ci && k < nb; ++k) row[k] = (ff[k] - left) / (center - left);
+        for (size_t k = ci; k < ri && k < nb; ++k) row[k] = (right - ff[k]) / (right - center);
+        float sum = 0.0f;
+        for (size_t k = 0; k < nb; ++k) sum += row[k];
+        if (sum > 0.0f)
+            for (size_t k = 0; k < nb; ++k) row[k] /= sum;
+    }
+    free(mel); free(hz); free(ff);
+    return 0;
+}
+
+/* mel.c:204-245 (VV_DSP_LOG = logf) */
+int orc_log_mel(const float* power, size_t frames, size_t nb, const float* fb, size_t n_mels, float eps,
+                float* out) {
+    if (!power || !fb || !out) return 1;
+    if (frames == 0 || nb == 0 || n_mels == 0) return 2;
+    if (eps < 0.0f) return 3;
+    for (size_t f = 0; f < frames; ++f)
+        for (size_t m = 0; m < n_mels; ++m) {
+            float e = 0.0f;
+            for (size_t k = 0; k < nb; ++k) e += power[f * nb + k] * fb[m * nb + k];
+            out[f * n_mels + m] = logf(e + eps);
+        }
+    return 0;
+}
+
+/* mel.c:249-309: DCT-II (dct.c forward) per frame, first n_coeffs, lifter (VV_DSP_SIN = sinf) */
+int orc_mfcc(const float* log_mel, size_t frames, size_t n_mels, size_t n_coeffs, float lifter, float* out) {
+    if (!log_mel || !out) return 1;
+    if (frames == 0 || n_mels == 0 || n_coeffs == 0 || n_coeffs > n_mels) return 2;
+    if (lifter < 0.0f) return 3;
+    float* d = (float*)malloc(n_mels * sizeof(float));
+    if (!d) return 4;
+    for (size_t f = 0; f < frames; ++f) {
+        const int st = orc_dct(log_mel + f * n_mels, d, n_mels, 2, 1);
+        if (st) { free(d); return st; }
+        float* o = out + f * n_coeffs;
+        for (size_t i = 0; i < n_coeffs; ++i) o[i] = d[i];
+        if (lifter > 0.0f)
+            for (size_t i = 1; i < n_coeffs; ++i)
+                o[i] *= 1.0f + (lifter / 2.0f) * sinf((float)M_PI * (float)i / lifter);
+    }
+    free(d);
+    return 0;
+}

@@ -52,6 +52,16 @@ int orc_fir_apply(const float* h, size_t taps, float* history, size_t* hist_idx,
 /* Single-block FFT convolution exactly as :75-135 (its C2R is O(Nfft^2): small n only). */
 int orc_fir_apply_fft(const float* h, size_t taps, const float* x, float* y, size_t n);
 
+/* Mel / MFCC (src/features/mel.c; HTK variant, the only one the reference builds) */
+float orc_hz_to_mel(float hz);                                            /* :14-20 */
+float orc_mel_to_hz(float mel);                                           /* :22-28 */
+int orc_mel_filterbank(size_t n_fft, size_t n_mels, float sample_rate, float fmin, float fmax,
+                       float* fb);                                        /* :66-193 */
+int orc_log_mel(const float* power, size_t frames, size_t nb, const float* fb, size_t n_mels,
+                float eps, float* out);                                   /* :204-245 */
+int orc_mfcc(const float* log_mel, size_t frames, size_t n_mels, size_t n_coeffs, float lifter,
+             float* out);                                                 /* :249-309 */
+
 #ifdef __cplusplus
 }
 #endif

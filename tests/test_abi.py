@@ -98,6 +98,39 @@ def test_fir_design_bitexact_host_setup(cpu_lib, orc):
                                   equal_nan=True)
 
 
+def test_mel_filterbank_bitexact_host_setup(cpu_lib, orc, ref):
+    """The mel filterbank and conversions are host setup with the reference's
+    arithmetic (mel.c:14-193): bit-identical to the reference and the oracle."""
+    import numpy as np
+    for hz in (0.0, 440.0, 8000.0, -1.0):
+        assert cpu_lib.hz_to_mel(hz) == ref.hz_to_mel(hz)
+        assert cpu_lib.mel_to_hz(hz) == ref.mel_to_hz(hz)
+    for args in ((512, 26, 16000.0, 0.0, 8000.0), (1024, 40, 48000.0, 20.0, 20000.0), (2048, 128, 44100.0, 0.0,
+                                                                                        22050.0)):
+        st, fb = cpu_lib.mel_filterbank(*args)
+        st_r, fb_r = ref.mel_filterbank(*args)
+        assert st == st_r == 0 and np.array_equal(fb, fb_r) and np.array_equal(fb, orc.mel_filterbank(*args)[1])
+    # argument errors are the reference's codes (mel.c:78-98): size, range, variant
+    for bad in ((512, 300, 16000.0, 0.0, 8000.0), (512, 26, 16000.0, 0.0, 9000.0), (0, 26, 16000.0, 0.0, 8000.0)):
+        assert cpu_lib.mel_filterbank(*bad)[0] == ref.mel_filterbank(*bad)[0]
+    assert cpu_lib.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0, variant=1)[0] == \
+        ref.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0, variant=1)[0] == ERR_RANGE
+
+
+def test_no_gpu_mel_fails_loudly(cpu_lib):
+    """The per-frame mel/MFCC work has no CPU path: without a device it reports UNSUPPORTED."""
+    import numpy as np
+    if not _no_gpu(cpu_lib):
+        pytest.skip("a GPU is visible")
+    st, fb = cpu_lib.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)
+    assert st == OK
+    power = np.ones((2, 257), np.float32)
+    for call in (lambda: cpu_lib.log_mel(power, fb, 1e-10), lambda: cpu_lib.mfcc(np.ones((2, 26), np.float32), 13, 0.0),
+                 lambda: cpu_lib.mfcc_pipeline(power, 512, 26, 13, 16000.0, 0.0, 8000.0, 22.0, 1e-10)):
+        with pytest.raises(RuntimeError, match="status 6"):
+            call()
+
+
 def test_no_gpu_fails_loudly(cpu_lib):
     if not _no_gpu(cpu_lib):
         pytest.skip("a GPU is visible")

@@ -422,3 +422,84 @@ def test_dct_roundtrip_known_answer(amd):
     np.testing.assert_allclose(amd.dct(amd.dct(x, 2), 2, True), x, atol=1e-5)
     x4 = np.cos(2 * np.pi * (np.arange(n) + 0.3) / n).astype(np.float32)
     np.testing.assert_allclose(amd.dct(amd.dct(x4, 4), 4, True), x4, atol=1e-5)
+
+
+# ---------------------------------------------------------------- mel / MFCC
+MEL = [(512, 26, 16000.0, 0.0, 8000.0), (1024, 40, 48000.0, 20.0, 20000.0), (2048, 128, 44100.0, 0.0, 22050.0)]
+
+
+def test_mfcc_reference_tests(amd):
+    """tests/mfcc_tests.c of the reference, restated."""
+    for hz in (0.0, 100.0, 1000.0, 4000.0, 8000.0):
+        assert abs(amd.mel_to_hz(amd.hz_to_mel(hz)) - hz) <= 1e-3 * max(1.0, hz)
+    assert amd.hz_to_mel(-100.0) == 0.0 and amd.mel_to_hz(-100.0) == 0.0
+    st, fb = amd.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)
+    assert st == OK and fb.shape == (26, 257) and (fb > 0).any()
+    power = (1.0 / (1.0 + np.arange(257, dtype=np.float32))).astype(np.float32)[None, :]
+    m = amd.mfcc_pipeline(power, 512, 26, 13, 16000.0, 0.0, 8000.0, 22.0, 1e-10)
+    assert m.shape == (1, 13) and np.isfinite(m).all()
+
+
+@pytest.mark.parametrize("args", MEL)
+def test_log_mel_and_mfcc_vs_oracle(amd, orc, args):
+    n_fft, n_mels = args[0], args[1]
+    st, fb = orc.mel_filterbank(*args)
+    assert st == 0
+    rng = np.random.default_rng(n_mels)
+    power = ((rng.random((37, n_fft // 2 + 1)) ** 2) * 10).astype(np.float32)
+    lm, lm_o = amd.log_mel(power, fb, 1e-10), orc.log_mel(power, fb, 1e-10)
+    # the filterbank sums are bit-identical (same order, no FMA); logf may differ by an ulp
+    np.testing.assert_allclose(lm, lm_o, rtol=1e-6, atol=1e-6)
+    for lifter in (0.0, 22.0):
+        m, m_o = amd.mfcc(lm_o, 13, lifter), orc.mfcc(lm_o, 13, lifter)
+        # DCT-II: the reference accumulates cosf terms in f32 (dct.c:21-30), ours uses a
+        # table rounded from double: normwise agreement at the harness tolerance
+        assert _normwise(m, m_o) <= 5e-5, _normwise(m, m_o)
+    p = amd.mfcc_pipeline(power, n_fft, n_mels, 13, args[2], args[3], args[4], 22.0, 1e-10)
+    assert _normwise(p, orc.mfcc(lm_o, 13, 22.0)) <= 5e-5
+
+
+def test_stft_power_to_mfcc_device(vdev, orc):
+    """Device pipeline: multi-channel power spectrogram (STFT mode 2) -> fused
+    log-mel + MFCC, against the oracle chain on NumPy f64 power spectra."""
+    import ctypes as C
+    import torch
+    nfft, hop, nch, n = 1024, 256, 3, 48000 + 333
+    g = torch.Generator(device="cuda").manual_seed(8)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
+    st = vdev.Stft(nfft, hop)
+    pw = st.power(sig)
+    fr = st.frames(n)
+    assert pw.shape == (nch, fr, nfft // 2 + 1)
+    x = sig.cpu().numpy().astype(np.float64)
+    w = orc.window(1, nfft).astype(np.float64)
+    ref_pw = []
+    for c in range(nch):
+        pad = np.concatenate([x[c], np.zeros(nfft)])
+        F = np.fft.rfft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1)
+        ref_pw.append(np.abs(F) ** 2)
+    ref_pw = np.stack(ref_pw)
+    assert _normwise(pw.cpu().numpy(), ref_pw) <= 1e-5
+    # fused log-mel + MFCC on the device
+    L = vdev.lib()
+    L.vv_dsp_mfcc_init.argtypes = [C.c_size_t, C.c_size_t, C.c_size_t, C.c_float, C.c_float, C.c_float, C.c_int,
+                                   C.c_int, C.c_float, C.c_float, C.POINTER(C.c_void_p)]
+    L.vv_dsp_mfcc_process_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
+    L.vv_dsp_log_mel_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
+    L.vv_dsp_mfcc_destroy.argtypes = [C.c_void_p]
+    plan = C.c_void_p()
+    assert L.vv_dsp_mfcc_init(nfft, 40, 13, 48000.0, 20.0, 20000.0, 0, 2, 22.0, 1e-10, C.byref(plan)) == 0
+    try:
+        rows = nch * fr
+        mf = torch.empty(rows, 13, device="cuda")
+        lmd = torch.empty(rows, 40, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        assert L.vv_dsp_mfcc_process_device(plan, pw.data_ptr(), rows, mf.data_ptr(), s) == 0
+        assert L.vv_dsp_log_mel_device(plan, pw.data_ptr(), rows, lmd.data_ptr(), s) == 0
+        torch.cuda.synchronize()
+    finally:
+        L.vv_dsp_mfcc_destroy(plan)
+    _, fb = orc.mel_filterbank(nfft, 40, 48000.0, 20.0, 20000.0)
+    lm_ref = orc.log_mel(ref_pw.reshape(rows, -1).astype(np.float32), fb, 1e-10)
+    np.testing.assert_allclose(lmd.cpu().numpy(), lm_ref, rtol=1e-4, atol=1e-4)
+    assert _normwise(mf.cpu().numpy(), orc.mfcc(lm_ref, 13, 22.0)) <= 1e-4

@@ -45,6 +45,37 @@ def test_oracle_stft_hilbert_dct_fir_bitexact(orc, ref):
                               equal_nan=True)
 
 
+MEL_CASES = [(512, 26, 16000.0, 0.0, 8000.0), (1024, 40, 48000.0, 20.0, 20000.0), (2048, 128, 44100.0, 0.0,
+                                                                                   22050.0), (256, 10, 8000.0, 300.0, 3400.0)]
+
+
+def test_oracle_mel_mfcc_bitexact(orc, ref):
+    """src/features/mel.c restated: conversions, filterbank, log-mel and MFCC
+    bit-identical to the reference compiled in place (oracle/_ref)."""
+    for hz in (0.0, 1.0, 440.0, 1000.0, 8000.0, 24000.0, -5.0):
+        assert orc.hz_to_mel(hz) == ref.hz_to_mel(hz)
+        assert orc.mel_to_hz(hz) == ref.mel_to_hz(hz)
+    rng = np.random.default_rng(21)
+    for n_fft, n_mels, sr, fmin, fmax in MEL_CASES:
+        st_o, fb_o = orc.mel_filterbank(n_fft, n_mels, sr, fmin, fmax)
+        st_r, fb_r = ref.mel_filterbank(n_fft, n_mels, sr, fmin, fmax)
+        assert st_o == st_r == 0
+        assert np.array_equal(fb_o, fb_r)
+        power = (rng.random((7, n_fft // 2 + 1)) ** 2).astype(np.float32)
+        lm_o, lm_r = orc.log_mel(power, fb_o, 1e-10), ref.log_mel(power, fb_r, 1e-10)
+        assert np.array_equal(lm_o, lm_r)
+        nc = min(13, n_mels)
+        for ncoef, lifter in ((nc, 22.0), (n_mels, 0.0)):
+            assert np.array_equal(orc.mfcc(lm_o, ncoef, lifter), ref.mfcc(lm_r, ncoef, lifter))
+        assert np.array_equal(ref.mfcc_pipeline(power, n_fft, n_mels, nc, sr, fmin, fmax, 22.0, 1e-10),
+                              orc.mfcc(orc.log_mel(power, fb_o, 1e-10), nc, 22.0))
+    # argument validation is the reference's (mel.c:78-98)
+    assert orc.mel_filterbank(512, 300, 16000.0, 0.0, 8000.0)[0] == ref.mel_filterbank(512, 300, 16000.0, 0.0,
+                                                                                        8000.0)[0] == 2
+    assert orc.mel_filterbank(512, 26, 16000.0, 0.0, 9000.0)[0] == ref.mel_filterbank(512, 26, 16000.0, 0.0,
+                                                                                       9000.0)[0] == 3
+
+
 def test_oracle_matches_golden(orc, golden):
     g = golden("fft_testpy_n1024")
     assert np.array_equal(orc.fft(g["x"], C2C, FWD), g["c2c_fwd_kiss"])

@@ -195,6 +195,85 @@ class VvDsp:
         assert self.lib.vv_dsp_window_hann(n, _fp(w)) == OK
         return w
 
+    # ---- mel / MFCC (include/vv_dsp/features/mel.h) ---------------------
+    def _mel_setup(self):
+        L = self.lib
+        if getattr(self, "_mel_ok", False):
+            return L
+        L.vv_dsp_hz_to_mel.argtypes = [C.c_float]
+        L.vv_dsp_hz_to_mel.restype = C.c_float
+        L.vv_dsp_mel_to_hz.argtypes = [C.c_float]
+        L.vv_dsp_mel_to_hz.restype = C.c_float
+        L.vv_dsp_mel_filterbank_create.argtypes = [C.c_size_t, C.c_size_t, C.c_float, C.c_float, C.c_float,
+                                                   C.c_int, C.POINTER(_f32p), C.POINTER(C.c_size_t),
+                                                   C.POINTER(C.c_size_t)]
+        L.vv_dsp_mel_filterbank_free.argtypes = [_f32p, C.c_size_t]
+        L.vv_dsp_mel_filterbank_free.restype = None
+        L.vv_dsp_compute_log_mel_spectrogram.argtypes = [_f32p, C.c_size_t, C.c_size_t, _f32p, C.c_size_t,
+                                                         C.c_float, _f32p]
+        L.vv_dsp_mfcc.argtypes = [_f32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int, C.c_float, _f32p]
+        L.vv_dsp_mfcc_init.argtypes = [C.c_size_t, C.c_size_t, C.c_size_t, C.c_float, C.c_float, C.c_float,
+                                       C.c_int, C.c_int, C.c_float, C.c_float, C.POINTER(_vp)]
+        L.vv_dsp_mfcc_process.argtypes = [_vp, _f32p, C.c_size_t, _f32p]
+        L.vv_dsp_mfcc_destroy.argtypes = [_vp]
+        self._mel_ok = True
+        return L
+
+    def hz_to_mel(self, hz):
+        return self._mel_setup().vv_dsp_hz_to_mel(hz)
+
+    def mel_to_hz(self, mel):
+        return self._mel_setup().vv_dsp_mel_to_hz(mel)
+
+    def mel_filterbank(self, n_fft, n_mels, sr, fmin, fmax, variant=0):
+        L = self._mel_setup()
+        p, nf, fl = _f32p(), C.c_size_t(), C.c_size_t()
+        st = L.vv_dsp_mel_filterbank_create(n_fft, n_mels, sr, fmin, fmax, variant, C.byref(p), C.byref(nf),
+                                            C.byref(fl))
+        if st != OK:
+            return st, None
+        fb = np.ctypeslib.as_array(p, shape=(nf.value * fl.value,)).copy().reshape(nf.value, fl.value)
+        L.vv_dsp_mel_filterbank_free(p, nf.value)
+        return OK, fb
+
+    def log_mel(self, power, fb, eps):
+        L = self._mel_setup()
+        power = np.ascontiguousarray(power, np.float32)
+        fb = np.ascontiguousarray(fb, np.float32)
+        out = np.zeros((power.shape[0], fb.shape[0]), np.float32)
+        st = L.vv_dsp_compute_log_mel_spectrogram(_fp(power), power.shape[0], power.shape[1], _fp(fb),
+                                                  fb.shape[0], eps, _fp(out))
+        if st != OK:
+            raise RuntimeError(f"log_mel status {st}{self._err()}")
+        return out
+
+    def mfcc(self, log_mel, n_coeffs, lifter, dct_type=DCT_II):
+        L = self._mel_setup()
+        log_mel = np.ascontiguousarray(log_mel, np.float32)
+        out = np.zeros((log_mel.shape[0], n_coeffs), np.float32)
+        st = L.vv_dsp_mfcc(_fp(log_mel), log_mel.shape[0], log_mel.shape[1], n_coeffs, dct_type, lifter,
+                           _fp(out))
+        if st != OK:
+            raise RuntimeError(f"mfcc status {st}{self._err()}")
+        return out
+
+    def mfcc_pipeline(self, power, n_fft, n_mels, n_coeffs, sr, fmin, fmax, lifter, eps):
+        """vv_dsp_mfcc_init / _process / _destroy"""
+        L = self._mel_setup()
+        power = np.ascontiguousarray(power, np.float32)
+        plan = _vp()
+        st = L.vv_dsp_mfcc_init(n_fft, n_mels, n_coeffs, sr, fmin, fmax, 0, DCT_II, lifter, eps, C.byref(plan))
+        if st != OK:
+            raise RuntimeError(f"mfcc_init status {st}{self._err()}")
+        try:
+            out = np.zeros((power.shape[0], n_coeffs), np.float32)
+            st = L.vv_dsp_mfcc_process(plan, _fp(power), power.shape[0], _fp(out))
+            if st != OK:
+                raise RuntimeError(f"mfcc_process status {st}{self._err()}")
+        finally:
+            L.vv_dsp_mfcc_destroy(plan)
+        return out
+
 
 class Oracle:
     """Binding of oracle/liboracle.so (our C restatement; test infrastructure)."""
@@ -267,6 +346,39 @@ class Oracle:
         h = np.zeros(taps, np.float32)
         assert self.lib.orc_fir_design_lowpass(_fp(h), taps, fc, wkind) == 0
         return h
+
+    # ---- mel / MFCC (oracle restatement of src/features/mel.c) ----------
+    def hz_to_mel(self, hz):
+        self.lib.orc_hz_to_mel.argtypes = [C.c_float]
+        self.lib.orc_hz_to_mel.restype = C.c_float
+        return self.lib.orc_hz_to_mel(hz)
+
+    def mel_to_hz(self, mel):
+        self.lib.orc_mel_to_hz.argtypes = [C.c_float]
+        self.lib.orc_mel_to_hz.restype = C.c_float
+        return self.lib.orc_mel_to_hz(mel)
+
+    def mel_filterbank(self, n_fft, n_mels, sr, fmin, fmax):
+        self.lib.orc_mel_filterbank.argtypes = [C.c_size_t, C.c_size_t, C.c_float, C.c_float, C.c_float, _f32p]
+        fb = np.zeros((n_mels, n_fft // 2 + 1), np.float32)
+        st = self.lib.orc_mel_filterbank(n_fft, n_mels, sr, fmin, fmax, _fp(fb))
+        return st, (fb if st == 0 else None)
+
+    def log_mel(self, power, fb, eps):
+        self.lib.orc_log_mel.argtypes = [_f32p, C.c_size_t, C.c_size_t, _f32p, C.c_size_t, C.c_float, _f32p]
+        power = np.ascontiguousarray(power, np.float32)
+        fb = np.ascontiguousarray(fb, np.float32)
+        out = np.zeros((power.shape[0], fb.shape[0]), np.float32)
+        assert self.lib.orc_log_mel(_fp(power), power.shape[0], power.shape[1], _fp(fb), fb.shape[0], eps,
+                                    _fp(out)) == 0
+        return out
+
+    def mfcc(self, log_mel, n_coeffs, lifter):
+        self.lib.orc_mfcc.argtypes = [_f32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_float, _f32p]
+        log_mel = np.ascontiguousarray(log_mel, np.float32)
+        out = np.zeros((log_mel.shape[0], n_coeffs), np.float32)
+        assert self.lib.orc_mfcc(_fp(log_mel), log_mel.shape[0], log_mel.shape[1], n_coeffs, lifter, _fp(out)) == 0
+        return out
 
     def fir_apply(self, h, x, fft=False):
         h = np.ascontiguousarray(h, np.float32)

@@ -290,16 +290,20 @@ struct vvhip_stft {
     DevBuf b0, b1, b2;
 };
 
+// out_kind: 0 magnitude rows [frame][nfft], 1 complex rows [frame][nfft],
+// 2 power rows [frame][nfft/2+1]
 static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch, size_t ch_stride,
-                           void* out, size_t out_ch_stride, int complex_out, hipStream_t s) {
+                           void* out, size_t out_ch_stride, int out_kind, hipStream_t s) {
     const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
     const long long NF = (long long)h->nfft;
+    if (out_kind < 0 || out_kind > 2) return fail(ST_RANGE, "stft output kind");
     if (stft_fused_supported(NF)) {
-        HIPCHK(launch_stft(NF, (long long)h->hop, complex_out ? 1 : 0, sig, (long long)n, (long long)nch,
-                           (long long)ch_stride, (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
+        HIPCHK(launch_stft(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch, (long long)ch_stride,
+                           (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
                ST_INTERNAL);
         return ST_OK;
     }
+    const int complex_out = out_kind == 1;
     // generic nfft: gather windowed complex frames, batched C2C, magnitude
     for (size_t c = 0; c < nch; ++c) {
         Scratch fr(s);
@@ -314,8 +318,13 @@ static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch
         } else {
             int st = fft_run(h->nfft, 0, 1, fr.p, fr.p, frames, s);
             if (st) return st;
-            HIPCHK(launch_magnitude((const float2*)fr.p, (float*)out + c * out_ch_stride, (long long)cnt, s),
-                   ST_INTERNAL);
+            if (out_kind == 2)
+                HIPCHK(launch_power_half((const float2*)fr.p, (float*)out + c * out_ch_stride, NF, (long long)frames,
+                                         s),
+                       ST_INTERNAL);
+            else
+                HIPCHK(launch_magnitude((const float2*)fr.p, (float*)out + c * out_ch_stride, (long long)cnt, s),
+                       ST_INTERNAL);
         }
     }
     return ST_OK;
@@ -732,6 +741,123 @@ int vvhip_dct_host(const float* in, float* out, size_t n, int type, int dir, int
     if (dout) (void)hipFree(dout);
     (void)hipStreamDestroy(s);
     return st;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Mel / MFCC (src/features/mel.c): filterbank tables staged on the device
+// ---------------------------------------------------------------------------
+struct vvhip_mel {
+    int n_mels = 0, nbins = 0, n_coeffs = 0, nnz = 0;
+    float eps = 0.0f;
+    float* W = nullptr;     // non-zero weight ranges of every filter, packed
+    int* meta = nullptr;    // per filter: lo, len, offset into W
+    float* D = nullptr;     // DCT-II table [n_coeffs][n_mels]
+    float* lift = nullptr;  // lifter factors [n_coeffs]
+    hipStream_t stream = nullptr;
+    DevBuf bin, bout;
+};
+
+extern "C" {
+
+void vvhip_mel_destroy(vvhip_mel* m) {
+    if (!m) return;
+    if (m->stream) {
+        (void)hipStreamSynchronize(m->stream);
+        (void)hipStreamDestroy(m->stream);
+    }
+    if (m->W) (void)hipFree(m->W);
+    if (m->meta) (void)hipFree(m->meta);
+    if (m->D) (void)hipFree(m->D);
+    if (m->lift) (void)hipFree(m->lift);
+    m->bin.release();
+    m->bout.release();
+    delete m;
+}
+
+int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coeffs, float lifter, float eps,
+                     vvhip_mel** out) {
+    if (!out) return ST_NULL;
+    *out = nullptr;
+    if (n_mels == 0 || (fb && nbins == 0) || n_coeffs > n_mels) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    vvhip_mel* m = new (std::nothrow) vvhip_mel;
+    if (!m) return ST_INTERNAL;
+    m->n_mels = (int)n_mels;
+    m->nbins = fb ? (int)nbins : 0;
+    m->n_coeffs = (int)n_coeffs;
+    m->eps = eps;
+    std::vector<float> w;
+    std::vector<int> meta(3 * n_mels, 0);
+    if (fb) {
+        for (size_t f = 0; f < n_mels; ++f) {
+            const float* r = fb + f * nbins;
+            size_t lo = 0, hi = 0;
+            for (size_t k = 0; k < nbins; ++k)
+                if (r[k] != 0.0f) {
+                    if (hi == 0) lo = k;
+                    hi = k + 1;
+                }
+            meta[3 * f] = (int)lo;
+            meta[3 * f + 1] = (int)(hi > lo ? hi - lo : 0);
+            meta[3 * f + 2] = (int)w.size();
+            for (size_t k = lo; k < hi; ++k) w.push_back(r[k]);
+        }
+    }
+    m->nnz = (int)w.size();
+    // DCT-II rows cos(pi (j + 1/2) i / M) (dct.c:21-30), and the lifter of mel.c:300-302
+    std::vector<float> D(n_coeffs * n_mels), L(n_coeffs, 1.0f);
+    for (size_t i = 0; i < n_coeffs; ++i)
+        for (size_t j = 0; j < n_mels; ++j)
+            D[i * n_mels + j] = (float)std::cos(M_PI * ((double)j + 0.5) * (double)i / (double)n_mels);
+    if (lifter > 0.0f)
+        for (size_t i = 1; i < n_coeffs; ++i)
+            L[i] = 1.0f + (lifter / 2.0f) * sinf((float)M_PI * (float)i / lifter);
+    bool ok = hipMalloc(&m->meta, sizeof(int) * meta.size()) == hipSuccess &&
+              hipMemcpy(m->meta, meta.data(), sizeof(int) * meta.size(), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMalloc(&m->W, sizeof(float) * (w.size() + 1)) == hipSuccess &&
+              (w.empty() || hipMemcpy(m->W, w.data(), sizeof(float) * w.size(), hipMemcpyHostToDevice) == hipSuccess) &&
+              hipMalloc(&m->D, sizeof(float) * (D.size() + 1)) == hipSuccess &&
+              (D.empty() || hipMemcpy(m->D, D.data(), sizeof(float) * D.size(), hipMemcpyHostToDevice) == hipSuccess) &&
+              hipMalloc(&m->lift, sizeof(float) * (L.size() + 1)) == hipSuccess &&
+              (L.empty() || hipMemcpy(m->lift, L.data(), sizeof(float) * L.size(), hipMemcpyHostToDevice) == hipSuccess);
+    if (!ok) {
+        vvhip_mel_destroy(m);
+        return fail(ST_INTERNAL, "mel tables upload");
+    }
+    *out = m;
+    return ST_OK;
+}
+
+static size_t mel_in_len(const vvhip_mel* m, int kind) { return kind == 2 ? (size_t)m->n_mels : (size_t)m->nbins; }
+static size_t mel_out_len(const vvhip_mel* m, int kind) { return kind == 0 ? (size_t)m->n_mels : (size_t)m->n_coeffs; }
+
+int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_out, int kind, void* stream) {
+    if (!m || !d_in || !d_out) return ST_NULL;
+    if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
+    if ((kind != 2 && m->nbins == 0) || (kind != 0 && m->n_coeffs == 0)) return fail(ST_RANGE, "mel plan lacks tables");
+    if (frames == 0) return ST_OK;
+    HIPCHK(launch_mel(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->meta, m->nnz, m->D,
+                      m->lift, m->eps, d_out, (hipStream_t)stream),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_mel_host(vvhip_mel* m, const float* in, size_t frames, float* out, int kind) {
+    if (!m || !in || !out) return ST_NULL;
+    if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
+    if (frames == 0) return ST_OK;
+    if (!m->stream) HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking), ST_INTERNAL);
+    const size_t ib = sizeof(float) * frames * mel_in_len(m, kind), ob = sizeof(float) * frames * mel_out_len(m, kind);
+    HIPCHK(m->bin.ensure(ib), ST_INTERNAL);
+    HIPCHK(m->bout.ensure(ob), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(m->bin.p, in, ib, hipMemcpyHostToDevice, m->stream), ST_INTERNAL);
+    int st = vvhip_mel_device(m, (const float*)m->bin.p, frames, (float*)m->bout.p, kind, m->stream);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(out, m->bout.p, ob, hipMemcpyDeviceToHost, m->stream), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(m->stream), ST_INTERNAL);
+    return ST_OK;
 }
 
 }  // extern "C"

@@ -62,17 +62,18 @@ __device__ __forceinline__ float cmag(float re, float im) {
 //   Xa[k] = Z[k] + conj Z[N-k],  Xb[k] = -i (Z[k] - conj Z[N-k]).
 // The 1/2 rides in the window (a power-of-two scale commutes with every
 // rounding, so this is bit-identical to halving at the end).  Packed f32 math.
-// MODE 0: A.x = |Xa[k]|, B.x = |Xb[k]|;  MODE 1: A = Xa[k], B = Xb[k].
+// MODE 0: A.x = |Xa[k]|, B.x = |Xb[k]|;  MODE 1: A = Xa[k], B = Xb[k];
+// MODE 2: A.x = |Xa[k]|^2, B.x = |Xb[k]|^2 (power, bins 0..N/2 stored).
 template <int MODE>
 __device__ __forceinline__ void pair_post(float2 Z, float2 Zm, float2* A, float2* B) {
     const vf2_t z = {Z.x, Z.y}, zm = {Zm.x, Zm.y};
     const vf2_t s = z + zm;   // (Re Xa, Re Xb)
     const vf2_t d = z - zm;   // (-Im Xb, Im Xa)
-    if constexpr (MODE == 0) {
+    if constexpr (MODE == 0 || MODE == 2) {
         const vf2_t dd = d * d;
         const vf2_t m2 = s * s + dd.yx;   // (|Xa|^2, |Xb|^2)
-        A->x = __builtin_amdgcn_sqrtf(m2.x);
-        B->x = __builtin_amdgcn_sqrtf(m2.y);
+        A->x = MODE == 0 ? __builtin_amdgcn_sqrtf(m2.x) : m2.x;
+        B->x = MODE == 0 ? __builtin_amdgcn_sqrtf(m2.y) : m2.y;
         A->y = B->y = 0.0f;
     } else {
         *A = make_float2(s.x, d.y);
@@ -80,11 +81,14 @@ __device__ __forceinline__ void pair_post(float2 Z, float2 Zm, float2* A, float2
     }
 }
 
-// bin k of an output row (MODE 0: float magnitudes, MODE 1: float2 spectrum)
-template <int MODE>
+// bin k of an output row (MODE 0: float magnitudes, MODE 1: float2 spectrum,
+// MODE 2: float power of the half spectrum -- bins above N/2 are not stored)
+template <int MODE, int N>
 __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
     if constexpr (MODE == 0) *(reinterpret_cast<float*>(row) + k) = X.x;
-    else *(reinterpret_cast<float2*>(row) + k) = X;
+    else if constexpr (MODE == 2) {
+        if (k <= N / 2) *(reinterpret_cast<float*>(row) + k) = X.x;
+    } else *(reinterpret_cast<float2*>(row) + k) = X;
 }
 
 // Frame pairs (2j, 2j+1) of one channel, j in [pair0, pair0 + ppc): pairs never
@@ -170,7 +174,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     int kb[G::NPT];   // last-pass butterfly of each slot (loop invariant)
 #pragma unroll
     for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
-    constexpr long long ES = MODE == 0 ? 4 : 8;
+    constexpr long long ES = MODE == 1 ? 8 : 4;            // bytes per bin
+    constexpr long long ROW = MODE == 2 ? N / 2 + 1 : N;   // bins per row
     for (; p < p_end; p += p_step) {
         const bool more = p + p_step < p_end;
         long long cn = c, fn = fa;
@@ -198,8 +203,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
         fft_regs<N, true, true>(v, t, my, tw);
-        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * (long long)N) * ES;
-        char* rowb = rowa + N * ES;
+        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
+        char* rowb = rowa + ROW * ES;
         const bool has_b = TAIL ? fa + 1 < frames : true;
         if constexpr (STAGE) {
             // both magnitude rows through the (now idle) exchange buffer, then
@@ -246,8 +251,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             for (int q = 0; q < G::P; ++q) {
                 float2 A, B;
                 pair_post<MODE>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
-                put_bin<MODE>(rowa, q, A);
-                if (has_b) put_bin<MODE>(rowb, q, B);
+                put_bin<MODE, N>(rowa, q, A);
+                if (has_b) put_bin<MODE, N>(rowb, q, B);
             }
         } else {
             // even slots hold bins k, their partner slots hold N-k: one post
@@ -267,11 +272,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                         Bm = select2(t == 0, B2, Bm);
                     }
                     const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
-                    put_bin<MODE>(rowa, k, A);
-                    put_bin<MODE>(rowa, km, Am);
+                    put_bin<MODE, N>(rowa, k, A);
+                    put_bin<MODE, N>(rowa, km, Am);
                     if (has_b) {
-                        put_bin<MODE>(rowb, k, B);
-                        put_bin<MODE>(rowb, km, Bm);
+                        put_bin<MODE, N>(rowb, k, B);
+                        put_bin<MODE, N>(rowb, km, Bm);
                     }
                 }
             }
@@ -328,7 +333,7 @@ k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, l
         for (int r = 0; r < G::P; ++r) v[r] = make_float2(nx[r].x * w[r].x, nx[r].y * w[r].y);
         if (it + it_step < it_end) load(it + it_step);
         fft_regs<M, true, PAIR>(v, t, my, tw);
-        const long long row = c * out_ch_stride + fr * (long long)NR;
+        const long long row = c * out_ch_stride + fr * (long long)(MODE == 2 ? M + 1 : NR);
         float2 A[G::P], B[G::P];
         int K[G::P];
         if constexpr (PAIR) {
@@ -364,6 +369,16 @@ k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, l
                     const float mag = cmag(X.x, X.y);
                     *(o + k) = mag;
                     *(o + (NR - k)) = mag;
+                }
+            } else if (MODE == 2) {   // power of bins 0..M
+                float* o = reinterpret_cast<float*>(out) + row;
+                if (k == 0) {
+                    const float x0 = A[q].x + A[q].y, xm = A[q].x - A[q].y;
+                    *(o) = x0 * x0;
+                    *(o + M) = xm * xm;
+                } else {
+                    const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
+                    *(o + k) = __builtin_fmaf(X.x, X.x, X.y * X.y);
                 }
             } else {
                 float2* o = reinterpret_cast<float2*>(out) + row;
@@ -439,9 +454,10 @@ bool stft_fused_supported(long long nfft) {
 hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,
                        long long nch, long long ch_stride, long long frames, const float* win,
                        void* out, long long out_ch_stride, hipStream_t s) {
-#define CALL(NN)                                                                                   \
-    (mode == 0 ? run_stft<NN, 0>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s)   \
-               : run_stft<NN, 1>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s))
+#define CALL(NN)                                                                                     \
+    (mode == 0   ? run_stft<NN, 0>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s) \
+     : mode == 1 ? run_stft<NN, 1>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s) \
+                 : run_stft<NN, 2>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s))
     switch (nfft) {
         case 2: return CALL(2); case 4: return CALL(4); case 8: return CALL(8); case 16: return CALL(16);
         case 32: return CALL(32); case 64: return CALL(64); case 128: return CALL(128);
@@ -498,6 +514,26 @@ hipError_t launch_magnitude(const float2* in, float* out, long long count, hipSt
     long long blocks = (count + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(k_magnitude, dim3((unsigned)blocks), dim3(256), 0, s, in, out, count);
+    return hipGetLastError();
+}
+
+// |X[k]|^2 for k <= nfft/2 of rows [rows][nfft] -> [rows][nfft/2+1]
+__global__ void k_power_half(const float2* in, float* out, long long nfft, long long count) {
+    const long long nh = nfft / 2 + 1;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long r = i / nh, k = i - r * nh;
+        const float2 v = in[r * nfft + k];
+        out[i] = __builtin_fmaf(v.x, v.x, v.y * v.y);
+    }
+}
+
+hipError_t launch_power_half(const float2* in, float* out, long long nfft, long long rows, hipStream_t s) {
+    const long long count = rows * (nfft / 2 + 1);
+    if (count <= 0) return hipSuccess;
+    long long blocks = (count + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_power_half, dim3((unsigned)blocks), dim3(256), 0, s, in, out, nfft, count);
     return hipGetLastError();
 }
 

@@ -30,6 +30,13 @@ hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, f
 // real[batch][n] -> complex[batch][n] (imaginary 0)
 hipError_t launch_promote_real(const float* in, float2* out, long long count, hipStream_t s);
 
+// ---- mel / MFCC (mel_kernels.hip) ---------------------------------------
+// mode 0: power rows [frames][nbins] -> log-mel [frames][n_mels]
+//      1: power rows -> MFCC [frames][n_coeffs];  2: log-mel rows -> MFCC
+hipError_t launch_mel(int mode, const float* in, long long frames, int nbins, int n_mels, int n_coeffs,
+                      const float* W, const int* meta, int nnz, const float* D, const float* lift, float eps,
+                      float* out, hipStream_t s);
+
 // Write sink (SINK_FLOATS floats): destination of lanes that must issue a store
 // with nothing to write, in kernels that hand-count their memory operations.
 constexpr size_t SINK_FLOATS = 1u << 18;   // 1 MiB = 4096 waves x 64 lanes
@@ -61,7 +68,8 @@ hipError_t launch_zero_nyquist_imag(float2* out, long long n, long long batch, l
                                     hipStream_t s);
 
 // ---- STFT (stft_kernels.hip) -------------------------------------------
-// mode 0: magnitude rows [frames][nfft] ; mode 1: complex rows [frames][nfft]
+// mode 0: magnitude rows [frames][nfft]; 1: complex rows [frames][nfft];
+// 2: power rows [frames][nfft/2+1]
 bool stft_fused_supported(long long nfft);
 hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,
                        long long nch, long long ch_stride, long long frames, const float* win,
@@ -74,13 +82,14 @@ hipError_t launch_frame_gather(long long nfft, long long hop, const float* sig, 
                                long long nch, long long ch_stride, long long frames,
                                const float* win, float2* out, hipStream_t s);
 hipError_t launch_magnitude(const float2* in, float* out, long long count, hipStream_t s);
+hipError_t launch_power_half(const float2* in, float* out, long long nfft, long long rows, hipStream_t s);
 // ISTFT accumulate (stft_reconstruct batch): out_add[i] += Re(t[f][i])*w[i] for frames at hop
 hipError_t launch_ola(long long nfft, long long hop, const float2* time_frames, long long count,
                       const float* win, float* out_add, float* norm_add, hipStream_t s);
 
 // ---- FIR overlap-save (fir_kernels.hip) ---------------------------------
 bool fir_ols_supported(long long nfft);
-// H: nfft/2+1 complex, already scaled by 2/nfft.  prefix: [nch][taps-1] chronological or null.
+// H: nfft complex bins of FFT(h zero-padded)/nfft.  prefix: [nch][taps-1] chronological or null.
 hipError_t launch_fir_ols(long long nfft, long long taps, const float2* H, const float* x,
                           float* y, long long n, long long nch, long long x_stride,
                           long long y_stride, const float* prefix, hipStream_t s);

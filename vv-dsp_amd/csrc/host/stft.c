@@ -109,6 +109,15 @@ vv_dsp_status vv_dsp_stft_spectrum_device(vv_dsp_stft* h, const vv_dsp_real* d_s
                                                         out_ch_stride, 1, stream);
 }
 
+vv_dsp_status vv_dsp_stft_power_device(vv_dsp_stft* h, const vv_dsp_real* d_signal, size_t n, size_t nch,
+                                       size_t ch_stride, vv_dsp_real* d_out_power, size_t out_ch_stride,
+                                       void* stream, size_t* out_frames) {
+    if (!h || !d_signal || !d_out_power) return VV_DSP_ERROR_NULL_POINTER;
+    if (out_frames) *out_frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    return (vv_dsp_status)vvhip_stft_spectrogram_device(h->dev, d_signal, n, nch, ch_stride, d_out_power,
+                                                        out_ch_stride, 2, stream);
+}
+
 vv_dsp_status vv_dsp_stft_process_device(vv_dsp_stft* h, const vv_dsp_real* d_frames, size_t count,
                                          vv_dsp_cpx* d_spec, void* stream) {
     if (!h || !d_frames || !d_spec) return VV_DSP_ERROR_NULL_POINTER;

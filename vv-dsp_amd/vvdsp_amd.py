@@ -52,6 +52,7 @@ def lib():
     L.vv_dsp_stft_destroy.argtypes = [_vp]
     L.vv_dsp_stft_spectrogram_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_spectrum_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_stft_power_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_process_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.vv_dsp_stft_reconstruct_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp]
     L.vv_dsp_fir_plan_create.argtypes = [_vp, _sz, C.POINTER(_vp)]
@@ -139,6 +140,19 @@ class Stft:
         f = lib().vv_dsp_stft_spectrum_device if complex_out else lib().vv_dsp_stft_spectrogram_device
         _check(f(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * self.nfft, _stream(stream),
                  C.byref(nf)), "stft_spectrogram_device")
+        assert nf.value == fr
+        return out if sig.dim() == 2 else out[0]
+
+    def power(self, sig, out=None, stream=None):
+        """sig: (nch, n) or (n,) float32 -> power spectrogram (nch, frames, nfft//2 + 1)."""
+        sig2 = sig if sig.dim() == 2 else sig.unsqueeze(0)
+        nch, n = sig2.shape
+        fr, nh = self.frames(n), self.nfft // 2 + 1
+        if out is None:
+            out = torch.empty((nch, fr, nh), dtype=torch.float32, device=sig.device)
+        nf = _sz(0)
+        _check(lib().vv_dsp_stft_power_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * nh,
+                                               _stream(stream), C.byref(nf)), "stft_power_device")
         assert nf.value == fr
         return out if sig.dim() == 2 else out[0]
 
