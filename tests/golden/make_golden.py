@@ -101,6 +101,18 @@ def main():
          h=h, x=xs, kiss=ref.fir_apply(h, xs, fft=True),
          np64=scipy.signal.lfilter(h.astype(np.float64), [1.0], xs.astype(np.float64)))
 
+    # 7. mel filterbank / log-mel / MFCC (src/features/mel.c; mfcc_tests.c parameters)
+    rng = np.random.default_rng(7)
+    st, fb = ref.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)
+    assert st == 0
+    power = (rng.random((16, 257)) ** 2).astype(np.float32)
+    power[0] = 1.0 / (1.0 + np.arange(257, dtype=np.float32))   # mfcc_tests.c synthetic spectrum
+    lm = ref.log_mel(power, fb, 1e-10)
+    save("mel_512_26", man, "mel filterbank 512-pt/26 mels/16 kHz/0-8 kHz (HTK), log-mel eps 1e-10 of 16 power "
+         "rows (row 0 = 1/(1+k), others uniform^2 seed 7), MFCC 13 coeffs lifter 22",
+         fb=fb, power=power, log_mel_kiss=lm, mfcc_kiss=ref.mfcc(lm, 13, 22.0),
+         log_mel_np64=np.log(power.astype(np.float64) @ fb.astype(np.float64).T + 1e-10))
+
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
     print("wrote", len(man), "golden sets")

@@ -503,3 +503,13 @@ def test_stft_power_to_mfcc_device(vdev, orc):
     lm_ref = orc.log_mel(ref_pw.reshape(rows, -1).astype(np.float32), fb, 1e-10)
     np.testing.assert_allclose(lmd.cpu().numpy(), lm_ref, rtol=1e-4, atol=1e-4)
     assert _normwise(mf.cpu().numpy(), orc.mfcc(lm_ref, 13, 22.0)) <= 1e-4
+
+
+def test_golden_mel(amd, golden):
+    g = golden("mel_512_26")
+    st, fb = amd.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)
+    assert st == OK and np.array_equal(fb, g["fb"])   # host setup: bit-identical
+    np.testing.assert_allclose(amd.log_mel(g["power"], fb, 1e-10), g["log_mel_kiss"], rtol=1e-6, atol=1e-6)
+    assert _normwise(amd.mfcc(g["log_mel_kiss"], 13, 22.0), g["mfcc_kiss"]) <= 5e-5
+    assert _normwise(amd.mfcc_pipeline(g["power"], 512, 26, 13, 16000.0, 0.0, 8000.0, 22.0, 1e-10),
+                     g["mfcc_kiss"]) <= 5e-5

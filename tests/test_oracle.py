@@ -100,6 +100,11 @@ def test_oracle_matches_golden(orc, golden):
     assert np.array_equal(orc.fir_apply(g["h"], g["x"]), g["kiss"])
     g = golden("firfft_257_n1500")
     assert np.array_equal(orc.fir_apply(g["h"], g["x"], fft=True), g["kiss"])
+    g = golden("mel_512_26")
+    assert np.array_equal(orc.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)[1], g["fb"])
+    assert np.array_equal(orc.log_mel(g["power"], g["fb"], 1e-10), g["log_mel_kiss"])
+    assert np.array_equal(orc.mfcc(g["log_mel_kiss"], 13, 22.0), g["mfcc_kiss"])
+    np.testing.assert_allclose(g["log_mel_kiss"], g["log_mel_np64"], rtol=1e-5, atol=1e-5)
 
 
 def _err_over_tol(y, ref, rtol, atol):
