@@ -462,7 +462,6 @@ def test_log_mel_and_mfcc_vs_oracle(amd, orc, args):
 def test_stft_power_to_mfcc_device(vdev, orc):
     """Device pipeline: multi-channel power spectrogram (STFT mode 2) -> fused
     log-mel + MFCC, against the oracle chain on NumPy f64 power spectra."""
-    import ctypes as C
     import torch
     nfft, hop, nch, n = 1024, 256, 3, 48000 + 333
     g = torch.Generator(device="cuda").manual_seed(8)
@@ -480,25 +479,13 @@ def test_stft_power_to_mfcc_device(vdev, orc):
         ref_pw.append(np.abs(F) ** 2)
     ref_pw = np.stack(ref_pw)
     assert _normwise(pw.cpu().numpy(), ref_pw) <= 1e-5
-    # fused log-mel + MFCC on the device
-    L = vdev.lib()
-    L.vv_dsp_mfcc_init.argtypes = [C.c_size_t, C.c_size_t, C.c_size_t, C.c_float, C.c_float, C.c_float, C.c_int,
-                                   C.c_int, C.c_float, C.c_float, C.POINTER(C.c_void_p)]
-    L.vv_dsp_mfcc_process_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
-    L.vv_dsp_log_mel_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
-    L.vv_dsp_mfcc_destroy.argtypes = [C.c_void_p]
-    plan = C.c_void_p()
-    assert L.vv_dsp_mfcc_init(nfft, 40, 13, 48000.0, 20.0, 20000.0, 0, 2, 22.0, 1e-10, C.byref(plan)) == 0
-    try:
-        rows = nch * fr
-        mf = torch.empty(rows, 13, device="cuda")
-        lmd = torch.empty(rows, 40, device="cuda")
-        s = torch.cuda.current_stream().cuda_stream
-        assert L.vv_dsp_mfcc_process_device(plan, pw.data_ptr(), rows, mf.data_ptr(), s) == 0
-        assert L.vv_dsp_log_mel_device(plan, pw.data_ptr(), rows, lmd.data_ptr(), s) == 0
-        torch.cuda.synchronize()
-    finally:
-        L.vv_dsp_mfcc_destroy(plan)
+    # fused log-mel + MFCC on the device (vv_dsp_mfcc_process_device / vv_dsp_log_mel_device)
+    plan = vdev.Mfcc(nfft, 40, 13, 48000.0, 20.0, 20000.0, lifter=22.0, eps=1e-10)
+    rows = nch * fr
+    mf = plan(pw).reshape(rows, 13)
+    lmd = plan.log_mel(pw).reshape(rows, 40)
+    torch.cuda.synchronize()
+    del plan
     _, fb = orc.mel_filterbank(nfft, 40, 48000.0, 20.0, 20000.0)
     lm_ref = orc.log_mel(ref_pw.reshape(rows, -1).astype(np.float32), fb, 1e-10)
     np.testing.assert_allclose(lmd.cpu().numpy(), lm_ref, rtol=1e-4, atol=1e-4)

@@ -15,7 +15,6 @@
 // are not powers of two use an O(n^2) DFT kernel with f64 accumulation (the
 // reference's own complexity for them: fft_kiss.c:76-92).
 #include "fft_core.hpp"
-#include <cstdlib>
 #include "vvhip_internal.hpp"
 
 namespace vvh {
@@ -72,12 +71,11 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     if (!tab || !pas) return hipErrorOutOfMemory;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     static int grid_cap = 0;
-    static size_t xlds = getenv("VVHIP_EXP_DYNLDS") ? (size_t)atol(getenv("VVHIP_EXP_DYNLDS")) : 0;  // EXPERIMENT
-    if (!grid_cap) grid_cap = persistent_grid((const void*)k_c2c<N, FWD>, WG, xlds, 1LL << 40);
+    if (!grid_cap) grid_cap = persistent_grid((const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < grid_cap ? need : grid_cap);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_c2c<N, FWD>), dim3(grid), dim3(WG), xlds, s, in, out, batch, in_dist, out_dist,
+    hipLaunchKernelGGL((k_c2c<N, FWD>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist,
                        pas, tab, scale);
     return hipGetLastError();
 }

@@ -15,11 +15,16 @@
 // k_stft_half<M>: one frame per M = nfft/2 point complex FFT plus the real
 // split step (nfft = 256 and 4096, where N cannot be mirror-paired).
 //
-// Scheduling: each persistent slot walks a CONTIGUOUS chunk of frame pairs,
-// so the nfft-hop overlap of consecutive frames is re-read from L1/L2 of the
-// same CU, never from HBM by another XCD; the next pair's samples are
-// prefetched into registers while the current pair is transformed; window
-// values are per-thread constants in registers; twiddles live in LDS.
+// Scheduling: the frame pairs are split into 8 contiguous shares, one per XCD
+// (xcd_walk: blockIdx % 8 selects the share), and the slots of one XCD stride
+// through their share, so the nfft-hop overlap of consecutive frames is re-read
+// from that XCD's L2, never from HBM by another XCD.  The bulk variant (VAR 0)
+// streams each pair's input span (N + N/2 samples) into LDS with
+// global_load_lds_dwordx4 one pair ahead, waits on hand-counted vmcnt, and
+// writes magnitude rows through LDS as full 16-byte non-temporal stores; the
+// register variant (VAR 1) covers unaligned hops/channel strides and VAR 2 the
+// zero-padded tail frames.  Window values are per-thread constants in
+// registers; twiddles live in LDS.
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
 

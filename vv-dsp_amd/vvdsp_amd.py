@@ -63,6 +63,11 @@ def lib():
     L.vv_dsp_dct_make_plan.argtypes = [_sz, C.c_int, C.c_int, C.POINTER(_vp)]
     L.vv_dsp_dct_execute_device.argtypes = [_vp, _vp, _vp, _sz, _vp]
     L.vv_dsp_dct_destroy.argtypes = [_vp]
+    L.vv_dsp_mfcc_init.argtypes = [_sz, _sz, _sz, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, C.c_float,
+                                   C.c_float, C.POINTER(_vp)]
+    L.vv_dsp_mfcc_destroy.argtypes = [_vp]
+    L.vv_dsp_mfcc_process_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.vv_dsp_log_mel_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.vvhip_fir_block_size.argtypes = [_vp, _sz]
     L.vvhip_fir_block_size.restype = _sz
     _lib = L
@@ -172,6 +177,36 @@ class Stft:
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
             _lib.vv_dsp_stft_destroy(self.h)
+            self.h = None
+
+
+class Mfcc:
+    """vv_dsp_mfcc_init plan (src/features/mel.c:249-310) run on device power rows:
+    (..., n_fft//2 + 1) float32 -> MFCC (..., n_coeffs) or log-mel (..., n_mels)."""
+
+    def __init__(self, n_fft, n_mels, n_coeffs, sample_rate, fmin, fmax, lifter=0.0, eps=1e-10):
+        self.n_fft, self.n_mels, self.n_coeffs = n_fft, n_mels, n_coeffs
+        self.h = _vp()
+        _check(lib().vv_dsp_mfcc_init(n_fft, n_mels, n_coeffs, sample_rate, fmin, fmax, 0, 2, lifter, eps,
+                                      C.byref(self.h)), "mfcc_init")
+
+    def _run(self, power, width, f, what, stream):
+        nb = self.n_fft // 2 + 1
+        assert power.shape[-1] == nb, f"power rows must have {nb} bins"
+        p2 = power.reshape(-1, nb)
+        out = torch.empty((p2.shape[0], width), dtype=torch.float32, device=power.device)
+        _check(f(self.h, _ptr(p2), p2.shape[0], _ptr(out), _stream(stream)), what)
+        return out.reshape(*power.shape[:-1], width)
+
+    def __call__(self, power, stream=None):
+        return self._run(power, self.n_coeffs, lib().vv_dsp_mfcc_process_device, "mfcc_process_device", stream)
+
+    def log_mel(self, power, stream=None):
+        return self._run(power, self.n_mels, lib().vv_dsp_log_mel_device, "log_mel_device", stream)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.vv_dsp_mfcc_destroy(self.h)
             self.h = None
 
 
