@@ -110,7 +110,50 @@ def case_rw(w, in_bytes=3686400000, blocks=4096):
     return (lambda: lib.membench_rw(a.data_ptr(), b.data_ptr(), n4, w, blocks, s)), in_bytes * (1 + w), (a, b, lib)
 
 
+_SHARED = {}
+
+
+def case_rwc(w, u, ntl, nts, blocks, in_bytes=3686400000):
+    """contiguous mixed stream (membench.hip k_rwc): 1 KB read -> w KB written per wave item"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libmembench.so"))
+    lib.membench_rwc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong] + [ctypes.c_int] * 5 + \
+        [ctypes.c_void_p]
+    items = in_bytes // 1024
+    if ("rwc", w) not in _SHARED:   # one buffer pair per write ratio, shared by all rwc cases
+        _SHARED[("rwc", w)] = (torch.empty(items * 256, device="cuda"), torch.empty(items * 256 * w, device="cuda"))
+    a, b = _SHARED[("rwc", w)]
+    s = torch.cuda.current_stream().cuda_stream
+    f = (lambda: lib.membench_rwc(a.data_ptr(), b.data_ptr(), items, w, u, ntl, nts, blocks, s))
+    assert f() == 0
+    return f, in_bytes * (1 + w), (a, b, lib)
+
+
+def case_model(depth, work, lds_bytes, walk=0, ld=0, pairs=1799968):
+    """STFT memory-pipeline model (membench.hip k_model): LDS-DMA spans DEPTH pairs
+    ahead, WORK x 16 packed FMAs, 8 x 1 KB nt stores per pair; LDS pad sets occupancy"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libmembench.so"))
+    lib.membench_model.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    if "model" not in _SHARED:
+        _SHARED["model"] = (torch.empty(pairs * 512 + 4096, device="cuda"), torch.empty(pairs * 2048, device="cuda"))
+    a, b = _SHARED["model"]
+    s = torch.cuda.current_stream().cuda_stream
+    f = (lambda: lib.membench_model(a.data_ptr(), b.data_ptr(), pairs, 256, depth, work, lds_bytes, walk, ld, s))
+    assert f() == 0
+    return f, pairs * 10240, (a, b, lib)
+
+
 CASES = {
+    **{f"model_d{d}w{w}l{l}k{k}": (lambda d=d, w=w, l=l, k=k: case_model(d, w, l * 1024, k))
+       for d in (1, 2, 3) for w in (0, 12, 25) for l in (66, 50, 40, 32, 20) for k in (0, 1, 2)},
+    **{f"model_ld{ld}w{w}l{l}": (lambda ld=ld, w=w, l=l: case_model(1, w, l * 1024, 1, ld))
+       for ld in (1, 2) for w in (0, 12) for l in (66, 40, 20)},
+    **{f"rwc{w}u{u}l{l}s{s_}b{b}": (lambda w=w, u=u, l=l, s_=s_, b=b: case_rwc(w, u, l, s_, b))
+       for (w, u, l, s_) in [(4, 1, 1, 1), (4, 2, 1, 1), (4, 4, 1, 1), (4, 1, 0, 0), (4, 2, 0, 0), (4, 4, 0, 0),
+                             (4, 2, 0, 1), (4, 2, 1, 0), (1, 2, 1, 1), (1, 2, 0, 0), (4, 8, 1, 1)]
+       for b in (1024, 2048, 4096, 8192)},
     **{f"ex{e}": (lambda e=e: case_stft_exp(e)) for e in range(8)},
     "rw1": lambda: case_rw(1), "rw4": lambda: case_rw(4),
     **{f"rw{w}b{b}": (lambda w=w, b=b: case_rw(w, blocks=b)) for w in (1, 4) for b in (256, 512, 1024, 2048, 16384)},

@@ -71,6 +71,8 @@ extern "C" int membench_write(float* out, long long rows, int mode, int nt, int 
 // magnitudes) with parts switched off.  E bit0: no FFT, bit1: no stores
 // (guarded by an impossible value), bit2: no loads (synthetic samples).
 #include "../vv-dsp_amd/csrc/hip/fft_core.hpp"
+using vvh::vf2_t;
+using vvh::vf4_t;
 #include <cmath>
 #include <vector>
 
@@ -207,4 +209,181 @@ extern "C" int membench_rw(const float* in, float* out, long long n4, int w, int
     else if (w == 4) hipLaunchKernelGGL((k_rw<4>), dim3(blocks), dim3(256), 0, s, (const vf4*)in, (vf4*)out, n4);
     else return -1;
     return (int)hipGetLastError();
+}
+
+// Contiguous mixed stream: wave item i reads 1 KB at in + i KB and writes W KB
+// contiguous at out + i*W KB (the STFT's per-frame shape: hop 256 samples in,
+// one 4 KB row out).  U items are loaded before any is stored (loads in flight).
+template <int W, int U, bool NTL, bool NTS>
+__global__ void __launch_bounds__(256) k_rwc(const vf4* __restrict__ in, vf4* __restrict__ out, long long items) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long nw = (long long)gridDim.x * 4;
+    for (long long i0 = wave * U; i0 < items; i0 += nw * U) {
+        vf4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long i = i0 + u < items ? i0 + u : items - 1;
+            v[u] = NTL ? __builtin_nontemporal_load(in + i * 64 + lane) : in[i * 64 + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (i0 + u >= items) break;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                vf4* p = out + (i0 + u) * 64 * W + w * 64 + lane;
+                if (NTS) __builtin_nontemporal_store(v[u], p);
+                else *p = v[u];
+            }
+        }
+    }
+}
+
+extern "C" int membench_rwc(const float* in, float* out, long long items, int w, int u, int ntl, int nts, int blocks,
+                            void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const vf4* a = (const vf4*)in;
+    vf4* b = (vf4*)out;
+#define RWC(WW, UU, L, S)                                                                                  \
+    if (w == WW && u == UU && ntl == L && nts == S) {                                                      \
+        hipLaunchKernelGGL((k_rwc<WW, UU, L, S>), dim3(blocks), dim3(256), 0, s, a, b, items);             \
+        return (int)hipGetLastError();                                                                     \
+    }
+    RWC(4, 1, 1, 1) RWC(4, 2, 1, 1) RWC(4, 4, 1, 1) RWC(4, 1, 0, 0) RWC(4, 2, 0, 0) RWC(4, 4, 0, 0)
+    RWC(4, 2, 0, 1) RWC(4, 2, 1, 0) RWC(1, 2, 1, 1) RWC(1, 2, 0, 0) RWC(4, 8, 1, 1)
+#undef RWC
+    return -1;
+}
+
+// ---- model of the STFT bulk kernel's memory pipeline ------------------------
+// Persistent 256-thread blocks (4 independent waves), xcd_walk over frame
+// pairs, per pair: wait for the pair's 1280-float input span (LDS-DMA issued
+// DEPTH pairs ahead), read 32 floats of it from LDS, WORK x 16 dependent-free
+// v_pk_fma_f32 (stand-in for the FFT), 8 x 16 B/lane nt stores (two 4 KB rows).
+// Dynamic LDS pads the block to `lds_bytes` to set the occupancy.
+#include "../vv-dsp_amd/csrc/hip/fft_core.hpp"
+using vvh::vf2_t;
+using vvh::vf4_t;
+
+template <int DEPTH, int WORK, int WALK, int LD = 0>
+__global__ void __launch_bounds__(256) k_model(const float* __restrict__ sig, float* __restrict__ out, long long pairs,
+                                               long long hop) {
+    extern __shared__ __attribute__((aligned(16))) float dyn[];
+    // LD 0: the whole 1280-float span by LDS-DMA (5 ops); 1: only the 512 new floats by LDS-DMA (2 ops);
+    // 2: the 512 new floats into registers (2 x global_load_dwordx4, DEPTH must be 1)
+    constexpr int SPAN = 1280, NLD = LD == 0 ? 5 : 2, NST = 8;
+    vf4_t rg[2];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float* ring = dyn + wv * DEPTH * SPAN;
+    long long p, p_end, p_step;
+    if constexpr (WALK == 0) {   // 8 contiguous shares, one per XCD
+        vvh::xcd_walk(pairs, 4, wv, &p, &p_end, &p_step);
+    } else if constexpr (WALK == 1) {   // one front, consecutive waves -> consecutive pairs
+        p = (long long)blockIdx.x * 4 + wv;
+        p_step = (long long)gridDim.x * 4;
+        p_end = pairs;
+    } else {   // one front; each XCD (blockIdx % 8) takes a contiguous block of it
+        const long long ng = 8, nbg = ((long long)gridDim.x + 7) / 8;   // gridDim.x % 8 == 0 assumed
+        const long long wx = nbg * 4;                                     // wave slots per XCD
+        p = ((long long)blockIdx.x % ng) * wx + ((long long)blockIdx.x / ng) * 4 + wv;
+        p_step = ng * wx;
+        p_end = pairs;
+    }
+    p = vvh::uni<64>(p);
+    p_end = vvh::uni<64>(p_end);
+    p_step = vvh::uni<64>(p_step);
+    if (p >= p_end) return;
+    auto issue = [&](long long q, int slot) {
+        const float* s0 = sig + q * 2 * hop;
+        if constexpr (LD == 2) {
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rg[0]) : "v"(s0 + lane * 4) : "memory");
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rg[1]) : "v"(s0 + 256 + lane * 4) : "memory");
+        } else {
+            for (int u = 0; u < NLD; ++u) vvh::glds16(s0 + u * 256 + lane * 4, ring + slot * SPAN + u * 256);
+        }
+    };
+    // prologue: DEPTH spans in flight (past the end: re-issue the last pair, counted the same)
+    for (int d = 0; d < DEPTH; ++d) {
+        const long long q = p + d * p_step;
+        issue(q < p_end ? q : p, d);
+    }
+    vf2_t acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = vf2_t{(float)lane, 1.0f};
+    const vf2_t a = {0.999f, 0.999f}, b = {0.001f, 0.001f};
+    int slot = 0;
+    long long it = 0;
+    for (; p < p_end; p += p_step, ++it) {
+        // outstanding younger than this pair's span: (DEPTH-1) later spans + the stores between
+        if (it == 0) vvh::vm_wait<(DEPTH - 1) * NLD>();
+        else vvh::vm_wait<(DEPTH - 1) * (NLD + NST) + NST>();
+        const float* sp = ring + slot * SPAN;
+        if constexpr (LD == 2) {
+            acc[0] += vf2_t{rg[0].x, rg[0].y};
+            acc[1] += vf2_t{rg[0].z, rg[0].w};
+            acc[2] += vf2_t{rg[1].x, rg[1].y};
+            acc[3] += vf2_t{rg[1].z, rg[1].w};
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[r] += vf2_t{sp[lane + 64 * r], sp[256 + lane + 64 * r]};
+        }
+        vvh::lgkm_wait0();
+        {
+            const long long q = p + DEPTH * p_step;
+            issue(q < p_end ? q : p, slot);   // always NLD ops, so the counts stay exact
+        }
+        slot = slot + 1 == DEPTH ? 0 : slot + 1;
+#pragma unroll 1
+        for (int k = 0; k < WORK; ++k) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[r]) : "v"(a), "v"(b));
+#pragma unroll
+            for (int r = 0; r < 8; ++r) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[r]) : "v"(b), "v"(a));
+        }
+        float* o = out + p * 2048;
+#pragma unroll
+        for (int j = 0; j < NST; ++j) {
+            const vf4_t v = {acc[j].x, acc[j].y, acc[(j + 1) & 7].x, acc[(j + 1) & 7].y};
+            vvh::st16_nt_counted(reinterpret_cast<vf4_t*>(o) + j * 64 + lane, v);
+        }
+    }
+    vvh::vm_wait<0>();
+}
+
+extern "C" int membench_model(const float* sig, float* out, long long pairs, long long hop, int depth, int work,
+                              int lds_bytes, int walk, int ld, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+#define MODEL(D, W)                                                                                               \
+    if (depth == D && work == W) {                                                                                \
+        const void* k = walk == 0 ? (const void*)k_model<D, W, 0>                                                 \
+                        : walk == 1 ? (const void*)k_model<D, W, 1> : (const void*)k_model<D, W, 2>;              \
+        size_t need = (size_t)4 * D * 1280 * 4;                                                                   \
+        size_t lds = (size_t)lds_bytes > need ? (size_t)lds_bytes : need;                                         \
+        int per_cu = 0;                                                                                           \
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                       \
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds);                                 \
+        if (per_cu < 1) per_cu = 1;                                                                               \
+        if (walk == 0) hipLaunchKernelGGL((k_model<D, W, 0>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop); \
+        else if (walk == 1) hipLaunchKernelGGL((k_model<D, W, 1>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop); \
+        else hipLaunchKernelGGL((k_model<D, W, 2>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop); \
+        return (int)hipGetLastError();                                                                            \
+    }
+    if (ld == 0) { MODEL(1, 0) MODEL(1, 12) MODEL(1, 25) MODEL(2, 0) MODEL(2, 12) MODEL(2, 25) MODEL(3, 25) }
+#undef MODEL
+#define MODEL_LD(L, W)                                                                                              \
+    if (ld == L && depth == 1 && work == W) {                                                                       \
+        const void* k = (const void*)k_model<1, W, 1, L>;                                                           \
+        int per_cu = 0;                                                                                             \
+        size_t lds = (size_t)lds_bytes > 20480 ? (size_t)lds_bytes : 20480;                                         \
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds);                                   \
+        if (per_cu < 1) per_cu = 1;                                                                                 \
+        hipLaunchKernelGGL((k_model<1, W, 1, L>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop);     \
+        return (int)hipGetLastError();                                                                              \
+    }
+    MODEL_LD(1, 0) MODEL_LD(1, 12) MODEL_LD(2, 0) MODEL_LD(2, 12)
+#undef MODEL_LD
+    return -1;
 }

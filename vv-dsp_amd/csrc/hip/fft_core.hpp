@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace vvh {
 
@@ -49,17 +50,28 @@ __device__ __forceinline__ constexpr float cos16(int m) {
     }
 }
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
-    return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
-}
-__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
-
-// Streaming (non-temporal) global accesses: data touched exactly once.
+// Complex arithmetic as packed-f32 vector ops (v_pk_add/mul/fma_f32 with
+// op_sel swizzles and neg modifiers): one instruction per complex add and two
+// per complex multiply, instead of letting the SLP vectorizer pair unrelated
+// scalars (which costs a v_mov per operand).
 typedef float vf2_t __attribute__((ext_vector_type(2)));
 typedef float vf4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ vf2_t pk(float2 a) { return vf2_t{a.x, a.y}; }
+__device__ __forceinline__ float2 upk(vf2_t v) { return make_float2(v.x, v.y); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return upk(pk(a) + pk(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return upk(pk(a) - pk(b)); }
+// a*w = a.xx * w + a.yy * (-w.y, w.x)
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+    const vf2_t A = pk(a), W = pk(w);
+    return upk(A.xx * W + A.yy * (W.yx * vf2_t{-1.0f, 1.0f}));
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return upk(pk(a) * vf2_t{1.0f, -1.0f}); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return upk(pk(a) * s); }
+// -i*a (forward quarter turn) and +i*a
+__device__ __forceinline__ float2 cmul_mi(float2 a) { return upk(pk(a).yx * vf2_t{1.0f, -1.0f}); }
+__device__ __forceinline__ float2 cmul_pi(float2 a) { return upk(pk(a).yx * vf2_t{-1.0f, 1.0f}); }
+
+// Streaming (non-temporal) global accesses: data touched exactly once.
 __device__ __forceinline__ float2 ld_nt(const float2* p) {
     const vf2_t v = __builtin_nontemporal_load(reinterpret_cast<const vf2_t*>(p));
     return make_float2(v.x, v.y);
@@ -77,12 +89,13 @@ template <int R, bool FWD>
 __device__ __forceinline__ float2 twc(float2 v, int k) {
     const int m = ((k * (16 / R)) & 15);   // angle in units of 2*pi/16
     if (m == 0) return v;
-    if (m == 8) return make_float2(-v.x, -v.y);
-    if (m == 4) return FWD ? make_float2(v.y, -v.x) : make_float2(-v.y, v.x);
-    if (m == 12) return FWD ? make_float2(-v.y, v.x) : make_float2(v.y, -v.x);
+    if (m == 8) return upk(-pk(v));
+    if (m == 4) return FWD ? cmul_mi(v) : cmul_pi(v);
+    if (m == 12) return FWD ? cmul_pi(v) : cmul_mi(v);
     const float c = cos16(m);
     const float s = FWD ? -cos16(m + 12) : cos16(m + 12);   // sin(2*pi*m/16) = cos16(m-4)
-    return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+    const vf2_t V = pk(v);
+    return upk(V.xx * vf2_t{c, s} + V.yy * vf2_t{-s, c});
 }
 
 // In-register DFT of length R (1,2,4,8,16), natural order in and out.
@@ -120,7 +133,7 @@ struct Dft<4, FWD> {
         const float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
         const float2 s13 = cadd(v[1], v[3]), d13 = csub(v[1], v[3]);
         // d13 * W_4^1: forward -i, backward +i
-        const float2 r = FWD ? make_float2(d13.y, -d13.x) : make_float2(-d13.y, d13.x);
+        const float2 r = FWD ? cmul_mi(d13) : cmul_pi(d13);
         v[0] = cadd(s02, s13);
         v[2] = csub(s02, s13);
         v[1] = cadd(d02, r);
@@ -374,6 +387,22 @@ __device__ __forceinline__ void st16_nt_counted(vf4_t* p, vf4_t v) {
 }
 __device__ __forceinline__ void st4_counted(float* p, float v) {
     asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+// dword streaming store at wave-uniform base (SGPR pair) + 32-bit lane offset + IMM
+// (13-bit signed immediate: -4096..4095)
+template <int IMM>
+__device__ __forceinline__ void st4_nt_sbase(unsigned lane_off, float v, const void* base) {
+    static_assert(IMM >= -4096 && IMM <= 4095, "global offset range");
+    asm volatile("global_store_dword %0, %1, %2 offset:%3 nt" ::"v"(lane_off), "v"(v), "s"(base), "n"(IMM)
+                 : "memory");
+}
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
 }
 template <int CNT>
 __device__ __forceinline__ void vm_wait() {

@@ -114,7 +114,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr bool STAGE = VAR == 0 && MODE == 0 && G::NPASS > 1 && G::T > 1;
     constexpr bool GLDS = STAGE && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
     constexpr int SPAN = GLDS ? N + N / 2 : 1;   // floats per transform: hop <= N/2
-    constexpr int NST = 2 * (G::P / 4);          // 16 B stores per pair (both rows)
+    // T == 64 (one wave per transform): magnitudes go straight from registers as
+    // full-line dword stores (DIRECT); otherwise they are staged through LDS and
+    // written as 16 B/lane stores
+    constexpr bool DIRECT = GLDS && G::T == 64;
+    constexpr int NST = DIRECT ? 2 * G::P : 2 * (G::P / 4);   // stores per pair (both rows)
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
     __shared__ float2 lds[LDSN];
@@ -211,7 +215,58 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
         char* rowb = rowa + ROW * ES;
         const bool has_b = TAIL ? fa + 1 < frames : true;
-        if constexpr (STAGE) {
+        if constexpr (DIRECT) {
+            // Even slot j holds bins k = t + T j + r NB (lane-contiguous, 256 B
+            // aligned per store); its partner slot holds N - k, which for lanes
+            // t >= 1 covers N - k of the same magnitude.  Lane 0's partner bins
+            // are shifted by one slot (lane 0 writes the mirror of its own bin in
+            // slot j + 1, or its self-mirrored bin NB/2 + .. in the last slot), so
+            // that every store instruction covers one aligned 256 B block: full
+            // 128 B lines for the streaming stores, no LDS staging.
+            constexpr int J = G::NPT / 2, NB = G::NB, T = G::T;
+            float ea[J][R], eb[J][R], sa[R], sb[R];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int q = 2 * j * R + r;
+                    float2 A, B;
+                    pair_post<0>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                    ea[j][r] = A.x;
+                    eb[j][r] = B.x;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {   // lane 0's odd slot 1: bins NB/2 + (R-1-r) NB, their own mirrors
+                const int qm = Mi::normal(r);
+                float2 A2, B2;
+                pair_post<0>(v[qm], v[Mi::special(qm)], &A2, &B2);
+                sa[r] = A2.x;
+                sb[r] = B2.x;
+            }
+            const unsigned ve = 4u * (unsigned)t;
+            const unsigned vo = 4u * (unsigned)(t == 0 ? NB - T : NB - t);
+            const void* ra = rowa;
+            const void* rb = rowb;
+            static_for<0, J>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                static_for<0, R>([&](auto rc) {
+                    constexpr int r = decltype(rc)::value;
+                    st4_nt_sbase<4 * (T * j + r * NB)>(ve, ea[j][r], ra);
+                    st4_nt_sbase<4 * (T * j + r * NB)>(ve, eb[j][r], rb);
+                    float oa, ob;
+                    if constexpr (j + 1 < J) {
+                        oa = t == 0 ? ea[j + 1][r] : ea[j][r];
+                        ob = t == 0 ? eb[j + 1][r] : eb[j][r];
+                    } else {
+                        oa = t == 0 ? sa[r] : ea[j][r];
+                        ob = t == 0 ? sb[r] : eb[j][r];
+                    }
+                    st4_nt_sbase<4 * ((R - 1 - r) * NB - T * j)>(vo, oa, ra);
+                    st4_nt_sbase<4 * ((R - 1 - r) * NB - T * j)>(vo, ob, rb);
+                });
+            });
+        } else if constexpr (STAGE) {
             // both magnitude rows through the (now idle) exchange buffer, then
             // full-line 16 B/lane streaming stores: 2N/(4T) instead of 2P per lane
             float* sf = reinterpret_cast<float*>(my);
