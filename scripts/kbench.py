@@ -31,7 +31,16 @@ def case_c2c(n, batch, fwd=True):
     return (lambda: p(x, out=y)), 2 * batch * n * 8, (x, y, p)
 
 
-def case_r2c(n, batch):
+def case_r2c(n, batch, env=None):
+    if env:
+        inner = case_r2c(n, batch)
+        fn = inner[0]
+
+        def run():
+            os.environ[env[0]] = env[1]
+            fn()
+            os.environ[env[0]] = ""
+        return (run,) + tuple(inner[1:])
     x = torch.rand(batch, n, device="cuda")
     y = torch.empty(batch, n // 2 + 1, dtype=torch.complex64, device="cuda")
     p = vv.FftPlan(n, vv.R2C, vv.FWD, batch=batch)
@@ -45,7 +54,17 @@ def case_c2r(n, batch):
     return (lambda: p(X, out=y)), batch * n * 4 + batch * (n // 2 + 1) * 8, (X, y, p)
 
 
-def case_stft(nch, seconds, complex_out=False):
+def case_stft(nch, seconds, complex_out=False, env=None):
+    if env:   # experiment switch read by the launcher at each call
+        k, v = env
+        inner = case_stft(nch, seconds, complex_out)
+        fn = inner[0]
+
+        def run():
+            os.environ[k] = v
+            fn()
+            os.environ[k] = ""
+        return (run,) + tuple(inner[1:])
     n = seconds * 48000
     sig = torch.rand(nch, n, device="cuda") * 2 - 1
     st = vv.Stft(1024, 256)
@@ -145,6 +164,20 @@ def case_model(depth, work, lds_bytes, walk=0, ld=0, pairs=1799968):
     return f, pairs * 10240, (a, b, lib)
 
 
+def with_env(case, key, val):
+    """run a case with an environment switch the launcher reads at each call"""
+    def make():
+        inner = case()
+        fn = inner[0]
+
+        def run():
+            os.environ[key] = val
+            fn()
+            os.environ[key] = ""
+        return (run,) + tuple(inner[1:])
+    return make
+
+
 CASES = {
     **{f"model_d{d}w{w}l{l}k{k}": (lambda d=d, w=w, l=l, k=k: case_model(d, w, l * 1024, k))
        for d in (1, 2, 3) for w in (0, 12, 25) for l in (66, 50, 40, 32, 20) for k in (0, 1, 2)},
@@ -172,6 +205,7 @@ CASES = {
     "stftc": lambda: case_stft(8, 600, complex_out=True),
     "fir": lambda: case_fir(8, 1 << 24),
 }
+# A/B switches for launcher experiments: CASES["stftX"] = with_env(CASES["stft"], "VVHIP_EXP_...", "1")
 
 
 def main():

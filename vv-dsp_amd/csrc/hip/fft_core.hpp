@@ -331,23 +331,66 @@ __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
     if constexpr (G::T > 64) xsync<G::T>();   // next pass' writes must not race these reads
 }
 
-template <int N, bool FWD, int p, bool PAIRED>
+// The same exchange through a buffer of half the size (Geo<N>::LDS floats):
+// real parts first, then imaginary parts.  Twice the LDS instructions (b32
+// instead of b64), half the LDS footprint -- for kernels whose occupancy is
+// bounded by LDS.
+template <int N, int p, bool PAIRED>
+__device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
+    using G = Geo<N>;
+    constexpr int R = G::radix(p), Ns = G::ns(p), R2 = G::radix(p + 1);
+    float nx[G::P];
+#pragma unroll
+    for (int i = 0; i < G::P / R; ++i) {
+        const int b = bfly<N, p, PAIRED>(t, i);
+        const int base = (b / Ns) * Ns * R + (b % Ns);
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[G::pad(base + r * Ns)] = v[i * R + r].x;
+    }
+    xsync<G::T>();
+#pragma unroll
+    for (int i = 0; i < G::P / R2; ++i) {
+        const int b = bfly<N, p + 1, PAIRED>(t, i);
+#pragma unroll
+        for (int r = 0; r < R2; ++r) nx[i * R2 + r] = lds[G::pad(b + r * (N / R2))];
+    }
+    xsync<G::T>();   // one wave: LDS ops execute in order; across waves: s_barrier
+#pragma unroll
+    for (int i = 0; i < G::P / R; ++i) {
+        const int b = bfly<N, p, PAIRED>(t, i);
+        const int base = (b / Ns) * Ns * R + (b % Ns);
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[G::pad(base + r * Ns)] = v[i * R + r].y;
+    }
+    xsync<G::T>();
+#pragma unroll
+    for (int i = 0; i < G::P / R2; ++i) {
+        const int b = bfly<N, p + 1, PAIRED>(t, i);
+#pragma unroll
+        for (int r = 0; r < R2; ++r) v[i * R2 + r] = make_float2(nx[i * R2 + r], lds[G::pad(b + r * (N / R2))]);
+    }
+    if constexpr (G::T > 64) xsync<G::T>();
+}
+
+template <int N, bool FWD, int p, bool PAIRED, bool RI = false>
 struct PassChain {
     __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TwTab<N>& tw) {
         pass_compute<N, FWD, p, PAIRED>(v, t, tw);
         if constexpr (p + 1 < Geo<N>::NPASS) {
-            pass_exchange<N, p, PAIRED>(v, t, lds);
-            PassChain<N, FWD, p + 1, PAIRED>::run(v, t, lds, tw);
+            if constexpr (RI) pass_exchange_ri<N, p, PAIRED>(v, t, reinterpret_cast<float*>(lds));
+            else pass_exchange<N, p, PAIRED>(v, t, lds);
+            PassChain<N, FWD, p + 1, PAIRED, RI>::run(v, t, lds, tw);
         }
     }
 };
 
 // Full transform.  On entry v[r] = x[t + r*T] (r < P).  On exit register q
-// holds X[out_pos<N, PAIRED>(t, q)].
-template <int N, bool FWD, bool PAIRED = false>
+// holds X[out_pos<N, PAIRED>(t, q)].  RI: `lds` needs only Geo<N>::LDS floats
+// (pass_exchange_ri) instead of Geo<N>::LDS float2.
+template <int N, bool FWD, bool PAIRED = false, bool RI = false>
 __device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TwTab<N>& tw) {
     static_assert(!PAIRED || Geo<N>::CAN_PAIR, "mirror pairing needs >= 2 last-pass butterflies per thread");
-    PassChain<N, FWD, 0, PAIRED>::run(v, t, lds, tw);
+    PassChain<N, FWD, 0, PAIRED, RI>::run(v, t, lds, tw);
 }
 
 // ---- shared pieces of the persistent streaming kernels ---------------------

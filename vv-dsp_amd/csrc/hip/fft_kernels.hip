@@ -237,7 +237,10 @@ static hipError_t run_r2c(const float* in, float2* out, long long batch, long lo
     if (!tM || !t2M || !pM) return hipErrorOutOfMemory;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
     static int cap = 0;
-    if (!cap) cap = persistent_grid((const void*)k_r2c<M>, WG, 0, 1LL << 40);
+    // one resident workgroup per CU: measured 15-20 % faster than the 3 the
+    // LDS/VGPR budget allows (the partial-line n/2+1 rows combine better with
+    // fewer concurrent writers; profiles/r01_kbench_occupancy.jsonl)
+    if (!cap) cap = persistent_grid((const void*)k_r2c<M>, WG, 0, 1LL << 40, 1);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < cap ? need : cap);
     if (grid < 1) return hipSuccess;

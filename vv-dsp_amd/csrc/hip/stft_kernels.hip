@@ -120,7 +120,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr bool DIRECT = GLDS && G::T == 64;
     constexpr int NST = DIRECT ? 2 * G::P : 2 * (G::P / 4);   // stores per pair (both rows)
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
-    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
+    // DIRECT needs no staging buffer: the exchange goes through a half-size
+    // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
+    constexpr bool RI = DIRECT;
+    constexpr int XF = RI ? (G::LDS + 1) / 2 : G::LDS;   // float2 per transform
+    constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
     __shared__ float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
@@ -128,7 +132,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     __syncthreads();
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
-    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
     float w[G::P];
 #pragma unroll
     for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * G::T];
@@ -211,7 +215,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
-        fft_regs<N, true, true>(v, t, my, tw);
+        fft_regs<N, true, true, RI>(v, t, my, tw);
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
         char* rowb = rowa + ROW * ES;
         const bool has_b = TAIL ? fa + 1 < frames : true;

@@ -3,6 +3,7 @@
 // (device, kind, n) for the process lifetime; kernels stage them into LDS.
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
+#include <cstdlib>
 
 #include <cmath>
 #include <map>
@@ -135,7 +136,7 @@ const float2* pass_twiddles(int n) {
     });
 }
 
-int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks) {
+int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks, int max_per_cu) {
     static int cus = 0;
     if (cus == 0) {
         int dev = current_device();
@@ -146,6 +147,7 @@ int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long wor
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;
+    if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
     long long g = (long long)cus * per_cu;
     if (work_blocks < g) g = work_blocks;
     if (g < 1) g = 1;

@@ -43,7 +43,8 @@ constexpr size_t SINK_FLOATS = 1u << 18;   // 1 MiB = 4096 waves x 64 lanes
 float* store_sink();
 
 // Persistent-grid sizing: resident blocks for `kernel` x CUs, capped by work.
-int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks);
+// CUs x resident workgroups of `kernel` (capped at max_per_cu when > 0), at most work_blocks
+int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks, int max_per_cu = 0);
 
 // ---- pow2 register/LDS FFTs (fft_kernels.hip) -----------------------------
 bool c2c_supported(long long n);           // pow2, 2..4096
