@@ -180,7 +180,7 @@ def with_env(case, key, val):
 
 CASES = {
     **{f"model_d{d}w{w}l{l}k{k}": (lambda d=d, w=w, l=l, k=k: case_model(d, w, l * 1024, k))
-       for d in (1, 2, 3) for w in (0, 12, 25) for l in (66, 50, 40, 32, 20) for k in (0, 1, 2)},
+       for d in (1, 2, 3) for w in (0, 12, 25) for l in (66, 50, 40, 32, 20) for k in (0, 1, 2, 3, 4)},
     **{f"model_ld{ld}w{w}l{l}": (lambda ld=ld, w=w, l=l: case_model(1, w, l * 1024, 1, ld))
        for ld in (1, 2) for w in (0, 12) for l in (66, 40, 20)},
     **{f"rwc{w}u{u}l{l}s{s_}b{b}": (lambda w=w, u=u, l=l, s_=s_, b=b: case_rwc(w, u, l, s_, b))

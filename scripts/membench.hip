@@ -282,12 +282,18 @@ __global__ void __launch_bounds__(256) k_model(const float* __restrict__ sig, fl
         p = (long long)blockIdx.x * 4 + wv;
         p_step = (long long)gridDim.x * 4;
         p_end = pairs;
-    } else {   // one front; each XCD (blockIdx % 8) takes a contiguous block of it
+    } else if constexpr (WALK == 2) {   // one front; each XCD (blockIdx % 8) takes a contiguous block of it
         const long long ng = 8, nbg = ((long long)gridDim.x + 7) / 8;   // gridDim.x % 8 == 0 assumed
         const long long wx = nbg * 4;                                     // wave slots per XCD
         p = ((long long)blockIdx.x % ng) * wx + ((long long)blockIdx.x / ng) * 4 + wv;
         p_step = ng * wx;
         p_end = pairs;
+    } else {   // not persistent: block b owns pairs [b*4*PPW, (b+1)*4*PPW), its waves interleaved
+        constexpr long long PPW = WALK == 3 ? 16 : 4;
+        p = (long long)blockIdx.x * 4 * PPW + wv;
+        p_step = 4;
+        p_end = (long long)(blockIdx.x + 1) * 4 * PPW;
+        if (p_end > pairs) p_end = pairs;
     }
     p = vvh::uni<64>(p);
     p_end = vvh::uni<64>(p_end);
@@ -358,7 +364,9 @@ extern "C" int membench_model(const float* sig, float* out, long long pairs, lon
 #define MODEL(D, W)                                                                                               \
     if (depth == D && work == W) {                                                                                \
         const void* k = walk == 0 ? (const void*)k_model<D, W, 0>                                                 \
-                        : walk == 1 ? (const void*)k_model<D, W, 1> : (const void*)k_model<D, W, 2>;              \
+                        : walk == 1 ? (const void*)k_model<D, W, 1>                                               \
+                        : walk == 2 ? (const void*)k_model<D, W, 2>                                               \
+                        : walk == 3 ? (const void*)k_model<D, W, 3> : (const void*)k_model<D, W, 4>;              \
         size_t need = (size_t)4 * D * 1280 * 4;                                                                   \
         size_t lds = (size_t)lds_bytes > need ? (size_t)lds_bytes : need;                                         \
         int per_cu = 0;                                                                                           \
@@ -367,7 +375,9 @@ extern "C" int membench_model(const float* sig, float* out, long long pairs, lon
         if (per_cu < 1) per_cu = 1;                                                                               \
         if (walk == 0) hipLaunchKernelGGL((k_model<D, W, 0>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop); \
         else if (walk == 1) hipLaunchKernelGGL((k_model<D, W, 1>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop); \
-        else hipLaunchKernelGGL((k_model<D, W, 2>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop); \
+        else if (walk == 2) hipLaunchKernelGGL((k_model<D, W, 2>), dim3(cus * per_cu), dim3(256), lds, s, sig, out, pairs, hop); \
+        else if (walk == 3) hipLaunchKernelGGL((k_model<D, W, 3>), dim3((pairs + 63) / 64), dim3(256), lds, s, sig, out, pairs, hop); \
+        else hipLaunchKernelGGL((k_model<D, W, 4>), dim3((pairs + 15) / 16), dim3(256), lds, s, sig, out, pairs, hop); \
         return (int)hipGetLastError();                                                                            \
     }
     if (ld == 0) { MODEL(1, 0) MODEL(1, 12) MODEL(1, 25) MODEL(2, 0) MODEL(2, 12) MODEL(2, 25) MODEL(3, 25) }

@@ -484,6 +484,21 @@ __device__ __forceinline__ void xcd_walk(long long total, int F, int slot, long 
     *step = nbg * F;
 }
 
+// Work sequence of transform slot `slot` (of F per block): with chunk > 0 the
+// launch is not persistent -- block b owns items [b*chunk, (b+1)*chunk), its
+// slots interleaved -- otherwise the persistent xcd_walk.
+__device__ __forceinline__ void work_walk(long long total, int F, int slot, long long chunk, long long* first,
+                                          long long* end, long long* step) {
+    if (chunk > 0) {
+        *first = (long long)blockIdx.x * chunk + slot;
+        *step = F;
+        const long long e = (long long)(blockIdx.x + 1) * chunk;
+        *end = e < total ? e : total;
+    } else {
+        xcd_walk(total, F, slot, first, end, step);
+    }
+}
+
 // Workgroup geometry: 256 threads (several transforms per block) unless one
 // transform needs more threads.
 template <int N>

@@ -73,10 +73,10 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     static int grid_cap = 0;
     if (!grid_cap) grid_cap = persistent_grid((const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;
-    int grid = (int)(need < grid_cap ? need : grid_cap);
+    const int grid = (int)(need < grid_cap ? need : grid_cap);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_c2c<N, FWD>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist,
-                       pas, tab, scale);
+    hipLaunchKernelGGL((k_c2c<N, FWD>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pas, tab,
+                       scale);
     return hipGetLastError();
 }
 

@@ -78,7 +78,7 @@ template <int N, bool BULK>
 __global__ void __launch_bounds__(Wg<N>::value)
 k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float* y, long long n,
            long long nch, long long x_stride, long long y_stride, const float* prefix, long long cnt,
-           long long qlo, long long qhi, const float2* gpass, const float2* gtab, float* sink) {
+           long long qlo, long long qhi, const float2* gpass, const float2* gtab, float* sink, long long chunk) {
     using G = Geo<N>;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     constexpr int SPAN = BULK ? N + (3 * N) / 4 : 1;   // N + Lout, Lout <= 3N/4
@@ -96,7 +96,7 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
     float2* my = lds + slot * G::LDS;
     const long long lout = N - le;
     long long p, p_end, p_step;
-    xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+    work_walk(nch * cnt, F, slot, chunk, &p, &p_end, &p_step);
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
     p_step = uni<G::T>(p_step);
@@ -234,9 +234,9 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
         if constexpr (FIR_BULK<N>) {
             if (!cap_b) cap_b = persistent_grid((const void*)k_fir_pair<N, true>, WG, 0, 1LL << 40);
             const long long cnt = ql - qf, need = (nch * cnt + F - 1) / F;
-            const int grid = (int)(need < cap_b ? need : cap_b);
+            const int grid = (int)(need < cap_b ? need : cap_b);   // persistent (chunked launches measured slower)
             hipLaunchKernelGGL((k_fir_pair<N, true>), dim3(grid), dim3(WG), 0, s, lm1, le, H, x, y, n, nch,
-                               x_stride, y_stride, prefix, cnt, 0LL, qf, pN, tN, sink);
+                               x_stride, y_stride, prefix, cnt, 0LL, qf, pN, tN, sink, 0LL);
         }
     }
     const long long ecnt = qf + (ppc - ql);   // edge pairs per channel: [0, qf) and [ql, ppc)
@@ -245,7 +245,7 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
         const long long need = (nch * ecnt + F - 1) / F;
         const int grid = (int)(need < cap_e ? need : cap_e);
         hipLaunchKernelGGL((k_fir_pair<N, false>), dim3(grid), dim3(WG), 0, s, lm1, le, H, x, y, n, nch,
-                           x_stride, y_stride, prefix, ecnt, qf, ql, pN, tN, sink);
+                           x_stride, y_stride, prefix, ecnt, qf, ql, pN, tN, sink, 0LL);
     }
     return hipGetLastError();
 }

@@ -15,16 +15,19 @@
 // k_stft_half<M>: one frame per M = nfft/2 point complex FFT plus the real
 // split step (nfft = 256 and 4096, where N cannot be mirror-paired).
 //
-// Scheduling: the frame pairs are split into 8 contiguous shares, one per XCD
-// (xcd_walk: blockIdx % 8 selects the share), and the slots of one XCD stride
-// through their share, so the nfft-hop overlap of consecutive frames is re-read
-// from that XCD's L2, never from HBM by another XCD.  The bulk variant (VAR 0)
-// streams each pair's input span (N + N/2 samples) into LDS with
-// global_load_lds_dwordx4 one pair ahead, waits on hand-counted vmcnt, and
-// writes magnitude rows through LDS as full 16-byte non-temporal stores; the
-// register variant (VAR 1) covers unaligned hops/channel strides and VAR 2 the
-// zero-padded tail frames.  Window values are per-thread constants in
-// registers; twiddles live in LDS.
+// Scheduling: the bulk variant (VAR 0) is launched non-persistently, one
+// workgroup per 16 consecutive frame pairs per transform slot, the slots of a
+// workgroup interleaved, so the nfft-hop overlap of neighbouring frames is
+// re-read from the same CU's L1/L2 and the dispatcher balances the CUs (no
+// straggler tail).  VAR 1 (unaligned hops / channel strides) and VAR 2 (the
+// zero-padded tail frames) are persistent and walk XCD-aware shares
+// (xcd_walk).  VAR 0 streams each pair's input span (N + hop samples) into LDS
+// with global_load_lds_dwordx4 one pair ahead and waits on hand-counted
+// vmcnt.  For N = 1024 (one wave per transform) the magnitudes go straight
+// from registers as full-line dword streaming stores and the FFT exchanges
+// through a half-size real/imaginary buffer (3 workgroups per CU); other N
+// stage the rows through LDS for 16-byte stores.  Window values are
+// per-thread constants in registers; twiddles live in LDS.
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
 
@@ -107,7 +110,7 @@ template <int N, int MODE, int VAR>
 __global__ void __launch_bounds__(Wg<N>::value)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
-            long long out_ch_stride, const float2* gpass, const float2* gtab) {
+            long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk) {
     using G = Geo<N>;
     using Mi = Mirror<N>;
     constexpr bool TAIL = VAR == 2;
@@ -139,7 +142,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
 
     const long long pairs = nch * ppc;
     long long p, p_end, p_step;
-    xcd_walk(pairs, F, slot, &p, &p_end, &p_step);
+    work_walk(pairs, F, slot, chunk, &p, &p_end, &p_step);
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
     p_step = uni<G::T>(p_step);
@@ -476,12 +479,22 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
         static int cap[3] = {0, 0, 0};
+        // The bulk launch is NOT persistent: one workgroup per STFT_CHUNK pairs
+        // per transform slot, so the hardware dispatcher balances the CUs and
+        // the launch has no straggler tail (measured 8-13 % faster than the
+        // persistent walk at 16-64 pairs per slot; profiles/r01_kbench_chunk.jsonl)
+        constexpr long long STFT_CHUNK = 16;
         auto launch = [&](auto kern, int var, long long pair0, long long cnt) {
             if (!cap[var]) cap[var] = persistent_grid((const void*)kern, WG, 0, 1LL << 40);
             const long long need = (nch * cnt + F - 1) / F;
-            const int grid = (int)(need < cap[var] ? need : cap[var]);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0, cnt,
-                               win, out, out_ch_stride, pN, tN);
+            long long grid = need < cap[var] ? need : cap[var];
+            long long chunk = 0;
+            if (var == 0) {
+                chunk = STFT_CHUNK * F;
+                grid = (nch * cnt + chunk - 1) / chunk;
+            }
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0,
+                               cnt, win, out, out_ch_stride, pN, tN, chunk);
         };
         // 16 B aligned output rows allow the staged 16 B/lane stores
         bool aligned = ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0 && N >= 4;
