@@ -335,6 +335,17 @@ __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
 // real parts first, then imaginary parts.  Twice the LDS instructions (b32
 // instead of b64), half the LDS footprint -- for kernels whose occupancy is
 // bounded by LDS.
+// Per-exchange padding of the dword layout: for N = 1024 (passes 16, 16, 4)
+// these make both b32 exchanges bank-conflict-free (64 banks of 4 B, 32-lane
+// groups; the b64 padding G::pad costs 2x on every read), and keep all
+// compile-time offsets additive.  Largest index 1075 < G::LDS.
+template <int N, int p>
+__device__ __forceinline__ constexpr int ri_pad(int e) {
+    if constexpr (N == 1024 && p == 0) return e + (e >> 5);
+    else if constexpr (N == 1024 && p == 1) return e + 4 * (e >> 7) + 8 * (e >> 8);
+    else return Geo<N>::pad(e);
+}
+
 template <int N, int p, bool PAIRED>
 __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
     using G = Geo<N>;
@@ -345,14 +356,14 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
         const int b = bfly<N, p, PAIRED>(t, i);
         const int base = (b / Ns) * Ns * R + (b % Ns);
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[G::pad(base + r * Ns)] = v[i * R + r].x;
+        for (int r = 0; r < R; ++r) lds[ri_pad<N, p>(base + r * Ns)] = v[i * R + r].x;
     }
     xsync<G::T>();
 #pragma unroll
     for (int i = 0; i < G::P / R2; ++i) {
         const int b = bfly<N, p + 1, PAIRED>(t, i);
 #pragma unroll
-        for (int r = 0; r < R2; ++r) nx[i * R2 + r] = lds[G::pad(b + r * (N / R2))];
+        for (int r = 0; r < R2; ++r) nx[i * R2 + r] = lds[ri_pad<N, p>(b + r * (N / R2))];
     }
     xsync<G::T>();   // one wave: LDS ops execute in order; across waves: s_barrier
 #pragma unroll
@@ -360,14 +371,14 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
         const int b = bfly<N, p, PAIRED>(t, i);
         const int base = (b / Ns) * Ns * R + (b % Ns);
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[G::pad(base + r * Ns)] = v[i * R + r].y;
+        for (int r = 0; r < R; ++r) lds[ri_pad<N, p>(base + r * Ns)] = v[i * R + r].y;
     }
     xsync<G::T>();
 #pragma unroll
     for (int i = 0; i < G::P / R2; ++i) {
         const int b = bfly<N, p + 1, PAIRED>(t, i);
 #pragma unroll
-        for (int r = 0; r < R2; ++r) v[i * R2 + r] = make_float2(nx[i * R2 + r], lds[G::pad(b + r * (N / R2))]);
+        for (int r = 0; r < R2; ++r) v[i * R2 + r] = make_float2(nx[i * R2 + r], lds[ri_pad<N, p>(b + r * (N / R2))]);
     }
     if constexpr (G::T > 64) xsync<G::T>();
 }

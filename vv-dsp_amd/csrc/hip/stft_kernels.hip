@@ -102,8 +102,8 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
 // Frame pairs (2j, 2j+1) of one channel, j in [pair0, pair0 + ppc): pairs never
 // span channels, so a channel's rows do not depend on how channels are grouped
 // into calls or shards.
-//   VAR 0: bulk (both frames inside the signal), magnitude rows staged in LDS
-//          and written with 16 B/lane stores (16 B aligned output rows)
+//   VAR 0: bulk (both frames inside the signal), input spans by LDS-DMA,
+//          magnitude rows as full-line streaming stores (16 B aligned rows)
 //   VAR 1: bulk, stores straight from registers
 //   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
 template <int N, int MODE, int VAR>
