@@ -183,6 +183,8 @@ CASES = {
        for d in (1, 2, 3) for w in (0, 12, 25) for l in (66, 50, 40, 32, 20) for k in (0, 1, 2, 3, 4)},
     **{f"model_ld{ld}w{w}l{l}": (lambda ld=ld, w=w, l=l: case_model(1, w, l * 1024, 1, ld))
        for ld in (1, 2) for w in (0, 12) for l in (66, 40, 20)},
+    **{f"model4_ld{ld}w{w}": (lambda ld=ld, w=w: case_model(1, w, 50 * 1024, 4, ld + 10))
+       for ld in (0, 1, 2) for w in (0, 12)},
     **{f"rwc{w}u{u}l{l}s{s_}b{b}": (lambda w=w, u=u, l=l, s_=s_, b=b: case_rwc(w, u, l, s_, b))
        for (w, u, l, s_) in [(4, 1, 1, 1), (4, 2, 1, 1), (4, 4, 1, 1), (4, 1, 0, 0), (4, 2, 0, 0), (4, 4, 0, 0),
                              (4, 2, 0, 1), (4, 2, 1, 0), (1, 2, 1, 1), (1, 2, 0, 0), (4, 8, 1, 1)]

@@ -395,5 +395,14 @@ extern "C" int membench_model(const float* sig, float* out, long long pairs, lon
     }
     MODEL_LD(1, 0) MODEL_LD(1, 12) MODEL_LD(2, 0) MODEL_LD(2, 12)
 #undef MODEL_LD
+#define MODEL_LD4(L, W)                                                                                             \
+    if (ld == L + 10 && depth == 1 && work == W) {                                                                  \
+        size_t lds = (size_t)lds_bytes > 20480 ? (size_t)lds_bytes : 20480;                                         \
+        (void)hipFuncSetAttribute((const void*)k_model<1, W, 4, L>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+        hipLaunchKernelGGL((k_model<1, W, 4, L>), dim3((pairs + 15) / 16), dim3(256), lds, s, sig, out, pairs, hop); \
+        return (int)hipGetLastError();                                                                              \
+    }
+    MODEL_LD4(0, 12) MODEL_LD4(1, 12) MODEL_LD4(2, 12) MODEL_LD4(0, 0) MODEL_LD4(2, 0)
+#undef MODEL_LD4
     return -1;
 }

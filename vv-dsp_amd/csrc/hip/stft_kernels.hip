@@ -106,11 +106,12 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
 //          magnitude rows as full-line streaming stores (16 B aligned rows)
 //   VAR 1: bulk, stores straight from registers
 //   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
+// N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
 template <int N, int MODE, int VAR>
-__global__ void __launch_bounds__(Wg<N>::value)
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && VAR == 0 && MODE == 0) ? 3 : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
-            long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk) {
+            long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink) {
     using G = Geo<N>;
     using Mi = Mirror<N>;
     constexpr bool TAIL = VAR == 2;
@@ -131,8 +132,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     __shared__ float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
-    stage_twiddles<N, WG>(ltab, gpass, gtab);
-    __syncthreads();
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
@@ -140,32 +139,90 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
 #pragma unroll
     for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * G::T];
 
+    int kb[G::NPT];   // last-pass butterfly of each slot (loop invariant)
+#pragma unroll
+    for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
+    constexpr long long ES = MODE == 1 ? 8 : 4;            // bytes per bin
+    constexpr long long ROW = MODE == 2 ? N / 2 + 1 : N;   // bins per row
+    // rows of one pair from the registers, plain stores (unaligned / tail pairs)
+    auto store_generic = [&](float2* v, char* rowa, char* rowb, bool has_b) {
+        if constexpr (G::T == 1) {
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                float2 A, B;
+                pair_post<MODE>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                put_bin<MODE, N>(rowa, q, A);
+                if (has_b) put_bin<MODE, N>(rowb, q, B);
+            }
+        } else {
+            // even slots hold bins k, their partner slots hold N-k: one post
+            // per (k, N-k) pair, stored at both (real input -> mirror = conj)
+#pragma unroll
+            for (int i = 0; i < G::NPT; i += 2) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int q = i * R + r, qm = Mi::normal(q);
+                    float2 A, B;
+                    pair_post<MODE>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                    float2 Am = MODE == 0 ? A : cconj(A), Bm = MODE == 0 ? B : cconj(B);
+                    if (i == 0) {   // thread 0: slot 1 is butterfly NB/2, its own mirror
+                        float2 A2, B2;
+                        pair_post<MODE>(v[qm], v[Mi::special(qm)], &A2, &B2);
+                        Am = select2(t == 0, A2, Am);
+                        Bm = select2(t == 0, B2, Bm);
+                    }
+                    const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
+                    put_bin<MODE, N>(rowa, k, A);
+                    put_bin<MODE, N>(rowa, km, Am);
+                    if (has_b) {
+                        put_bin<MODE, N>(rowb, k, B);
+                        put_bin<MODE, N>(rowb, km, Bm);
+                    }
+                }
+            }
+        }
+    };
     const long long pairs = nch * ppc;
     long long p, p_end, p_step;
     work_walk(pairs, F, slot, chunk, &p, &p_end, &p_step);
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
     p_step = uni<G::T>(p_step);
-    if (p >= p_end) return;   // uniform per transform (F == 1 whenever T > 64)
+    const bool any = p < p_end;   // uniform per transform
     // (channel, first frame) of a pair; this launch covers frames
     // [2*pair0, 2*(pair0 + ppc)) of every channel
     auto locate = [&](long long q, long long* cc, long long* ff) {
         *cc = q / ppc;
         *ff = 2 * (pair0 + q - *cc * ppc);
     };
-    long long c, fa;
-    locate(p, &c, &fa);
+    long long c = 0, fa = 0;
+    if (any) locate(p, &c, &fa);
     float xa[G::P], xb[G::P];
     // GLDS: the pair's span [fa*hop, fa*hop + hop + N) goes HBM/L2 -> LDS by
     // 16 B/lane LDS-DMA, issued right after the previous span was read, so it
     // lands while that pair is transformed -- no VGPRs held across iterations.
     float* span = span_all + (GLDS ? slot * SPAN : 0);
+    // Pairs that reach past the end of the signal (the zero-padded tail, at
+    // most a few per channel) fill the span with ordinary bounds-checked loads
+    // and LDS stores instead: the compiler waits on those itself, and being
+    // younger than every hand-counted operation they keep the counts valid.
     auto issue_span = [&](long long cc, long long ff) {
         const float* s0 = sig + cc * ch_stride + ff * hop;
         const int len = (int)(N + hop), lane = t & 63;
-        for (int u = t >> 6; u * 256 < len; u += G::T / 64) {
-            const int e = u * 256 + lane * 4;
-            glds16(s0 + (e < len ? e : 0), span + u * 256);
+        if (ff * hop + len <= n) {
+            for (int u = t >> 6; u * 256 < len; u += G::T / 64) {
+                const int e = u * 256 + lane * 4;
+                glds16(s0 + (e < len ? e : 0), span + u * 256);
+            }
+        } else {
+            const long long left = n - ff * hop;   // samples of this span inside the signal
+            for (int u = t >> 6; u * 256 < len; u += G::T / 64) {
+                const int e = u * 256 + lane * 4;
+                vf4_t q;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[k] = e + k < left ? s0[e + k] : 0.0f;
+                *reinterpret_cast<vf4_t*>(span + u * 256 + lane * 4) = q;
+            }
         }
     };
     auto load_pair = [&](long long cc, long long ff) {
@@ -185,13 +242,12 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             }
         }
     };
-    load_pair(c, fa);
+    // the first span's DMA is in flight while the block stages its twiddles
+    if (any) load_pair(c, fa);
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    __syncthreads();
+    if (!any) return;
     if constexpr (GLDS) vm_wait<0>();
-    int kb[G::NPT];   // last-pass butterfly of each slot (loop invariant)
-#pragma unroll
-    for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
-    constexpr long long ES = MODE == 1 ? 8 : 4;            // bytes per bin
-    constexpr long long ROW = MODE == 2 ? N / 2 + 1 : N;   // bins per row
     for (; p < p_end; p += p_step) {
         const bool more = p + p_step < p_end;
         long long cn = c, fn = fa;
@@ -221,7 +277,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         fft_regs<N, true, true, RI>(v, t, my, tw);
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
         char* rowb = rowa + ROW * ES;
-        const bool has_b = TAIL ? fa + 1 < frames : true;
+        const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
         if constexpr (DIRECT) {
             // Even slot j holds bins k = t + T j + r NB (lane-contiguous, 256 B
             // aligned per store); its partner slot holds N - k, which for lanes
@@ -254,7 +310,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             const unsigned ve = 4u * (unsigned)t;
             const unsigned vo = 4u * (unsigned)(t == 0 ? NB - T : NB - t);
             const void* ra = rowa;
-            const void* rb = rowb;
+            const void* rb = has_b ? rowb : (void*)sink;   // counted stores must all issue
             static_for<0, J>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 static_for<0, R>([&](auto rc) {
@@ -305,48 +361,17 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 const vf4_t a = *reinterpret_cast<const vf4_t*>(sf + e);
                 const vf4_t b = *reinterpret_cast<const vf4_t*>(sf + N + e);
                 if constexpr (GLDS) {   // counted by the vm_wait<NST> above: exactly NST per pair
+                    char* rb = has_b ? rowb : reinterpret_cast<char*>(sink);
                     st16_nt_counted(reinterpret_cast<vf4_t*>(rowa) + (t + G::T * j), a);
-                    st16_nt_counted(reinterpret_cast<vf4_t*>(rowb) + (t + G::T * j), b);
+                    st16_nt_counted(reinterpret_cast<vf4_t*>(rb) + (t + G::T * j), b);
                 } else {
                     __builtin_nontemporal_store(a, reinterpret_cast<vf4_t*>(rowa) + (t + G::T * j));
                     __builtin_nontemporal_store(b, reinterpret_cast<vf4_t*>(rowb) + (t + G::T * j));
                 }
             }
             xsync<G::T>();   // the next transform's first exchange reuses `my`
-        } else if constexpr (G::T == 1) {
-#pragma unroll
-            for (int q = 0; q < G::P; ++q) {
-                float2 A, B;
-                pair_post<MODE>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
-                put_bin<MODE, N>(rowa, q, A);
-                if (has_b) put_bin<MODE, N>(rowb, q, B);
-            }
         } else {
-            // even slots hold bins k, their partner slots hold N-k: one post
-            // per (k, N-k) pair, stored at both (real input -> mirror = conj)
-#pragma unroll
-            for (int i = 0; i < G::NPT; i += 2) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int q = i * R + r, qm = Mi::normal(q);
-                    float2 A, B;
-                    pair_post<MODE>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
-                    float2 Am = MODE == 0 ? A : cconj(A), Bm = MODE == 0 ? B : cconj(B);
-                    if (i == 0) {   // thread 0: slot 1 is butterfly NB/2, its own mirror
-                        float2 A2, B2;
-                        pair_post<MODE>(v[qm], v[Mi::special(qm)], &A2, &B2);
-                        Am = select2(t == 0, A2, Am);
-                        Bm = select2(t == 0, B2, Bm);
-                    }
-                    const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
-                    put_bin<MODE, N>(rowa, k, A);
-                    put_bin<MODE, N>(rowa, km, Am);
-                    if (has_b) {
-                        put_bin<MODE, N>(rowb, k, B);
-                        put_bin<MODE, N>(rowb, km, Bm);
-                    }
-                }
-            }
+            store_generic(v, rowa, rowb, has_b);
         }
         c = cn;
         fa = fn;
@@ -479,33 +504,46 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
         static int cap[3] = {0, 0, 0};
-        // The bulk launch is NOT persistent: one workgroup per STFT_CHUNK pairs
-        // per transform slot, so the hardware dispatcher balances the CUs and
-        // the launch has no straggler tail (measured 8-13 % faster than the
-        // persistent walk at 16-64 pairs per slot; profiles/r01_kbench_chunk.jsonl)
-        constexpr long long STFT_CHUNK = 16;
+        // The bulk launch is NOT persistent: one workgroup per `cps` pairs per
+        // transform slot, so the hardware dispatcher balances the CUs and the
+        // launch has no straggler tail (measured 8-13 % faster than the
+        // persistent walk at 16-64 pairs per slot; profiles/r01_kbench_chunk.jsonl).
+        // Small jobs use fewer pairs per slot so that the grid still spreads over
+        // all CUs (>= ~2048 workgroups) instead of serialising on a few.
+        const long long bulk_pairs = nch * ppc;
+        long long cps = bulk_pairs / (2048LL * F);
+        cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
+        float* sink = store_sink();
+        if (!sink) return hipErrorOutOfMemory;
         auto launch = [&](auto kern, int var, long long pair0, long long cnt) {
             if (!cap[var]) cap[var] = persistent_grid((const void*)kern, WG, 0, 1LL << 40);
             const long long need = (nch * cnt + F - 1) / F;
             long long grid = need < cap[var] ? need : cap[var];
             long long chunk = 0;
             if (var == 0) {
-                chunk = STFT_CHUNK * F;
+                chunk = cps * F;
                 grid = (nch * cnt + chunk - 1) / chunk;
             }
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0,
-                               cnt, win, out, out_ch_stride, pN, tN, chunk);
+                               cnt, win, out, out_ch_stride, pN, tN, chunk, sink);
         };
         // 16 B aligned output rows allow the staged 16 B/lane stores
         bool aligned = ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0 && N >= 4;
         // T >= 64: VAR 0 also reads its input spans by 16 B LDS-DMA
         if (Geo<N>::T >= 64)
             aligned = aligned && hop % 4 == 0 && hop <= N / 2 && ((uintptr_t)sig & 15) == 0 && (ch_stride & 3) == 0;
-        if (mpc > 0) {
-            if (aligned) launch(k_stft_pair<N, MODE, 0>, 0, 0LL, mpc);
-            else launch(k_stft_pair<N, MODE, 1>, 1, 0LL, mpc);
+        // the VAR 0 kernels that read spans by LDS-DMA run the tail pairs too:
+        // one launch for the whole job
+        constexpr bool FUSE_TAIL = MODE == 0 && Geo<N>::NPASS > 1 && Geo<N>::T >= 64;
+        if (aligned && FUSE_TAIL) {
+            launch(k_stft_pair<N, MODE, 0>, 0, 0LL, ppc);
+        } else {
+            if (mpc > 0) {
+                if (aligned) launch(k_stft_pair<N, MODE, 0>, 0, 0LL, mpc);
+                else launch(k_stft_pair<N, MODE, 1>, 1, 0LL, mpc);
+            }
+            if (tpc > 0) launch(k_stft_pair<N, MODE, 2>, 2, mpc, tpc);
         }
-        if (tpc > 0) launch(k_stft_pair<N, MODE, 2>, 2, mpc, tpc);
     } else {
         constexpr int M = N / 2;
         const float2* tM = twiddle_table(M);
