@@ -508,10 +508,12 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // transform slot, so the hardware dispatcher balances the CUs and the
         // launch has no straggler tail (measured 8-13 % faster than the
         // persistent walk at 16-64 pairs per slot; profiles/r01_kbench_chunk.jsonl).
-        // Small jobs use fewer pairs per slot so that the grid still spreads over
-        // all CUs (>= ~2048 workgroups) instead of serialising on a few.
+        // Small jobs use fewer pairs per slot: just enough that the grid fits the
+        // resident workgroup slots once (one round, every wave pipelining its
+        // pairs) instead of a few long chains or several short rounds.
         const long long bulk_pairs = nch * ppc;
-        long long cps = bulk_pairs / (2048LL * F);
+        if (!cap[0]) cap[0] = persistent_grid((const void*)k_stft_pair<N, MODE, 0>, WG, 0, 1LL << 40);
+        long long cps = (bulk_pairs + (long long)F * cap[0] - 1) / ((long long)F * cap[0]);
         cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
         float* sink = store_sink();
         if (!sink) return hipErrorOutOfMemory;
