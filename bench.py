@@ -298,8 +298,9 @@ def main():
             "output": "[ch][frame][1024] f32 magnitudes (stft.c:133-139)",
             "parallelism": f"dp{world} (channel shards, no data-path collective)"},
         "roofline": {"kernel": "vvh::k_stft_pair<1024,0,0> (LDS-DMA frame spans + Hann + two frames per "
-                               "1024-pt complex FFT + |X| rows, 16 B stores) + its zero-padded tail launch "
-                               "k_stft_pair<1024,0,2>; kernel_ms = HIP events around both on the launch stream",
+                               "1024-pt complex FFT + |X| rows as full-line streaming stores; the zero-padded "
+                               "tail pairs run in the same launch); kernel_ms = HIP events around the launch on "
+                               "the launch stream",
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,

@@ -82,6 +82,18 @@ def case_fir(nch, n, taps=257):
     return (lambda: p(x, out=y)), 2 * nch * n * 4, (x, y, p)
 
 
+def case_hilbert(n, batch):
+    x = torch.rand(batch, n, device="cuda") * 2 - 1
+    vv.hilbert(x)   # plan/tables
+    return (lambda: vv.hilbert(x)), batch * n * 12, (x,)
+
+
+def case_dct(n, batch):
+    x = torch.rand(batch, n, device="cuda") * 2 - 1
+    vv.dct(x)
+    return (lambda: vv.dct(x)), batch * n * 8, (x,)
+
+
 def case_copy(nbytes):
     a = torch.empty(nbytes // 4, device="cuda")
     b = torch.empty_like(a)
@@ -206,6 +218,8 @@ CASES = {
     "stft60": lambda: case_stft(1, 60),
     "stftc": lambda: case_stft(8, 600, complex_out=True),
     "fir": lambda: case_fir(8, 1 << 24),
+    "hilbert1024": lambda: case_hilbert(1024, 65536),
+    "dct1024": lambda: case_dct(1024, 131072),
 }
 # A/B switches for launcher experiments: CASES["stftX"] = with_env(CASES["stft"], "VVHIP_EXP_...", "1")
 

@@ -500,3 +500,63 @@ def test_golden_mel(amd, golden):
     assert _normwise(amd.mfcc(g["log_mel_kiss"], 13, 22.0), g["mfcc_kiss"]) <= 5e-5
     assert _normwise(amd.mfcc_pipeline(g["power"], 512, 26, 13, 16000.0, 0.0, 8000.0, 22.0, 1e-10),
                      g["mfcc_kiss"]) <= 5e-5
+
+
+# ---------------------------------------------------------------- batched single-pass Hilbert / DCT-II
+@pytest.mark.parametrize("n", [2, 8, 16, 128, 256, 1024, 2048, 4096])
+def test_hilbert_batched_device(vdev, n):
+    """vv_dsp_hilbert_analytic over a batch of rows (two rows per complex FFT,
+    odd batch -> last row alone) vs scipy.signal.hilbert in f64."""
+    import scipy.signal
+    import torch
+    rng = np.random.default_rng(100 + n)
+    for batch in (1, 5, 64):
+        x = rng.standard_normal((batch, n)).astype(np.float32)
+        z = vdev.hilbert(torch.from_numpy(x).cuda()).cpu().numpy()
+        ref = scipy.signal.hilbert(x.astype(np.float64), axis=1)
+        assert _normwise(z, ref) <= 2e-6 * max(1.0, np.log2(n)), (n, batch, _normwise(z, ref))
+        np.testing.assert_allclose(z.real, x, rtol=0, atol=0)   # the real part is the input itself
+
+
+@pytest.mark.parametrize("n", [2, 4, 16, 32, 128, 256, 512, 1024, 2048, 4096])
+def test_dct2_batched_device(vdev, n):
+    """DCT-II over a batch of rows (two rows per complex FFT where the FFT can
+    be mirror-paired) vs scipy.fft.dct(type 2)/2 in f64 (dct.c:21-30)."""
+    import scipy.fft
+    import torch
+    rng = np.random.default_rng(200 + n)
+    for batch in (1, 3, 64):
+        x = rng.standard_normal((batch, n)).astype(np.float32)
+        y = vdev.dct(torch.from_numpy(x).cuda()).cpu().numpy()
+        ref = scipy.fft.dct(x.astype(np.float64), 2, axis=1) / 2
+        assert _normwise(y, ref) <= 2e-6 * max(1.0, np.log2(n)), (n, batch, _normwise(y, ref))
+
+
+@pytest.mark.parametrize("policy", [0, 1, 2, 3])
+def test_dct_nan_policy_matches_reference(amd, ref, policy):
+    """NaN/Inf handling of vv_dsp_dct_execute (dct.c:98,130, nan_policy.c):
+    same status as the reference, same non-finite pattern, finite values within
+    tolerance -- for the single-pass (1024) and the multi-pass (1000) paths."""
+    import ctypes as C
+    for n in (1024, 1000):
+        rng = np.random.default_rng(n + policy)
+        x = rng.standard_normal(n).astype(np.float32)
+        x[[3, 77]] = np.nan
+        if policy != 3:
+            # clamp maps +-Inf to +-FLT_MAX, whose FFT-based transform overflows where the
+            # reference's O(n^2) f32 sums do not: only NaN is compared under clamp
+            x[500] = np.inf
+        outs = []
+        for lib in (amd, ref):
+            lib.lib.vv_dsp_set_nan_policy.argtypes = [C.c_int]
+            lib.lib.vv_dsp_set_nan_policy(policy)
+            try:
+                outs.append(lib.dct_status(x, 2, False))
+            finally:
+                lib.lib.vv_dsp_set_nan_policy(0)
+        (st_a, y_a), (st_r, y_r) = outs
+        assert st_a == st_r, (n, policy, st_a, st_r)
+        if st_a == 0:
+            fa, fr = np.isfinite(y_a), np.isfinite(y_r)
+            assert np.array_equal(fa, fr) and np.array_equal(np.isnan(y_a), np.isnan(y_r))
+            np.testing.assert_allclose(y_a[fa], y_r[fr], rtol=1e-4, atol=1e-2)

@@ -156,13 +156,17 @@ class VvDsp:
         return z.view(np.complex64)
 
     def dct(self, x, dct_type=DCT_II, inverse=False):
-        x = np.ascontiguousarray(x, np.float32)
-        y = np.zeros_like(x)
-        f = self.lib.vv_dsp_dct_inverse if inverse else self.lib.vv_dsp_dct_forward
-        st = f(len(x), dct_type, _fp(x), _fp(y))
+        st, y = self.dct_status(x, dct_type, inverse)
         if st != OK:
             raise RuntimeError(f"dct status {st}")
         return y
+
+    def dct_status(self, x, dct_type=DCT_II, inverse=False):
+        """(status, output) of vv_dsp_dct_forward / vv_dsp_dct_inverse."""
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros_like(x)
+        f = self.lib.vv_dsp_dct_inverse if inverse else self.lib.vv_dsp_dct_forward
+        return f(len(x), dct_type, _fp(x), _fp(y)), y
 
     def fir_design_lowpass(self, taps, fc, wkind=FIRWIN_HANNING):
         h = np.zeros(taps, np.float32)

@@ -1,0 +1,244 @@
+// analytic_kernels.hip -- single-pass Hilbert analytic signal and DCT-II for
+// gfx950: one HBM read of the input rows and one write of the output rows,
+// two rows per complex FFT, everything else in registers/LDS.
+//
+// Hilbert (src/spectral/hilbert.c:14-75): z = IFFT(m . FFT(x)) with the
+// one-sided mask m = 1 at DC and N/2, 2 on 1..N/2-1, 0 above, and the
+// backward transform scaled by 1/N (fft_kiss.c:45,70-73).  Two real rows a, b
+// share one forward FFT of a + i b; since the mask is linear,
+//   w = IFFT(m . FFT(a + i b)) = za + i zb,  za = a + i ha,  zb = b + i hb,
+// so  Re w = a - hb  and  Im w = ha + b:  the two analytic signals are
+//   za = (a, Im w - b),  zb = (b, a - Re w)
+// with a and b kept in registers.  After the forward Stockham FFT thread t
+// holds Z[t + T m], exactly the input set of the inverse FFT (register
+// re-index, no LDS re-order), and after the inverse it holds w[t + T m], the
+// same index set as its a[m], b[m].  Replaces R2C + mask + C2C (36 B/point of
+// HBM traffic) with 12 B/point.
+//
+// DCT-II (src/spectral/dct.c:21-30, X[k] = sum x[n] cos(pi (n+1/2) k / N)) by
+// Makhoul's permutation v[j] = x[2j] (j < N/2), v[N-1-j] = x[2j+1], an N-point
+// FFT and X[k] = Re(W_4N^k V[k]).  Two rows per complex FFT with the
+// mirror-paired last pass: Va[k] = (Z[k] + conj Z[N-k])/2,
+// Vb[k] = (Z[k] - conj Z[N-k])/2i straight from registers.  The NaN policy
+// (src/core/nan_policy.c) is applied as the input is read and as the output is
+// written, like dct.c:98,130 (propagate, zero, clamp; the error policy keeps
+// the multi-pass path, which must scan first).
+// Replaces copy + policy + permute + R2C + post (≈40 B/point) with 8 B/point.
+#include "fft_core.hpp"
+#include "vvhip_internal.hpp"
+
+namespace vvh {
+
+template <int N>
+__global__ void __launch_bounds__(Wg<N>::value)
+k_hilbert_pair(const float* __restrict__ x, float2* __restrict__ z, long long batch, long long x_dist,
+               long long z_dist, const float2* gpass, const float2* gtab) {
+    using G = Geo<N>;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
+    __shared__ float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    const long long pairs = (batch + 1) / 2;
+    const float inv = 1.0f / (float)N;
+    for (long long p = uni<G::T>((long long)blockIdx.x * F + slot); p < pairs; p += (long long)gridDim.x * F) {
+        const long long ra = 2 * p;
+        const bool hb = ra + 1 < batch;
+        const float* xa = x + ra * x_dist;
+        const float* xb = hb ? xa + x_dist : xa;   // unconditional loads (no exec-masked branch)
+        float a[G::P], b[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            a[r] = xa[t + r * G::T];
+            b[r] = xb[t + r * G::T];
+        }
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) b[r] = hb ? b[r] : 0.0f;
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(a[r], b[r]);
+        fft_regs<N, true>(v, t, my, tw);
+        float2 u[G::P];
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int m = q / G::RL + G::NPT * (q % G::RL);   // out_pos<N>(t, q) = t + T*m
+            const int k = t + G::T * m;
+            const float s = (k == 0 || 2 * k == N) ? 1.0f : (2 * k < N ? 2.0f : 0.0f);
+            u[m] = cscale(v[q], s);
+        }
+        fft_regs<N, false>(u, t, my, tw);
+        float2* za = z + ra * z_dist;
+        float2* zb = za + z_dist;
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int m = q / G::RL + G::NPT * (q % G::RL);
+            const int k = t + G::T * m;
+            const float2 w = cscale(u[q], inv);
+            st_nt(make_float2(a[m], w.y - b[m]), za + k);
+            if (hb) st_nt(make_float2(b[m], a[m] - w.x), zb + k);
+        }
+    }
+}
+
+bool hilbert_fused_supported(long long n) { return n >= 2 && n <= 4096 && (n & (n - 1)) == 0; }
+
+hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long long batch, hipStream_t s) {
+    if (batch <= 0) return hipSuccess;
+#define VVH_HIL(NN)                                                                                         \
+    case NN: {                                                                                              \
+        const float2* tab = twiddle_table(NN);                                                              \
+        const float2* pas = pass_twiddles(NN);                                                              \
+        if (!tab || !pas) return hipErrorOutOfMemory;                                                       \
+        constexpr int WG = Wg<NN>::value, F = Wg<NN>::F;                                                    \
+        static int cap = 0;                                                                                 \
+        if (!cap) cap = persistent_grid((const void*)k_hilbert_pair<NN>, WG, 0, 1LL << 40);                 \
+        const long long need = ((batch + 1) / 2 + F - 1) / F;                                               \
+        const int grid = (int)(need < cap ? need : cap);                                                    \
+        hipLaunchKernelGGL(k_hilbert_pair<NN>, dim3(grid), dim3(WG), 0, s, x, z, batch, n, n, pas, tab);    \
+        return hipGetLastError();                                                                           \
+    }
+    switch (n) {
+        VVH_HIL(2) VVH_HIL(4) VVH_HIL(8) VVH_HIL(16) VVH_HIL(32) VVH_HIL(64) VVH_HIL(128) VVH_HIL(256)
+        VVH_HIL(512) VVH_HIL(1024) VVH_HIL(2048) VVH_HIL(4096)
+        default: return hipErrorInvalidValue;
+    }
+#undef VVH_HIL
+}
+
+// NaN policy (src/core/nan_policy.c): 0 propagate, 1 zero, 3 clamp
+template <int POL>
+__device__ __forceinline__ float nan_fix(float v) {
+    if constexpr (POL == 0) return v;
+    else if constexpr (POL == 1) return isfinite(v) ? v : 0.0f;
+    else return isfinite(v) ? v : (isnan(v) ? 0.0f : (v > 0 ? 3.402823466e+38f : -3.402823466e+38f));
+}
+
+template <int N, int POL>
+__global__ void __launch_bounds__(Wg<N>::value)
+k_dct2_pair(const float* __restrict__ x, float* __restrict__ X, long long batch, long long dist,
+            const float2* gpass, const float2* gtab, const float2* __restrict__ tw4n) {
+    using G = Geo<N>;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
+    __shared__ float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    // W_4N^k for this thread's output bins (loop invariant)
+    float2 wk[G::P];
+    int kq[G::P];
+#pragma unroll
+    for (int q = 0; q < G::P; ++q) {
+        kq[q] = out_pos<N, true>(t, q);
+        wk[q] = tw4n[kq[q]];
+    }
+    const long long pairs = (batch + 1) / 2;
+    for (long long p = uni<G::T>((long long)blockIdx.x * F + slot); p < pairs; p += (long long)gridDim.x * F) {
+        const long long ra = 2 * p;
+        const bool hb = ra + 1 < batch;
+        const float* xa = x + ra * dist;
+        const float* xb = hb ? xa + dist : xa;   // unconditional loads; b zeroed below when absent
+        float2 v[G::P];
+        if constexpr (G::T == 1) {   // one thread owns the row pair: permute in registers
+#pragma unroll
+            for (int j = 0; j < G::P; ++j) {
+                const int src = j < N / 2 ? 2 * j : 2 * N - 2 * j - 1;
+                const float bv = xb[src];
+                v[j] = make_float2(nan_fix<POL>(xa[src]), hb ? nan_fix<POL>(bv) : 0.0f);
+            }
+        } else {   // coalesced loads, Makhoul permutation through LDS
+            float a[G::P], b[G::P];
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                a[r] = xa[t + r * G::T];
+                b[r] = xb[t + r * G::T];
+            }
+#pragma unroll
+            for (int r = 0; r < G::P; ++r)
+                my[G::pad(t + r * G::T)] = make_float2(nan_fix<POL>(a[r]), hb ? nan_fix<POL>(b[r]) : 0.0f);
+            xsync<G::T>();
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const int j = t + r * G::T;
+                v[r] = my[G::pad(j < N / 2 ? 2 * j : 2 * N - 2 * j - 1)];
+            }
+            xsync<G::T>();   // the FFT's first exchange overwrites `my`
+        }
+        fft_regs<N, true, true>(v, t, my, tw);
+        float* oa = X + ra * dist;
+        float* ob = oa + dist;
+        float2 o[G::P];   // (Xa[k], Xb[k]) at k = kq[q]
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const float2 Z = v[q], Zm = mirror_of<N, true>(v, t, q);
+            const float2 Va = make_float2(0.5f * (Z.x + Zm.x), 0.5f * (Z.y - Zm.y));
+            const float2 Vb = make_float2(0.5f * (Z.y + Zm.y), -0.5f * (Z.x - Zm.x));
+            const float2 W = wk[q];
+            // policy on the output too (dct.c:130)
+            o[q] = make_float2(nan_fix<POL>(W.x * Va.x - W.y * Va.y), nan_fix<POL>(W.x * Vb.x - W.y * Vb.y));
+        }
+        if constexpr (G::T == 1) {
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                oa[kq[q]] = o[q].x;
+                if (hb) ob[kq[q]] = o[q].y;
+            }
+        } else {   // back to natural order through LDS: lane-contiguous, full-line stores
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) my[G::pad(kq[q])] = o[q];
+            xsync<G::T>();
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const int k = t + r * G::T;
+                const float2 x2 = my[G::pad(k)];
+                __builtin_nontemporal_store(x2.x, oa + k);
+                if (hb) __builtin_nontemporal_store(x2.y, ob + k);
+            }
+            xsync<G::T>();
+        }
+    }
+}
+
+bool dct2_fused_supported(long long n) {
+    // mirror pairing needs >= 2 last-pass butterflies per thread (not 256, 4096)
+    return n >= 2 && n <= 2048 && (n & (n - 1)) == 0 && n != 256;
+}
+
+hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long batch, int policy, hipStream_t s) {
+    if (batch <= 0) return hipSuccess;
+    const float2* tw4n = twiddle_table((int)(4 * n));
+    if (!tw4n) return hipErrorOutOfMemory;
+#define VVH_DCT(NN)                                                                                          \
+    case NN: {                                                                                               \
+        const float2* tab = twiddle_table(NN);                                                               \
+        const float2* pas = pass_twiddles(NN);                                                               \
+        if (!tab || !pas) return hipErrorOutOfMemory;                                                        \
+        constexpr int WG = Wg<NN>::value, F = Wg<NN>::F;                                                     \
+        static int cap = 0;                                                                                  \
+        if (!cap) cap = persistent_grid((const void*)k_dct2_pair<NN, 0>, WG, 0, 1LL << 40);                  \
+        const long long need = ((batch + 1) / 2 + F - 1) / F;                                                \
+        const int grid = (int)(need < cap ? need : cap);                                                     \
+        if (policy == 1)                                                                                     \
+            hipLaunchKernelGGL((k_dct2_pair<NN, 1>), dim3(grid), dim3(WG), 0, s, x, X, batch, n, pas, tab, tw4n); \
+        else if (policy == 3)                                                                                \
+            hipLaunchKernelGGL((k_dct2_pair<NN, 3>), dim3(grid), dim3(WG), 0, s, x, X, batch, n, pas, tab, tw4n); \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_dct2_pair<NN, 0>), dim3(grid), dim3(WG), 0, s, x, X, batch, n, pas, tab, tw4n); \
+        return hipGetLastError();                                                                            \
+    }
+    switch (n) {
+        VVH_DCT(2) VVH_DCT(4) VVH_DCT(8) VVH_DCT(16) VVH_DCT(32) VVH_DCT(64) VVH_DCT(128) VVH_DCT(512)
+        VVH_DCT(1024) VVH_DCT(2048)
+        default: return hipErrorInvalidValue;
+    }
+#undef VVH_DCT
+}
+
+}  // namespace vvh

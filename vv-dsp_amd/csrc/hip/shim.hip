@@ -617,6 +617,10 @@ int vvhip_hilbert_device(const float* d_x, size_t n, size_t batch, float* d_z, v
     if (!d_x || !d_z) return ST_NULL;
     if (n == 0) return ST_SIZE;
     hipStream_t s = (hipStream_t)stream;
+    if (hilbert_fused_supported((long long)n)) {   // one pass: rows in, analytic rows out
+        HIPCHK(launch_hilbert_fused((long long)n, d_x, (float2*)d_z, (long long)batch, s), ST_INTERNAL);
+        return ST_OK;
+    }
     const size_t nh = n / 2 + 1;
     Scratch half(s);
     HIPCHK(half.alloc(8 * nh * batch), ST_INTERNAL);
@@ -664,6 +668,10 @@ int vvhip_dct_device(const float* d_in, float* d_out, size_t n, size_t batch, in
     if ((type != 2 && type != 3 && type != 4) || (dir != 1 && dir != -1)) return ST_RANGE;
     hipStream_t s = (hipStream_t)stream;
     const long long N = (long long)n, B = (long long)batch;
+    if (type == 2 && dir > 0 && nan_policy != 2 && dct2_fused_supported(N)) {   // one pass, policy on read
+        HIPCHK(launch_dct2_fused(N, d_in, d_out, B, nan_policy, s), ST_INTERNAL);
+        return ST_OK;
+    }
     Scratch xin(s), flag(s), v(s), V(s);
     HIPCHK(xin.alloc(sizeof(float) * n * batch), ST_INTERNAL);
     HIPCHK(hipMemcpyAsync(xin.p, d_in, sizeof(float) * n * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);

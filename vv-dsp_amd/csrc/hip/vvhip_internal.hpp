@@ -101,6 +101,11 @@ hipError_t launch_scale_real(float* p, long long count, float s, hipStream_t st)
 hipError_t launch_scale_cpx(float2* p, long long count, float s, hipStream_t st);
 
 // ---- DCT / Hilbert helpers (spectral_kernels.hip) ----------------------
+// single-pass analytic signal / DCT-II (analytic_kernels.hip): rows [batch][n]
+bool hilbert_fused_supported(long long n);
+hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long long batch, hipStream_t s);
+bool dct2_fused_supported(long long n);
+hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long batch, int policy, hipStream_t s);
 hipError_t launch_hilbert_mask(long long n, const float2* half, float2* full, long long batch,
                                long long half_dist, hipStream_t s);
 hipError_t launch_dct2_pre(long long n, const float* x, float* v, long long batch, hipStream_t s);
