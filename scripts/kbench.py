@@ -209,6 +209,18 @@ CASES = {
     "wr8nt": lambda: case_wr(2, 1), "wr16": lambda: case_wr(3, 0), "wr16nt": lambda: case_wr(3, 1),
     "copy1G": lambda: case_copy(1 << 29),
     "c2c1024": lambda: case_c2c(1024, 65536),
+    # large power-of-two (four-step) and Bluestein lengths; VVHIP_FS_* select the variant
+    "c2c2p20": lambda: case_c2c(1 << 20, 64),
+    "c2c2p20old": with_env(lambda: case_c2c(1 << 20, 64), "VVHIP_FS_OLD", "1"),
+    **{f"c2c2p20v{v}": with_env(lambda: case_c2c(1 << 20, 64), "VVHIP_FS_VAR", str(v)) for v in (1, 2, 3)},
+    **{f"c2c2p17v{v}": with_env(lambda: case_c2c(1 << 17, 512), "VVHIP_FS_VAR", str(v)) for v in (1, 2, 3)},
+    **{f"c2c2p20ch{c}": with_env(lambda: case_c2c(1 << 20, 64), "VVHIP_FS_CHUNK_MB", str(c)) for c in (0, 16, 32, 128)},
+    "c2c2p17": lambda: case_c2c(1 << 17, 512),
+    "c2c2p17old": with_env(lambda: case_c2c(1 << 17, 512), "VVHIP_FS_OLD", "1"),
+    "c2c2p13": lambda: case_c2c(1 << 13, 8192),
+    "c2c2p22": lambda: case_c2c(1 << 22, 16),
+    "blue48000": lambda: case_c2c(48000, 1024),
+    "blue48000old": with_env(lambda: case_c2c(48000, 1024), "VVHIP_FS_OLD", "1"),
     "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),
     "c2c4096": lambda: case_c2c(4096, 16384),
     "c2c256": lambda: case_c2c(256, 262144),

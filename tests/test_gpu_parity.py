@@ -152,6 +152,29 @@ def test_large_pow2_batched_device(vdev):
     assert _normwise(y, ref) <= 2e-6
 
 
+@pytest.mark.parametrize("n,b,chunk_mb", [(1 << 17, 5, "1"), (1 << 20, 2, "0"), (8192, 7, "")])
+def test_large_pow2_chunked_batch(vdev, n, b, chunk_mb):
+    """Two-pass four-step over a batch, the batch split into Infinity-Cache
+    sized chunks (VVHIP_FS_CHUNK_MB: 1 -> one transform per chunk, 0 -> the whole
+    batch at once), both directions, against NumPy f64 per transform."""
+    import os
+    import torch
+    rng = np.random.default_rng(n + b)
+    x = (rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)
+    xd = torch.from_numpy(x).cuda()
+    old = os.environ.get("VVHIP_FS_CHUNK_MB", "")
+    os.environ["VVHIP_FS_CHUNK_MB"] = chunk_mb
+    try:
+        yf = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xd).cpu().numpy()
+        yb = vdev.FftPlan(n, vdev.C2C, vdev.BWD, batch=b)(xd).cpu().numpy()
+    finally:
+        os.environ["VVHIP_FS_CHUNK_MB"] = old
+    x64 = x.astype(np.complex128)
+    for i in range(b):
+        assert _normwise(yf[i], np.fft.fft(x64[i])) <= 2e-6, i
+        assert _normwise(yb[i], np.fft.ifft(x64[i])) <= 2e-6, i
+
+
 def test_impulse_known_answer(amd):
     """tests/fft_backend_tests.c:70-99 and spectral_tests.c:14-35 of the reference."""
     for n in (8, 16, 1024):
@@ -560,3 +583,58 @@ def test_dct_nan_policy_matches_reference(amd, ref, policy):
             fa, fr = np.isfinite(y_a), np.isfinite(y_r)
             assert np.array_equal(fa, fr) and np.array_equal(np.isnan(y_a), np.isnan(y_r))
             np.testing.assert_allclose(y_a[fa], y_r[fr], rtol=1e-4, atol=1e-2)
+
+
+# ---------------------------------------------------------------- host-buffer pipeline
+@pytest.mark.parametrize("chunk_mb", ["1", "3"])
+def test_stft_host_pipeline_matches_device(amd, vdev, orc, chunk_mb, monkeypatch):
+    """vv_dsp_stft_spectrogram with host buffers above the pipeline threshold runs
+    frame chunks on two lanes (shim.hip run_lanes); chunks start on even frames, so
+    every frame pair is the one a single launch forms and the rows are
+    bit-identical to the one-launch host call; within one f32 ulp of the
+    device-pointer call (whose unaligned channel stride sends the zero-padded
+    tail pair through the register-load kernel variant), and within the harness
+    bound of the reference restatement."""
+    import torch
+    rng = np.random.default_rng(11)
+    n = 10 * 48000 + 333                       # 1874 frames, ragged tail
+    x = rng.uniform(-1, 1, n).astype(np.float32)
+    monkeypatch.setenv("VVHIP_HOST_CHUNK_MB", "1024")
+    one = amd.spectrogram(x, 1024, 256)
+    monkeypatch.setenv("VVHIP_HOST_CHUNK_MB", chunk_mb)
+    mag = amd.spectrogram(x, 1024, 256)
+    dev = vdev.Stft(1024, 256).spectrogram(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert mag.shape == one.shape == dev.shape == (1 + (n - 1024 + 256) // 256, 1024)
+    assert np.array_equal(mag, one)
+    np.testing.assert_allclose(mag, dev, rtol=2.5e-7, atol=0)
+    ref = orc.spectrogram(x[: 48000 * 2], 1024, 256)   # first 2 s: a bounded oracle sample
+    close(mag[: ref.shape[0] - 4], ref[: ref.shape[0] - 4], factor=2.0)
+
+
+def test_fft_host_pipeline_matches_device(amd_lib_path, vdev, monkeypatch):
+    """A batched plan executed on host buffers (vv_dsp_fft_make_plan_many +
+    vv_dsp_fft_execute) in 1 MiB chunks on two lanes equals the device call."""
+    import ctypes as C
+    import torch
+    monkeypatch.setenv("VVHIP_HOST_CHUNK_MB", "1")
+    L = C.CDLL(amd_lib_path)
+    L.vv_dsp_fft_make_plan_many.argtypes = [C.c_size_t, C.c_int, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]
+    L.vv_dsp_fft_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.vv_dsp_fft_destroy.argtypes = [C.c_void_p]
+    rng = np.random.default_rng(12)
+    for kind, n, b in ((C2C, 1024, 301), (R2C, 2048, 257), (C2C, 1 << 16, 5)):
+        if kind == C2C:
+            x = (rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)
+            y = np.empty_like(x)
+        else:
+            x = (rng.random((b, n)) - 0.5).astype(np.float32)
+            y = np.empty((b, n // 2 + 1), np.complex64)
+        p = C.c_void_p()
+        assert L.vv_dsp_fft_make_plan_many(n, kind, FWD, b, C.byref(p)) == OK
+        try:
+            assert L.vv_dsp_fft_execute(p, x.ctypes.data, y.ctypes.data) == OK
+        finally:
+            L.vv_dsp_fft_destroy(p)
+        d = vdev.FftPlan(n, vdev.C2C if kind == C2C else vdev.R2C, vdev.FWD, batch=b)(
+            torch.from_numpy(x).cuda()).cpu().numpy()
+        assert np.array_equal(y, d), (kind, n, b)

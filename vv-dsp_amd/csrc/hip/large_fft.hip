@@ -1,25 +1,314 @@
 // large_fft.hip -- power-of-two C2C transforms longer than one workgroup's
-// register/LDS FFT (n > 4096, up to 2^24), as a four-step FFT over the fused
-// batched kernels of fft_kernels.hip.
+// register/LDS FFT (n > 4096, up to 2^24), and Bluestein for other lengths.
 //
 // The reference computes every power of two with one radix-2 DIT
-// (src/spectral/fft_kiss.c:27-74).  Here n = N1*N2 (N1, N2 <= 4096) and
+// (src/spectral/fft_kiss.c:27-74).  Here n = N1*N2 and
 //   X[k1 + N1*k2] = sum_n2 W_N2^(n2 k2) * W_n^(n2 k1) * sum_n1 x[n1 N2 + n2] W_N1^(n1 k1)
-// runs as: transpose [N1][N2] -> [N2][N1]; N2 row FFTs of length N1; transpose
-// with the twiddle W_n^(n2 k1) fused; N1 row FFTs of length N2; transpose to
-// natural order.  Five HBM passes of 8n bytes each -- bandwidth-bound like the
-// rest of the path.  The backward 1/n is split as 1/N1 and 1/N2 over the two
-// FFT passes.
+//
+// n <= 2^20 (N1, N2 <= 1024): TWO HBM passes, no transposes.
+//   columns: a workgroup owns G = 16 adjacent columns n2 of [N1][N2]; lane l
+//            works on column l % G, so every load x[n1][n2..n2+15] and every
+//            store Y[k1][n2..n2+15] is a 128-B line.  N1-pt FFT down each
+//            column, times W_n^(n2 k1), stored in place of the column.
+//   rows:    a workgroup owns G = 16 adjacent rows k1; loads are row-contiguous
+//            (lanes along the row); the last Stockham exchange re-maps the
+//            threads so lanes run across the G rows, and the stores
+//            X[k1..k1+15 + N1*k2] are 128-B lines again.
+//   Batches are processed in chunks whose intermediate fits the 256 MiB
+//   Infinity Cache, so the rows pass reads the columns pass's output on-die.
+// n > 2^20: transpose -> N1-pt FFTs -> twiddled transpose -> N2-pt FFTs ->
+//   transpose (five passes of 8n bytes each way).
+// The backward 1/n is applied once, in the last pass.
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
 #include <vector>
 
 namespace vvh {
+
+// ---------------------------------------------------------------------------
+// Two-pass four-step
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wg_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// G transforms of length N per workgroup; LDS region per transform of S
+// elements (floats when RI, float2 otherwise).  S is odd, so the same offset in
+// the G regions falls in G different banks (lanes of one instruction work on
+// different transforms in the interleaved mapping).
+template <int N, int G, bool RI>
+struct FsGeo {
+    using Ge = Geo<N>;
+    static constexpr int T = Ge::T;
+    static constexpr int THREADS = G * T;
+    static constexpr int S = Ge::LDS | 1;
+    static constexpr int LDS_BYTES = G * S * (RI ? 4 : 8);
+    static_assert(THREADS <= 1024 && Ge::NPASS >= 2, "two-pass four-step geometry");
+};
+
+// Stockham exchange after pass p; the writer is thread wt of transform wj, the
+// reader thread rt of transform rj (a re-map of the workgroup when they differ).
+template <int N, int p, int S, bool RI>
+__device__ __forceinline__ void fs_exchange(float2* v, void* lds, int wj, int wt, int rj, int rt) {
+    using Ge = Geo<N>;
+    constexpr int R = Ge::radix(p), Ns = Ge::ns(p), R2 = Ge::radix(p + 1), T = Ge::T;
+    if constexpr (RI) {
+        float* W = reinterpret_cast<float*>(lds) + wj * S;
+        const float* Rd = reinterpret_cast<const float*>(lds) + rj * S;
+        float nx[Ge::P];
+#pragma unroll
+        for (int i = 0; i < Ge::P / R; ++i) {
+            const int b = wt + T * i, base = (b / Ns) * Ns * R + (b % Ns);
+#pragma unroll
+            for (int r = 0; r < R; ++r) W[Ge::pad(base + r * Ns)] = v[i * R + r].x;
+        }
+        wg_bar();
+#pragma unroll
+        for (int i = 0; i < Ge::P / R2; ++i) {
+            const int b = rt + T * i;
+#pragma unroll
+            for (int r = 0; r < R2; ++r) nx[i * R2 + r] = Rd[Ge::pad(b + r * (N / R2))];
+        }
+        wg_bar();
+#pragma unroll
+        for (int i = 0; i < Ge::P / R; ++i) {
+            const int b = wt + T * i, base = (b / Ns) * Ns * R + (b % Ns);
+#pragma unroll
+            for (int r = 0; r < R; ++r) W[Ge::pad(base + r * Ns)] = v[i * R + r].y;
+        }
+        wg_bar();
+#pragma unroll
+        for (int i = 0; i < Ge::P / R2; ++i) {
+            const int b = rt + T * i;
+#pragma unroll
+            for (int r = 0; r < R2; ++r) v[i * R2 + r] = make_float2(nx[i * R2 + r], Rd[Ge::pad(b + r * (N / R2))]);
+        }
+        wg_bar();
+    } else {
+        float2* W = reinterpret_cast<float2*>(lds) + wj * S;
+        const float2* Rd = reinterpret_cast<const float2*>(lds) + rj * S;
+#pragma unroll
+        for (int i = 0; i < Ge::P / R; ++i) {
+            const int b = wt + T * i, base = (b / Ns) * Ns * R + (b % Ns);
+#pragma unroll
+            for (int r = 0; r < R; ++r) W[Ge::pad(base + r * Ns)] = v[i * R + r];
+        }
+        wg_bar();
+#pragma unroll
+        for (int i = 0; i < Ge::P / R2; ++i) {
+            const int b = rt + T * i;
+#pragma unroll
+            for (int r = 0; r < R2; ++r) v[i * R2 + r] = Rd[Ge::pad(b + r * (N / R2))];
+        }
+        wg_bar();
+    }
+}
+
+// Pass chain; with REMAP the last pass runs in mapping (j2, t2), all others in (j1, t1).
+template <int N, bool FWD, int p, int S, bool RI, bool REMAP>
+struct FsChain {
+    __device__ __forceinline__ static void run(float2* v, void* lds, const TwTab<N>& tw, int j1, int t1, int j2,
+                                               int t2) {
+        constexpr int NP = Geo<N>::NPASS;
+        constexpr bool last = p == NP - 1;
+        pass_compute<N, FWD, p, false>(v, (REMAP && last) ? t2 : t1, tw);
+        if constexpr (!last) {
+            if constexpr (REMAP && p + 1 == NP - 1) fs_exchange<N, p, S, RI>(v, lds, j1, t1, j2, t2);
+            else fs_exchange<N, p, S, RI>(v, lds, j1, t1, j1, t1);
+            FsChain<N, FWD, p + 1, S, RI, REMAP>::run(v, lds, tw, j1, t1, j2, t2);
+        }
+    }
+};
+
+// Columns pass: Y[b][k1][n2] = W_n^(+-n2 k1) * FFT_N1(x[b][.][n2])[k1]
+template <int N1, int G, bool RI, bool FWD>
+__global__ void __launch_bounds__(G * Geo<N1>::T)
+k_fs_cols(const float2* __restrict__ in, float2* __restrict__ out, int N2, int cpb, const float2* gpass,
+          const float2* gtab, const float2* __restrict__ split, int lo_bits) {
+    using Ge = Geo<N1>;
+    using F = FsGeo<N1, G, RI>;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[F::LDS_BYTES];
+    __shared__ float2 ltab[TwLayout<N1>::ENTRIES];
+    // two-level W_n table (lo[2^lo_bits] ++ hi[n >> lo_bits], n <= 2^20) in LDS
+    __shared__ float2 lsplit[2048];
+    stage_twiddles<N1, F::THREADS>(ltab, gpass, gtab);
+    const long long n = (long long)N1 * N2;
+    {
+        const int nsplit = (1 << lo_bits) + (int)(n >> lo_bits);
+        for (int i = threadIdx.x; i < nsplit; i += F::THREADS) lsplit[i] = split[i];
+    }
+    const long long b = blockIdx.x / cpb;
+    const int col = (blockIdx.x % cpb) * G + (int)(threadIdx.x % G), t = threadIdx.x / G;
+    const float2* src = in + b * n + col;
+    float2 v[Ge::P];
+#pragma unroll
+    for (int r = 0; r < Ge::P; ++r) v[r] = ld_nt(src + (long long)(t + r * Ge::T) * N2);
+    __syncthreads();
+    const int j = threadIdx.x % G;
+    FsChain<N1, FWD, 0, F::S, RI, false>::run(v, lds, TwTab<N1>{ltab}, j, t, j, t);
+    const unsigned mask = (1u << lo_bits) - 1u;
+    const float2* hi = lsplit + (1u << lo_bits);
+    float2* dst = out + b * n + col;
+#pragma unroll
+    for (int q = 0; q < Ge::P; ++q) {
+        const int k1 = out_pos<N1>(t, q);
+        const unsigned k = (unsigned)col * (unsigned)k1;   // < n <= 2^20
+        float2 w = cmul(lsplit[k & mask], hi[k >> lo_bits]);
+        if (!FWD) w = cconj(w);
+        st_nt(cmul(v[q], w), dst + (long long)k1 * N2);
+    }
+}
+
+// Rows pass: X[b][k1 + N1 k2] = scale * FFT_N2(Y[b][k1][.])[k2]
+template <int N2, int G, bool RI, bool FWD>
+__global__ void __launch_bounds__(G * Geo<N2>::T)
+k_fs_rows(const float2* __restrict__ in, float2* __restrict__ out, int N1, int rpb, const float2* gpass,
+          const float2* gtab, float scale) {
+    using Ge = Geo<N2>;
+    using F = FsGeo<N2, G, RI>;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[F::LDS_BYTES];
+    __shared__ float2 ltab[TwLayout<N2>::ENTRIES];
+    stage_twiddles<N2, F::THREADS>(ltab, gpass, gtab);
+    const long long n = (long long)N1 * N2;
+    const long long b = blockIdx.x / rpb;
+    const int r0 = (blockIdx.x % rpb) * G;
+    const int j1 = threadIdx.x / Ge::T, t1 = threadIdx.x % Ge::T;   // lanes along a row
+    const int j2 = threadIdx.x % G, t2 = threadIdx.x / G;           // lanes across rows
+    const float2* src = in + b * n + (long long)(r0 + j1) * N2 + t1;
+    float2 v[Ge::P];
+#pragma unroll
+    for (int r = 0; r < Ge::P; ++r) v[r] = ld_nt(src + r * Ge::T);
+    __syncthreads();
+    FsChain<N2, FWD, 0, F::S, RI, true>::run(v, lds, TwTab<N2>{ltab}, j1, t1, j2, t2);
+    float2* dst = out + b * n + r0 + j2;
+#pragma unroll
+    for (int q = 0; q < Ge::P; ++q) {
+        const int k2 = out_pos<N2>(t2, q);
+        st_nt(FWD ? v[q] : cscale(v[q], scale), dst + (long long)k2 * N1);
+    }
+}
+
+namespace {
+// variant: 0 = RI exchange, G 16; 1 = float2 exchange, G 16 (default: fastest measured,
+// profiles/r01_kbench_fourstep.jsonl); 2 = float2, G 8; 3 = RI, G 8
+template <int N, int G, bool RI, bool FWD>
+hipError_t fs_cols_g(const float2* in, float2* out, int N2, long long batch, const float2* split, int lo_bits,
+                     hipStream_t s) {
+    const float2* tab = twiddle_table(N);
+    const float2* pas = pass_twiddles(N);
+    if (!tab || !pas) return hipErrorOutOfMemory;
+    const int cpb = N2 / G;
+    const long long blocks = (long long)cpb * batch;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_fs_cols<N, G, RI, FWD>), dim3((unsigned)blocks), dim3(FsGeo<N, G, RI>::THREADS), 0, s, in,
+                       out, N2, cpb, pas, tab, split, lo_bits);
+    return hipGetLastError();
+}
+
+template <int N, int G, bool RI, bool FWD>
+hipError_t fs_rows_g(const float2* in, float2* out, int N1, long long batch, float scale, hipStream_t s) {
+    const float2* tab = twiddle_table(N);
+    const float2* pas = pass_twiddles(N);
+    if (!tab || !pas) return hipErrorOutOfMemory;
+    const int rpb = N1 / G;
+    const long long blocks = (long long)rpb * batch;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_fs_rows<N, G, RI, FWD>), dim3((unsigned)blocks), dim3(FsGeo<N, G, RI>::THREADS), 0, s, in,
+                       out, N1, rpb, pas, tab, scale);
+    return hipGetLastError();
+}
+
+template <int N, bool FWD>
+hipError_t fs_cols(int var, const float2* in, float2* out, int N2, long long batch, const float2* split, int lo_bits,
+                   hipStream_t s) {
+    switch (var) {
+        case 1: return fs_cols_g<N, 16, false, FWD>(in, out, N2, batch, split, lo_bits, s);
+        case 2: return fs_cols_g<N, 8, false, FWD>(in, out, N2, batch, split, lo_bits, s);
+        case 3: return fs_cols_g<N, 8, true, FWD>(in, out, N2, batch, split, lo_bits, s);
+        default: return fs_cols_g<N, 16, true, FWD>(in, out, N2, batch, split, lo_bits, s);
+    }
+}
+
+template <int N, bool FWD>
+hipError_t fs_rows(int var, const float2* in, float2* out, int N1, long long batch, float scale, hipStream_t s) {
+    switch (var) {
+        case 1: return fs_rows_g<N, 16, false, FWD>(in, out, N1, batch, scale, s);
+        case 2: return fs_rows_g<N, 8, false, FWD>(in, out, N1, batch, scale, s);
+        case 3: return fs_rows_g<N, 8, true, FWD>(in, out, N1, batch, scale, s);
+        default: return fs_rows_g<N, 16, true, FWD>(in, out, N1, batch, scale, s);
+    }
+}
+
+template <bool FWD>
+hipError_t fs_cols_any(int N1, int var, const float2* in, float2* out, int N2, long long batch, const float2* split,
+                       int lo_bits, hipStream_t s) {
+    switch (N1) {
+        case 64: return fs_cols<64, FWD>(var, in, out, N2, batch, split, lo_bits, s);
+        case 128: return fs_cols<128, FWD>(var, in, out, N2, batch, split, lo_bits, s);
+        case 256: return fs_cols<256, FWD>(var, in, out, N2, batch, split, lo_bits, s);
+        case 512: return fs_cols<512, FWD>(var, in, out, N2, batch, split, lo_bits, s);
+        case 1024: return fs_cols<1024, FWD>(var, in, out, N2, batch, split, lo_bits, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <bool FWD>
+hipError_t fs_rows_any(int N2, int var, const float2* in, float2* out, int N1, long long batch, float scale,
+                       hipStream_t s) {
+    switch (N2) {
+        case 64: return fs_rows<64, FWD>(var, in, out, N1, batch, scale, s);
+        case 128: return fs_rows<128, FWD>(var, in, out, N1, batch, scale, s);
+        case 256: return fs_rows<256, FWD>(var, in, out, N1, batch, scale, s);
+        case 512: return fs_rows<512, FWD>(var, in, out, N1, batch, scale, s);
+        case 1024: return fs_rows<1024, FWD>(var, in, out, N1, batch, scale, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+long long env_ll(const char* name, long long dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoll(e) : dflt;
+}
+
+// n = N1*N2, 64 <= N1 <= N2 <= 1024
+hipError_t launch_c2c_twopass(long long n, int lg, int fwd, const float2* in, float2* out, long long batch,
+                              hipStream_t s) {
+    const int N1 = 1 << (lg / 2), N2 = (int)(n / N1);
+    int lo_bits = 0;
+    const float2* split = twiddle_split(n, &lo_bits);
+    if (!split) return hipErrorOutOfMemory;
+    const int var = (int)env_ll("VVHIP_FS_VAR", 1);
+    // chunk of transforms whose intermediate stays in the Infinity Cache
+    const long long chunk_bytes = env_ll("VVHIP_FS_CHUNK_MB", 0) << 20;
+    long long chunk = chunk_bytes > 0 ? chunk_bytes / (8 * n) : batch;
+    if (chunk < 1) chunk = 1;
+    if (chunk > batch) chunk = batch;
+    float2* y = nullptr;
+    hipError_t e = hipMallocAsync((void**)&y, sizeof(float2) * (size_t)n * (size_t)chunk, s);
+    if (e != hipSuccess) return e;
+    const float scale = 1.0f / (float)n;
+    for (long long c = 0; c < batch && e == hipSuccess; c += chunk) {
+        const long long nb = batch - c < chunk ? batch - c : chunk;
+        const float2* src = in + c * n;
+        float2* dst = out + c * n;
+        e = fwd ? fs_cols_any<true>(N1, var, src, y, N2, nb, split, lo_bits, s)
+                : fs_cols_any<false>(N1, var, src, y, N2, nb, split, lo_bits, s);
+        if (e == hipSuccess)
+            e = fwd ? fs_rows_any<true>(N2, var, y, dst, N1, nb, scale, s)
+                    : fs_rows_any<false>(N2, var, y, dst, N1, nb, scale, s);
+    }
+    (void)hipFreeAsync(y, s);
+    return e;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Five-pass four-step (n > 2^20)
+// ---------------------------------------------------------------------------
 
 constexpr int TT = 64;   // transpose tile
 
@@ -78,6 +367,7 @@ hipError_t launch_c2c_large(long long n, int fwd, const float2* in, float2* out,
     if (batch <= 0) return hipSuccess;
     int lg = 0;
     while ((1LL << lg) < n) ++lg;
+    if (lg <= 20 && env_ll("VVHIP_FS_OLD", 0) == 0) return launch_c2c_twopass(n, lg, fwd, in, out, batch, s);
     const long long N1 = 1LL << (lg / 2), N2 = n / N1;   // N1 <= N2 <= 4096
     int lo_bits = 0;
     const float2* tab = twiddle_split(n, &lo_bits);

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace vvh;
@@ -85,6 +86,67 @@ struct Scratch {
     }
 };
 
+// Host-buffer pipeline (the reference API's host pointers).  A large call is
+// cut into chunks that alternate between two lanes; each lane is a host thread
+// with its own stream and device buffers and runs host->device copy, kernels
+// and device->host copy for its chunks.  PCIe is full duplex, so one lane's
+// device->host copy overlaps the other lane's host->device copy; a pageable
+// hipMemcpy blocks its calling thread, hence two threads rather than two
+// streams issued from one.
+struct HostLane {
+    hipStream_t s = nullptr;
+    DevBuf a, b;
+    hipError_t init() { return s ? hipSuccess : hipStreamCreateWithFlags(&s, hipStreamNonBlocking); }
+    void release() {
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+        s = nullptr;
+        a.release();
+        b.release();
+    }
+};
+
+size_t host_chunk_bytes() {
+    const char* e = getenv("VVHIP_HOST_CHUNK_MB");
+    const long long mb = (e && *e) ? atoll(e) : 16;
+    return (size_t)(mb > 0 ? mb : 16) << 20;
+}
+
+// fn(chunk, lane) enqueues one chunk on lane.s and returns a status; the lane
+// synchronises its stream after every chunk, so the caller's host buffers are
+// complete when this returns.
+template <class F>
+int run_lanes(HostLane* lanes, long long nchunks, F&& fn) {
+    for (int l = 0; l < 2; ++l) HIPCHK(lanes[l].init(), ST_INTERNAL);
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev), ST_INTERNAL);
+    int st1 = ST_OK;
+    std::string err1;
+    std::thread worker([&] {
+        if (hipSetDevice(dev) != hipSuccess) {
+            st1 = ST_INTERNAL;
+            err1 = "host pipeline: hipSetDevice";
+            return;
+        }
+        for (long long c = 1; c < nchunks && st1 == ST_OK; c += 2) {
+            st1 = fn(c, lanes[1]);
+            if (st1 == ST_OK && hipStreamSynchronize(lanes[1].s) != hipSuccess) st1 = ST_INTERNAL;
+        }
+        if (st1 != ST_OK) err1 = g_err.empty() ? "host pipeline lane 1" : g_err;
+    });
+    int st0 = ST_OK;
+    for (long long c = 0; c < nchunks && st0 == ST_OK; c += 2) {
+        st0 = fn(c, lanes[0]);
+        if (st0 == ST_OK) HIPCHK(hipStreamSynchronize(lanes[0].s), ST_INTERNAL);
+    }
+    worker.join();
+    if (st0 != ST_OK) return st0;
+    if (st1 != ST_OK) return fail(st1, err1.c_str());
+    return ST_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -97,6 +159,7 @@ struct vvhip_fft {
     size_t batch = 1;
     hipStream_t stream = nullptr;
     DevBuf din, dout;
+    HostLane lanes[2];
 };
 
 static size_t fft_in_elems_bytes(const vvhip_fft* p) {
@@ -254,6 +317,25 @@ int vvhip_fft_exec_device(vvhip_fft* p, const void* d_in, void* d_out, size_t ba
 
 int vvhip_fft_exec_host(vvhip_fft* p, const void* in, void* out) {
     if (!p || !in || !out) return ST_NULL;
+    const size_t ie = fft_in_elems_bytes(p), oe = fft_out_elems_bytes(p);
+    const size_t chunk_b = host_chunk_bytes();
+    if ((ie + oe) * p->batch >= 2 * chunk_b && p->batch >= 2) {
+        // pipelined: chunks of whole transforms on two lanes
+        size_t per = chunk_b / (ie > oe ? ie : oe);
+        if (per < 1) per = 1;
+        const long long nchunks = (long long)((p->batch + per - 1) / per);
+        return run_lanes(p->lanes, nchunks, [&](long long c, HostLane& L) -> int {
+            const size_t b0 = (size_t)c * per, nb = (p->batch - b0) < per ? (p->batch - b0) : per;
+            HIPCHK(L.a.ensure(ie * per), ST_INTERNAL);
+            HIPCHK(L.b.ensure(oe * per), ST_INTERNAL);
+            HIPCHK(hipMemcpyAsync(L.a.p, (const char*)in + ie * b0, ie * nb, hipMemcpyHostToDevice, L.s),
+                   ST_INTERNAL);
+            int st = fft_run(p->n, p->type, p->dir, L.a.p, L.b.p, nb, L.s);
+            if (st != ST_OK) return st;
+            HIPCHK(hipMemcpyAsync((char*)out + oe * b0, L.b.p, oe * nb, hipMemcpyDeviceToHost, L.s), ST_INTERNAL);
+            return ST_OK;
+        });
+    }
     if (!p->stream) HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking), ST_INTERNAL);
     const size_t ib = fft_in_elems_bytes(p) * p->batch, ob = fft_out_elems_bytes(p) * p->batch;
     HIPCHK(p->din.ensure(ib), ST_INTERNAL);
@@ -274,6 +356,8 @@ void vvhip_fft_plan_destroy(vvhip_fft* p) {
     }
     p->din.release();
     p->dout.release();
+    p->lanes[0].release();
+    p->lanes[1].release();
     delete p;
 }
 
@@ -288,6 +372,7 @@ struct vvhip_stft {
     std::vector<float> h_win;
     hipStream_t stream = nullptr;
     DevBuf b0, b1, b2;
+    HostLane lanes[2];
 };
 
 // out_kind: 0 magnitude rows [frame][nfft], 1 complex rows [frame][nfft],
@@ -366,6 +451,8 @@ void vvhip_stft_destroy(vvhip_stft* h) {
     h->b0.release();
     h->b1.release();
     h->b2.release();
+    h->lanes[0].release();
+    h->lanes[1].release();
     delete h;
 }
 
@@ -388,6 +475,29 @@ int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, fl
     if (int st = stft_stream(h)) return st;
     const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
     const size_t ob = sizeof(float) * frames * h->nfft;
+    const size_t row = sizeof(float) * h->nfft;
+    size_t per = (host_chunk_bytes() / row) & ~(size_t)1;   // even: frames pair up as in one launch
+    if (per < 2) per = 2;
+    if (n >= h->nfft && frames >= 2 * per && stft_fused_supported((long long)h->nfft)) {
+        // pipelined over frame chunks; chunk c reads its own span (with the nfft-hop overlap)
+        const long long nchunks = (long long)((frames + per - 1) / per);
+        return run_lanes(h->lanes, nchunks, [&](long long c, HostLane& L) -> int {
+            const size_t f0 = (size_t)c * per, fc = (frames - f0) < per ? (frames - f0) : per;
+            const size_t start = f0 * h->hop;
+            const size_t want = (fc - 1) * h->hop + h->nfft;
+            const size_t len = (n - start) < want ? (n - start) : want;
+            HIPCHK(L.a.ensure(sizeof(float) * ((per - 1) * h->hop + h->nfft)), ST_INTERNAL);
+            HIPCHK(L.b.ensure(row * per), ST_INTERNAL);
+            HIPCHK(hipMemcpyAsync(L.a.p, signal + start, sizeof(float) * len, hipMemcpyHostToDevice, L.s),
+                   ST_INTERNAL);
+            HIPCHK(launch_stft((long long)h->nfft, (long long)h->hop, 0, (const float*)L.a.p, (long long)len, 1, 0,
+                               (long long)fc, h->d_win, L.b.p, (long long)(fc * h->nfft), L.s),
+                   ST_INTERNAL);
+            HIPCHK(hipMemcpyAsync(out_mag + f0 * h->nfft, L.b.p, row * fc, hipMemcpyDeviceToHost, L.s),
+                   ST_INTERNAL);
+            return ST_OK;
+        });
+    }
     HIPCHK(h->b0.ensure(sizeof(float) * (n ? n : 1)), ST_INTERNAL);
     HIPCHK(h->b1.ensure(ob), ST_INTERNAL);
     if (n) HIPCHK(hipMemcpyAsync(h->b0.p, signal, sizeof(float) * n, hipMemcpyHostToDevice, h->stream), ST_INTERNAL);
