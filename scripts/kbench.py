@@ -230,6 +230,7 @@ CASES = {
     "stft60": lambda: case_stft(1, 60),
     "stftc": lambda: case_stft(8, 600, complex_out=True),
     "fir": lambda: case_fir(8, 1 << 24),
+    "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "dct1024": lambda: case_dct(1024, 131072),
 }

@@ -247,7 +247,7 @@ template <int N>
 struct TwTab {
     const float2* tab;   // LDS: pass-major table, or lo[64] ++ hi[N/64] when SPLIT
     template <int p>
-    __device__ __forceinline__ float2 at(int j, int r) const {
+    __device__ __forceinline__ float2 at(int j, int r, int /*i*/ = 0) const {
         using G = Geo<N>;
         if constexpr (TwLayout<N>::SPLIT) {
             const int k = j * r * (N / (G::ns(p) * G::radix(p)));
@@ -290,8 +290,10 @@ __device__ __forceinline__ void xsync() {
 }
 
 // One Stockham pass p on the registers (twiddle + radix-R DFT), in place.
-template <int N, bool FWD, int p, bool PAIRED>
-__device__ __forceinline__ void pass_compute(float2* v, int t, const TwTab<N>& tw) {
+// TW: twiddle source with `at<p>(j, r, i)` (j = butterfly index mod Ns, i = the
+// thread's butterfly slot) -- TwTab<N>, or one holding some passes in registers.
+template <int N, bool FWD, int p, bool PAIRED, class TW>
+__device__ __forceinline__ void pass_compute(float2* v, int t, const TW& tw) {
     using G = Geo<N>;
     constexpr int R = G::radix(p);
     constexpr int Ns = G::ns(p);
@@ -301,7 +303,7 @@ __device__ __forceinline__ void pass_compute(float2* v, int t, const TwTab<N>& t
             const int j = bfly<N, p, PAIRED>(t, i) % Ns;
 #pragma unroll
             for (int r = 1; r < R; ++r) {
-                const float2 w = tw.template at<p>(j, r);
+                const float2 w = tw.template at<p>(j, r, i);
                 v[i * R + r] = cmul(v[i * R + r], FWD ? w : cconj(w));
             }
         }
@@ -385,7 +387,8 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
 
 template <int N, bool FWD, int p, bool PAIRED, bool RI = false>
 struct PassChain {
-    __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TwTab<N>& tw) {
+    template <class TW>
+    __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TW& tw) {
         pass_compute<N, FWD, p, PAIRED>(v, t, tw);
         if constexpr (p + 1 < Geo<N>::NPASS) {
             if constexpr (RI) pass_exchange_ri<N, p, PAIRED>(v, t, reinterpret_cast<float*>(lds));
@@ -398,8 +401,8 @@ struct PassChain {
 // Full transform.  On entry v[r] = x[t + r*T] (r < P).  On exit register q
 // holds X[out_pos<N, PAIRED>(t, q)].  RI: `lds` needs only Geo<N>::LDS floats
 // (pass_exchange_ri) instead of Geo<N>::LDS float2.
-template <int N, bool FWD, bool PAIRED = false, bool RI = false>
-__device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TwTab<N>& tw) {
+template <int N, bool FWD, bool PAIRED = false, bool RI = false, class TW = TwTab<N>>
+__device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TW& tw) {
     static_assert(!PAIRED || Geo<N>::CAN_PAIR, "mirror pairing needs >= 2 last-pass butterflies per thread");
     PassChain<N, FWD, 0, PAIRED, RI>::run(v, t, lds, tw);
 }

@@ -33,6 +33,7 @@
 #include "vvhip_internal.hpp"
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace vvh {
 
@@ -189,6 +190,137 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
     }
 }
 
+// ------------------------------------------------------------------------
+// k_fir_bulk<N, LQ>: the bulk pairs at three workgroups per CU (12 waves)
+// instead of two.  LDS per workgroup of four transforms: the FFT exchange
+// through the half-size real/imaginary buffer (pass_exchange_ri, conflict-free
+// for N = 1024), H for bins 0..N/2 only (h is real, so H[N-k] = conj H[k]),
+// the last pass' twiddles in registers (a thread's last-pass butterflies are
+// the same for every pair: j = t + T*i) and only the earlier passes' table in
+// LDS -- 52 KB instead of 80 KB.
+// LQ (le == N/4, e.g. taps <= N/4 + 1): the outputs below le are exactly the
+// registers q with q % RL == 0, so those stores are dropped at compile time
+// (no sink stores: 3/4 of the store instructions of the general variant).
+// ------------------------------------------------------------------------
+template <int N>
+struct TwLastReg {
+    using G = Geo<N>;
+    static constexpr int LAST = G::NPASS - 1, RL = G::RL, NS = G::ns(LAST);
+    static_assert(G::T * (G::P / RL) == NS && G::T == N / 16, "j = t + T*i < NS, and W_N^T = W_16");
+    const float2* tab;   // LDS: pass-major entries of passes < LAST
+    float2 w[RL - 1];    // W_N^{r t}, r = 1..RL-1
+    // last pass: j = t + T*i (< NS), twiddle W_N^{j r} = W_N^{t r} * W_N^{T i r}; with
+    // T = N/16 the second factor is W_16^{i r}, an exact in-register rotation
+    template <int p>
+    __device__ __forceinline__ float2 at(int j, int r, int i) const {
+        if constexpr (p == LAST) return twc<16, true>(w[r - 1], i * r);
+        else return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
+    }
+    __device__ __forceinline__ void load(const float2* gpass, int t) {
+#pragma unroll
+        for (int r = 1; r < RL; ++r) w[r - 1] = gpass[G::tw_off(LAST) + (r - 1) * NS + t];
+        // consume the loads here, so that the compiler's vmcnt wait for them
+        // sits before the streaming loop (it does not count the loop's asm ops)
+        opaque();
+    }
+    // Called before each transform: the derived twiddles then cannot be hoisted
+    // out of the pair loop (LICM would keep all (RL-1)*P/RL of them, and their
+    // conjugates, live across it -- 48 VGPRs and scratch spills).
+    __device__ __forceinline__ void opaque() {
+#pragma unroll
+        for (int r = 0; r < RL - 1; ++r) asm volatile("" : "+v"(w[r].x), "+v"(w[r].y));
+    }
+};
+
+template <int N, bool LQ>
+__global__ void __launch_bounds__(256, 3)   // 3 waves per SIMD: the LDS allows 3 workgroups per CU
+k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long nch, long long x_stride,
+           long long y_stride, long long cnt, long long q0, const float2* gpass, float* sink) {
+    using G = Geo<N>;
+    static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
+    constexpr int F = 4, RL = G::RL;
+    constexpr int SPAN = N + (3 * N) / 4;
+    constexpr int NST = LQ ? 2 * (G::P - G::P / RL) : 2 * G::P;   // stores per pair
+    constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
+    __shared__ float xch[F * G::LDS];
+    __shared__ float2 ltab[TWL];
+    __shared__ float2 lH[N / 2 + 1];
+    __shared__ float span_all[F * SPAN];
+    for (int i = threadIdx.x; i < G::tw_off(G::NPASS - 1); i += 256) ltab[i] = gpass[i];
+    for (int i = threadIdx.x; i <= N / 2; i += 256) lH[i] = Hg[i];
+    const int lt = threadIdx.x, slot = lt >> 6, t = lt & 63;
+    TwLastReg<N> tw;
+    tw.tab = ltab;
+    tw.load(gpass, t);
+    __syncthreads();
+    float2* my = reinterpret_cast<float2*>(xch + slot * G::LDS);
+    float* span = span_all + slot * SPAN;
+    const long long lout = N - le;
+    long long p, p_end, p_step;
+    xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+    p = uni<64>(p);
+    p_end = uni<64>(p_end);
+    p_step = uni<64>(p_step);
+    if (p >= p_end) return;
+    auto locate = [&](long long it, long long* cc, long long* jj) {
+        *cc = it / cnt;
+        *jj = 2 * (q0 + (it - *cc * cnt));
+    };
+    long long c, j;
+    locate(p, &c, &j);
+    float* snk = sink + ((((long long)blockIdx.x * F + slot) * 64) % SINK_FLOATS) + t;
+    auto issue_span = [&](long long cc, long long jj) {
+        const float* s0 = x + cc * x_stride + jj * lout - le;
+        const int len = (int)(N + lout);
+#pragma unroll
+        for (int u = 0; u < SPAN / 256; ++u) {
+            const int e = u * 256 + t * 4;
+            glds16(s0 + (e < len ? e : 0), span + u * 256);
+        }
+    };
+    issue_span(c, j);
+    vm_wait<0>();
+    for (; p < p_end; p += p_step) {
+        const bool more = p + p_step < p_end;
+        long long cn = c, jn = j;
+        if (more) locate(p + p_step, &cn, &jn);
+        vm_wait<NST>();   // this pair's span; the previous pair's stores may still fly
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(span[t + r * 64], span[lout + t + r * 64]);
+        lgkm_wait0();
+        if (more) issue_span(cn, jn);
+        tw.opaque();
+        fft_regs<N, true, false, true>(v, t, my, tw);
+        float2 u[G::P];
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int m = q / RL + G::NPT * (q % RL);   // out_pos<N>(t, q) = t + 64*m
+            if (m < G::P / 2) u[m] = cmul(v[q], lH[t + 64 * m]);
+            else u[m] = cmul(v[q], cconj(lH[N - t - 64 * m]));
+        }
+        tw.opaque();
+        fft_regs<N, false, false, true>(u, t, my, tw);
+        float* ya = y + c * y_stride + j * lout - le;   // + e: block j output (e >= le)
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const long long e = out_pos<N>(t, q);
+            if constexpr (LQ) {
+                if (q % RL != 0) {
+                    st4_counted(ya + e, u[q].x);
+                    st4_counted(ya + e + lout, u[q].y);
+                }
+            } else {
+                const bool ok = e >= le;
+                st4_counted(ok ? ya + e : snk, u[q].x);
+                st4_counted(ok ? ya + e + lout : snk, u[q].y);
+            }
+        }
+        c = cn;
+        j = jn;
+    }
+}
+
 // Effective history of the block geometry (see the header comment).
 long long fir_effective_history(long long nfft, long long taps) {
     long long le = taps - 1;
@@ -229,8 +361,19 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     // below (2q+2)*lout without bounds checks: verify the range on the host
     if (ql > qf && (2 * qf * lout < le || 2 * ql * lout > n || N + lout > N + (3 * N) / 4))
         return hipErrorInvalidValue;
-    static int cap_b = 0, cap_e = 0;
-    if (ql > qf) {
+    static int cap_b = 0, cap_e = 0, cap_v2 = 0;
+    const char* eo = getenv("VVHIP_FIR_OLD");   // A/B switch (scripts/kbench.py), read per call
+    const bool old = eo && *eo == '1';
+    // le == N/4 holds for every filter fir_block gives N = 1024 (taps <= 257)
+    if (ql > qf && le == N / 4 && !old) {
+        if constexpr (FIR_BULK<N>) {
+            if (!cap_v2) cap_v2 = persistent_grid((const void*)k_fir_bulk<N, true>, 256, 0, 1LL << 40);
+            const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
+            const int grid = (int)(need < cap_v2 ? need : cap_v2);
+            hipLaunchKernelGGL((k_fir_bulk<N, true>), dim3(grid), dim3(256), 0, s, le, H, x, y, nch, x_stride,
+                               y_stride, cnt, qf, pN, sink);
+        }
+    } else if (ql > qf) {
         if constexpr (FIR_BULK<N>) {
             if (!cap_b) cap_b = persistent_grid((const void*)k_fir_pair<N, true>, WG, 0, 1LL << 40);
             const long long cnt = ql - qf, need = (nch * cnt + F - 1) / F;
