@@ -82,6 +82,28 @@ def case_fir(nch, n, taps=257):
     return (lambda: p(x, out=y)), 2 * nch * n * 4, (x, y, p)
 
 
+def case_mel(kind, frames=3599936):
+    """log-mel (kind 0) / MFCC (kind 1) from power rows [frames][513] (40 mels, 13 coeffs)"""
+    if "pw513" not in _SHARED:
+        _SHARED["pw513"] = torch.rand(frames, 513, device="cuda") ** 2
+    pw = _SHARED["pw513"]
+    mf = vv.Mfcc(1024, 40, 13, 48000.0, 20.0, 20000.0, lifter=22.0)
+    if kind == 0:
+        return (lambda: mf.log_mel(pw)), frames * (513 + 40) * 4, (pw, mf)
+    return (lambda: mf(pw)), frames * (513 + 13) * 4, (pw, mf)
+
+
+def case_ola(seconds=600):
+    """ISTFT overlap-add of one channel's complex frames (vv_dsp_stft_reconstruct, batched)"""
+    st = vv.Stft(1024, 256)
+    n = seconds * 48000
+    fr = st.frames(n)
+    spec = torch.complex(torch.rand(fr, 1024, device="cuda"), torch.rand(fr, 1024, device="cuda"))
+    acc = torch.zeros(n + 1024, device="cuda")
+    norm = torch.zeros(n + 1024, device="cuda")
+    return (lambda: st.reconstruct(spec, acc, norm)), fr * 8192 + 2 * 2 * (n + 1024) * 4, (st, spec, acc, norm)
+
+
 def case_hilbert(n, batch):
     x = torch.rand(batch, n, device="cuda") * 2 - 1
     vv.hilbert(x)   # plan/tables
@@ -208,6 +230,9 @@ CASES = {
     "wrpat": lambda: case_wr(1, 0), "wrpatnt": lambda: case_wr(1, 1),
     "wr8nt": lambda: case_wr(2, 1), "wr16": lambda: case_wr(3, 0), "wr16nt": lambda: case_wr(3, 1),
     "copy1G": lambda: case_copy(1 << 29),
+    # the config-2 byte count (512 MiB read + 512 MiB written) as a pure 1:1 stream
+    **{f"rwc1G_u{u}b{b}": (lambda u=u, b=b: case_rwc(1, u, 1, 1, b, in_bytes=1 << 29))
+       for u in (1, 2, 4) for b in (1024, 2048, 4096, 8192, 16384)},
     "c2c1024": lambda: case_c2c(1024, 65536),
     # large power-of-two (four-step) and Bluestein lengths; VVHIP_FS_* select the variant
     "c2c2p20": lambda: case_c2c(1 << 20, 64),
@@ -232,6 +257,10 @@ CASES = {
     "fir": lambda: case_fir(8, 1 << 24),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "hilbert1024": lambda: case_hilbert(1024, 65536),
+    "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),
+    "logmelold": with_env(lambda: case_mel(0), "VVHIP_MEL_OLD", "1"),
+    "mfccold": with_env(lambda: case_mel(1), "VVHIP_MEL_OLD", "1"),
+    "ola": lambda: case_ola(),
     "dct1024": lambda: case_dct(1024, 131072),
 }
 # A/B switches for launcher experiments: CASES["stftX"] = with_env(CASES["stft"], "VVHIP_EXP_...", "1")

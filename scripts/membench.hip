@@ -251,6 +251,7 @@ extern "C" int membench_rwc(const float* in, float* out, long long items, int w,
     }
     RWC(4, 1, 1, 1) RWC(4, 2, 1, 1) RWC(4, 4, 1, 1) RWC(4, 1, 0, 0) RWC(4, 2, 0, 0) RWC(4, 4, 0, 0)
     RWC(4, 2, 0, 1) RWC(4, 2, 1, 0) RWC(1, 2, 1, 1) RWC(1, 2, 0, 0) RWC(4, 8, 1, 1)
+    RWC(1, 1, 1, 1) RWC(1, 4, 1, 1)
 #undef RWC
     return -1;
 }

@@ -871,6 +871,9 @@ struct vvhip_mel {
     float eps = 0.0f;
     float* W = nullptr;     // non-zero weight ranges of every filter, packed
     int* meta = nullptr;    // per filter: lo, len, offset into W
+    int* chunks = nullptr;  // balanced chunk schedule of the filters (mel_chunk_schedule)
+    int* cbeg = nullptr;    // first chunk of each filter, [n_mels + 1]
+    int nc = 0;
     float* D = nullptr;     // DCT-II table [n_coeffs][n_mels]
     float* lift = nullptr;  // lifter factors [n_coeffs]
     hipStream_t stream = nullptr;
@@ -887,6 +890,8 @@ void vvhip_mel_destroy(vvhip_mel* m) {
     }
     if (m->W) (void)hipFree(m->W);
     if (m->meta) (void)hipFree(m->meta);
+    if (m->chunks) (void)hipFree(m->chunks);
+    if (m->cbeg) (void)hipFree(m->cbeg);
     if (m->D) (void)hipFree(m->D);
     if (m->lift) (void)hipFree(m->lift);
     m->bin.release();
@@ -924,6 +929,9 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
         }
     }
     m->nnz = (int)w.size();
+    std::vector<int> chunks, cbeg;
+    mel_chunk_schedule(meta.data(), (int)n_mels, &chunks, &cbeg);
+    m->nc = (int)(chunks.size() / 3);
     // DCT-II rows cos(pi (j + 1/2) i / M) (dct.c:21-30), and the lifter of mel.c:300-302
     std::vector<float> D(n_coeffs * n_mels), L(n_coeffs, 1.0f);
     for (size_t i = 0; i < n_coeffs; ++i)
@@ -934,6 +942,11 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
             L[i] = 1.0f + (lifter / 2.0f) * sinf((float)M_PI * (float)i / lifter);
     bool ok = hipMalloc(&m->meta, sizeof(int) * meta.size()) == hipSuccess &&
               hipMemcpy(m->meta, meta.data(), sizeof(int) * meta.size(), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMalloc(&m->chunks, sizeof(int) * (chunks.size() + 1)) == hipSuccess &&
+              (chunks.empty() ||
+               hipMemcpy(m->chunks, chunks.data(), sizeof(int) * chunks.size(), hipMemcpyHostToDevice) == hipSuccess) &&
+              hipMalloc(&m->cbeg, sizeof(int) * cbeg.size()) == hipSuccess &&
+              hipMemcpy(m->cbeg, cbeg.data(), sizeof(int) * cbeg.size(), hipMemcpyHostToDevice) == hipSuccess &&
               hipMalloc(&m->W, sizeof(float) * (w.size() + 1)) == hipSuccess &&
               (w.empty() || hipMemcpy(m->W, w.data(), sizeof(float) * w.size(), hipMemcpyHostToDevice) == hipSuccess) &&
               hipMalloc(&m->D, sizeof(float) * (D.size() + 1)) == hipSuccess &&
@@ -956,9 +969,15 @@ int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_ou
     if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
     if ((kind != 2 && m->nbins == 0) || (kind != 0 && m->n_coeffs == 0)) return fail(ST_RANGE, "mel plan lacks tables");
     if (frames == 0) return ST_OK;
-    HIPCHK(launch_mel(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->meta, m->nnz, m->D,
-                      m->lift, m->eps, d_out, (hipStream_t)stream),
-           ST_INTERNAL);
+    const char* eo = getenv("VVHIP_MEL_OLD");   // A/B switch (scripts/kbench.py): one wave per frame
+    if (eo && *eo == '1')
+        HIPCHK(launch_mel(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->meta, m->nnz,
+                          m->D, m->lift, m->eps, d_out, (hipStream_t)stream),
+               ST_INTERNAL);
+    else
+        HIPCHK(launch_mel_grp(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->nnz,
+                              m->chunks, m->nc, m->cbeg, m->D, m->lift, m->eps, d_out, (hipStream_t)stream),
+               ST_INTERNAL);
     return ST_OK;
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 namespace vvh {
 
@@ -36,6 +37,12 @@ hipError_t launch_promote_real(const float* in, float2* out, long long count, hi
 hipError_t launch_mel(int mode, const float* in, long long frames, int nbins, int n_mels, int n_coeffs,
                       const float* W, const int* meta, int nnz, const float* D, const float* lift, float eps,
                       float* out, hipStream_t s);
+hipError_t launch_mel_grp(int mode, const float* in, long long frames, int nbins, int n_mels, int n_coeffs,
+                          const float* W, int nnz, const int* chunks, int nc, const int* cbeg, const float* D,
+                          const float* lift, float eps, float* out, hipStream_t s);
+// host: chunk schedule of the filters' non-zero ranges {lo, len, off}[n_mels] for
+// launch_mel_grp (chunks {lo, len, off}, cbeg[n_mels+1]); returns the chunk length
+int mel_chunk_schedule(const int* meta, int n_mels, std::vector<int>* chunks, std::vector<int>* cbeg);
 
 // Write sink (SINK_FLOATS floats): destination of lanes that must issue a store
 // with nothing to write, in kernels that hand-count their memory operations.
