@@ -261,6 +261,7 @@ CASES = {
     "logmelold": with_env(lambda: case_mel(0), "VVHIP_MEL_OLD", "1"),
     "mfccold": with_env(lambda: case_mel(1), "VVHIP_MEL_OLD", "1"),
     "ola": lambda: case_ola(),
+    "olaold": with_env(lambda: case_ola(), "VVHIP_ISTFT_OLD", "1"),
     "dct1024": lambda: case_dct(1024, 131072),
 }
 # A/B switches for launcher experiments: CASES["stftX"] = with_env(CASES["stft"], "VVHIP_EXP_...", "1")

@@ -258,6 +258,43 @@ struct TwTab {
     }
 };
 
+// Twiddle source for one-wave transforms (T = N/16) that streams many
+// transforms through one kernel: the passes before the last read the LDS
+// pass-major table (only tw_off(LAST) entries are staged); the last pass'
+// twiddles are derived in registers -- a thread's last-pass butterflies are the
+// same for every transform (j = t + T*i), W_N^{j r} = W_N^{t r} * W_16^{i r},
+// and W_16^{i r} is an exact in-register rotation.  Saves the largest part of
+// the table in LDS (6 KB of 8 KB for N = 1024).
+template <int N>
+struct TwLastReg {
+    using G = Geo<N>;
+    static constexpr int LAST = G::NPASS - 1, RL = G::RL, NS = G::ns(LAST);
+    static_assert(G::T * (G::P / RL) == NS && G::T == N / 16, "j = t + T*i < NS, and W_N^T = W_16");
+    const float2* tab;   // LDS: pass-major entries of passes < LAST
+    float2 w[RL - 1];    // W_N^{r t}, r = 1..RL-1
+    // last pass: j = t + T*i (< NS), twiddle W_N^{j r} = W_N^{t r} * W_N^{T i r}; with
+    // T = N/16 the second factor is W_16^{i r}, an exact in-register rotation
+    template <int p>
+    __device__ __forceinline__ float2 at(int j, int r, int i) const {
+        if constexpr (p == LAST) return twc<16, true>(w[r - 1], i * r);
+        else return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
+    }
+    __device__ __forceinline__ void load(const float2* gpass, int t) {
+#pragma unroll
+        for (int r = 1; r < RL; ++r) w[r - 1] = gpass[G::tw_off(LAST) + (r - 1) * NS + t];
+        // consume the loads here, so that the compiler's vmcnt wait for them
+        // sits before the streaming loop (it does not count the loop's asm ops)
+        opaque();
+    }
+    // Called before each transform: the derived twiddles then cannot be hoisted
+    // out of the pair loop (LICM would keep all (RL-1)*P/RL of them, and their
+    // conjugates, live across it -- 48 VGPRs and scratch spills).
+    __device__ __forceinline__ void opaque() {
+#pragma unroll
+        for (int r = 0; r < RL - 1; ++r) asm volatile("" : "+v"(w[r].x), "+v"(w[r].y));
+    }
+};
+
 // Stage the global table into LDS (all NTHREADS threads of the block).
 //   gpass : pass-major table for N (host: pass_twiddles(N)), used when !SPLIT
 //   gtab  : W_N^k, k < N (host: twiddle_table(N)), used when SPLIT

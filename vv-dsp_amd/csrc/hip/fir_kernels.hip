@@ -202,36 +202,6 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
 // registers q with q % RL == 0, so those stores are dropped at compile time
 // (no sink stores: 3/4 of the store instructions of the general variant).
 // ------------------------------------------------------------------------
-template <int N>
-struct TwLastReg {
-    using G = Geo<N>;
-    static constexpr int LAST = G::NPASS - 1, RL = G::RL, NS = G::ns(LAST);
-    static_assert(G::T * (G::P / RL) == NS && G::T == N / 16, "j = t + T*i < NS, and W_N^T = W_16");
-    const float2* tab;   // LDS: pass-major entries of passes < LAST
-    float2 w[RL - 1];    // W_N^{r t}, r = 1..RL-1
-    // last pass: j = t + T*i (< NS), twiddle W_N^{j r} = W_N^{t r} * W_N^{T i r}; with
-    // T = N/16 the second factor is W_16^{i r}, an exact in-register rotation
-    template <int p>
-    __device__ __forceinline__ float2 at(int j, int r, int i) const {
-        if constexpr (p == LAST) return twc<16, true>(w[r - 1], i * r);
-        else return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
-    }
-    __device__ __forceinline__ void load(const float2* gpass, int t) {
-#pragma unroll
-        for (int r = 1; r < RL; ++r) w[r - 1] = gpass[G::tw_off(LAST) + (r - 1) * NS + t];
-        // consume the loads here, so that the compiler's vmcnt wait for them
-        // sits before the streaming loop (it does not count the loop's asm ops)
-        opaque();
-    }
-    // Called before each transform: the derived twiddles then cannot be hoisted
-    // out of the pair loop (LICM would keep all (RL-1)*P/RL of them, and their
-    // conjugates, live across it -- 48 VGPRs and scratch spills).
-    __device__ __forceinline__ void opaque() {
-#pragma unroll
-        for (int r = 0; r < RL - 1; ++r) asm volatile("" : "+v"(w[r].x), "+v"(w[r].y));
-    }
-};
-
 template <int N, bool LQ>
 __global__ void __launch_bounds__(256, 3)   // 3 waves per SIMD: the LDS allows 3 workgroups per CU
 k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long nch, long long x_stride,

@@ -547,6 +547,13 @@ int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t cou
     if (!h || !d_spec || !d_out_add) return ST_NULL;
     if (hop == 0) return ST_SIZE;
     hipStream_t s = (hipStream_t)stream;
+    const char* eo = getenv("VVHIP_ISTFT_OLD");   // A/B switch (scripts/kbench.py): IFFT to scratch + k_ola
+    if (istft_fused_supported((long long)h->nfft, (long long)hop) && !(eo && *eo == '1')) {
+        HIPCHK(launch_istft_fused((long long)h->nfft, (long long)hop, (const float2*)d_spec, (long long)count,
+                                  h->d_win, d_out_add, d_norm_add, s),
+               ST_INTERNAL);
+        return ST_OK;
+    }
     Scratch tf(s);
     HIPCHK(tf.alloc(8 * h->nfft * count), ST_INTERNAL);
     int st = fft_run(h->nfft, 0, -1, d_spec, tf.p, count, s);

@@ -94,6 +94,10 @@ hipError_t launch_power_half(const float2* in, float* out, long long nfft, long 
 // ISTFT accumulate (stft_reconstruct batch): out_add[i] += Re(t[f][i])*w[i] for frames at hop
 hipError_t launch_ola(long long nfft, long long hop, const float2* time_frames, long long count,
                       const float* win, float* out_add, float* norm_add, hipStream_t s);
+// the same from the spectra in one kernel (inverse FFT + window + overlap-add): nfft 1024, hop | nfft, hop >= 256
+bool istft_fused_supported(long long nfft, long long hop);
+hipError_t launch_istft_fused(long long nfft, long long hop, const float2* spec, long long count,
+                              const float* win, float* out_add, float* norm_add, hipStream_t s);
 
 // ---- FIR overlap-save (fir_kernels.hip) ---------------------------------
 bool fir_ols_supported(long long nfft);
