@@ -74,6 +74,16 @@ def case_stft(nch, seconds, complex_out=False, env=None):
     return (lambda: st.spectrogram(sig, out=out, complex_out=complex_out)), byts, (sig, out, st)
 
 
+def case_stft_power(nch, seconds):
+    """power rows [ch][frame][513] (STFT mode 2, the mel kernel's input)"""
+    n = seconds * 48000
+    sig = torch.rand(nch, n, device="cuda") * 2 - 1
+    st = vv.Stft(1024, 256)
+    fr = st.frames(n)
+    out = torch.empty(nch, fr, 513, device="cuda")
+    return (lambda: st.power(sig, out=out)), nch * n * 4 + nch * fr * 513 * 4, (sig, out, st)
+
+
 def case_fir(nch, n, taps=257):
     h = torch.hann_window(taps, periodic=False) * 0.01
     x = torch.rand(nch, n, device="cuda") * 2 - 1
@@ -253,6 +263,8 @@ CASES = {
     "c2r1024": lambda: case_c2r(1024, 131072),
     "stft": lambda: case_stft(32, 600),
     "stft60": lambda: case_stft(1, 60),
+    "stftpow": lambda: case_stft_power(32, 600),
+    "stftpowold": with_env(lambda: case_stft_power(32, 600), "VVHIP_POW_OLD", "1"),
     "stftc": lambda: case_stft(8, 600, complex_out=True),
     "fir": lambda: case_fir(8, 1 << 24),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),

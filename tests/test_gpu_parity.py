@@ -546,6 +546,43 @@ def test_stft_power_to_mfcc_device(vdev, orc):
     assert _normwise(mf.cpu().numpy(), orc.mfcc(lm_ref, 13, 22.0)) <= 1e-4
 
 
+@pytest.mark.parametrize("nfft,hop,n,off", [(1024, 256, 48000 + 333, 0), (1024, 256, 48000 + 333, 1),
+                                            (1024, 256, 48128, 0), (1024, 256, 48000, 1), (1024, 128, 48000, 2),
+                                            (1024, 512, 20000, 3), (1024, 100, 9999, 0), (1024, 768, 30001, 0),
+                                            (1024, 256, 1024 + 256, 0), (1024, 256, 700, 1),
+                                            (256, 64, 10000, 1), (2048, 512, 30000, 0), (4096, 1024, 40000, 2)])
+def test_stft_power_rows(vdev, orc, nfft, hop, n, off):
+    """Power spectrogram (STFT mode 2, bins 0..nfft/2) per bin against NumPy f64
+    on the same f32 input, and against the magnitude kernel squared.  `off`
+    shifts the output by whole floats, so rows lose 16 B alignment (the
+    staged dword-store path for nfft = 1024 needs only 4 B); odd frame counts
+    exercise the pair whose second frame does not exist."""
+    import torch
+    nch = 3
+    g = torch.Generator(device="cuda").manual_seed(nfft + hop + n)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
+    st = vdev.Stft(nfft, hop)
+    fr, nh = st.frames(n), nfft // 2 + 1
+    buf = torch.full((off + nch * fr * nh + 64,), -7.0, device="cuda")
+    out = buf[off:off + nch * fr * nh].view(nch, fr, nh)
+    pw = st.power(sig, out=out)
+    mag = st.spectrogram(sig)
+    torch.cuda.synchronize()
+    b = buf.cpu().numpy()
+    assert np.all(b[:off] == -7.0) and np.all(b[off + nch * fr * nh:] == -7.0), "stores outside the rows"
+    x = sig.cpu().numpy().astype(np.float64)
+    w = orc.window(1, nfft).astype(np.float64)
+    pw = pw.cpu().numpy()
+    for c in range(nch):
+        pad = np.concatenate([x[c], np.zeros(nfft + hop)])
+        ref = np.abs(np.fft.rfft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1)) ** 2
+        scale = np.max(ref, axis=1, keepdims=True)
+        # |X|^2 carries twice the relative error of |X|: 2 x VV_PY_RTOL/ATOL (python/test_fft.py:37-38)
+        assert np.all(np.abs(pw[c] - ref) <= 1e-4 * np.abs(ref) + 1e-4 * scale), (c, np.max(np.abs(pw[c] - ref)))
+    m2 = mag.cpu().numpy()[:, :, :nh].astype(np.float64) ** 2
+    assert _normwise(pw, m2) <= 1e-5
+
+
 def test_golden_mel(amd, golden):
     g = golden("mel_512_26")
     st, fb = amd.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)

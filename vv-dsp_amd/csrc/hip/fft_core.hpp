@@ -490,6 +490,13 @@ __device__ __forceinline__ void st4_nt_sbase(unsigned lane_off, float v, const v
     asm volatile("global_store_dword %0, %1, %2 offset:%3 nt" ::"v"(lane_off), "v"(v), "s"(base), "n"(IMM)
                  : "memory");
 }
+// the same with a plain (write-back) store
+template <int IMM>
+__device__ __forceinline__ void st4_sbase(unsigned lane_off, float v, const void* base) {
+    static_assert(IMM >= -4096 && IMM <= 4095, "global offset range");
+    asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(lane_off), "v"(v), "s"(base), "n"(IMM)
+                 : "memory");
+}
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {

@@ -108,7 +108,7 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
 //   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
 // N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
 template <int N, int MODE, int VAR>
-__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && VAR == 0 && MODE == 0) ? 3 : 1)
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && VAR == 0 && MODE != 1) ? 3 : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink) {
@@ -116,13 +116,17 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     using Mi = Mirror<N>;
     constexpr bool TAIL = VAR == 2;
     constexpr bool STAGE = VAR == 0 && MODE == 0 && G::NPASS > 1 && G::T > 1;
-    constexpr bool GLDS = STAGE && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
+    // power rows (N = 1024): the DIRECT stores below, keeping only the
+    // 64-bin blocks under N/2 plus one lane for bin N/2
+    constexpr bool POWD = VAR == 0 && MODE == 2 && G::T == 64 && G::NPASS > 1;
+    constexpr bool GLDS = (STAGE || POWD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
     constexpr int SPAN = GLDS ? N + N / 2 : 1;   // floats per transform: hop <= N/2
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
     // written as 16 B/lane stores
     constexpr bool DIRECT = GLDS && G::T == 64;
-    constexpr int NST = DIRECT ? 2 * G::P : 2 * (G::P / 4);   // stores per pair (both rows)
+    // stores per pair (both rows): power rows keep half the blocks + bin N/2
+    constexpr int NST = DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
@@ -287,6 +291,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             // that every store instruction covers one aligned 256 B block: full
             // 128 B lines for the streaming stores, no LDS staging.
             constexpr int J = G::NPT / 2, NB = G::NB, T = G::T;
+            constexpr int PM = MODE == 2 ? 2 : 0;   // magnitude or power post
             float ea[J][R], eb[J][R], sa[R], sb[R];
 #pragma unroll
             for (int j = 0; j < J; ++j) {
@@ -294,7 +299,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 for (int r = 0; r < R; ++r) {
                     const int q = 2 * j * R + r;
                     float2 A, B;
-                    pair_post<0>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                    pair_post<PM>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
                     ea[j][r] = A.x;
                     eb[j][r] = B.x;
                 }
@@ -303,7 +308,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             for (int r = 0; r < R; ++r) {   // lane 0's odd slot 1: bins NB/2 + (R-1-r) NB, their own mirrors
                 const int qm = Mi::normal(r);
                 float2 A2, B2;
-                pair_post<0>(v[qm], v[Mi::special(qm)], &A2, &B2);
+                pair_post<PM>(v[qm], v[Mi::special(qm)], &A2, &B2);
                 sa[r] = A2.x;
                 sb[r] = B2.x;
             }
@@ -311,12 +316,24 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             const unsigned vo = 4u * (unsigned)(t == 0 ? NB - T : NB - t);
             const void* ra = rowa;
             const void* rb = has_b ? rowb : (void*)sink;   // counted stores must all issue
+            // Power rows (n/2+1 floats, so not line-aligned): a block is stored
+            // only if it lies below N/2, with plain stores (partial lines merge
+            // in L2; streaming stores of partial lines measured 1.65x slower)
+            auto st = [&](auto imm, unsigned off, float val, const void* base) {
+                constexpr int I = decltype(imm)::value;
+                if constexpr (MODE == 2) {
+                    if constexpr (I < 4 * (N / 2)) st4_sbase<I>(off, val, base);
+                } else {
+                    st4_nt_sbase<I>(off, val, base);
+                }
+            };
             static_for<0, J>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 static_for<0, R>([&](auto rc) {
                     constexpr int r = decltype(rc)::value;
-                    st4_nt_sbase<4 * (T * j + r * NB)>(ve, ea[j][r], ra);
-                    st4_nt_sbase<4 * (T * j + r * NB)>(ve, eb[j][r], rb);
+                    constexpr int IE = 4 * (T * j + r * NB), IO = 4 * ((R - 1 - r) * NB - T * j);
+                    st(std::integral_constant<int, IE>{}, ve, ea[j][r], ra);
+                    st(std::integral_constant<int, IE>{}, ve, eb[j][r], rb);
                     float oa, ob;
                     if constexpr (j + 1 < J) {
                         oa = t == 0 ? ea[j + 1][r] : ea[j][r];
@@ -325,10 +342,19 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                         oa = t == 0 ? sa[r] : ea[j][r];
                         ob = t == 0 ? sb[r] : eb[j][r];
                     }
-                    st4_nt_sbase<4 * ((R - 1 - r) * NB - T * j)>(vo, oa, ra);
-                    st4_nt_sbase<4 * ((R - 1 - r) * NB - T * j)>(vo, ob, rb);
+                    // mirror block: bins IO/4 + NB - 64 .. IO/4 + NB - 1
+                    st(std::integral_constant<int, IO + 4 * (NB - T)>{}, vo - 4u * (NB - T), oa, ra);
+                    st(std::integral_constant<int, IO + 4 * (NB - T)>{}, vo - 4u * (NB - T), ob, rb);
                 });
             });
+            if constexpr (MODE == 2) {
+                // bin N/2 = NB * (R/2): even slot j = 0, r = R/2, lane 0; the
+                // other lanes' copies go to the sink (one store per row, counted)
+                static_assert(N / 2 == NB * (R / 2), "Nyquist bin in lane 0 of an even block");
+                float* const sk = sink + 8192 + t;
+                st4_counted(t == 0 ? (float*)ra + N / 2 : sk, ea[0][R / 2]);
+                st4_counted(t == 0 ? (float*)rb + N / 2 : sk, eb[0][R / 2]);
+            }
         } else if constexpr (STAGE) {
             // both magnitude rows through the (now idle) exchange buffer, then
             // full-line 16 B/lane streaming stores: 2N/(4T) instead of 2P per lane
@@ -530,13 +556,19 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                                cnt, win, out, out_ch_stride, pN, tN, chunk, sink);
         };
         // 16 B aligned output rows allow the staged 16 B/lane stores
-        bool aligned = ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0 && N >= 4;
+        // (power rows are n/2+1 floats: their staged stores are dwords, 4 B suffice)
+        bool aligned = MODE == 2 ? ((uintptr_t)out & 3) == 0
+                                 : ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0 && N >= 4;
         // T >= 64: VAR 0 also reads its input spans by 16 B LDS-DMA
         if (Geo<N>::T >= 64)
             aligned = aligned && hop % 4 == 0 && hop <= N / 2 && ((uintptr_t)sig & 15) == 0 && (ch_stride & 3) == 0;
+        if (MODE == 2) {   // A/B switch: the register-load variant with per-bin stores
+            const char* e = getenv("VVHIP_POW_OLD");
+            if (e && *e == '1') aligned = false;
+        }
         // the VAR 0 kernels that read spans by LDS-DMA run the tail pairs too:
         // one launch for the whole job
-        constexpr bool FUSE_TAIL = MODE == 0 && Geo<N>::NPASS > 1 && Geo<N>::T >= 64;
+        constexpr bool FUSE_TAIL = (MODE == 0 || (MODE == 2 && Geo<N>::T == 64)) && Geo<N>::NPASS > 1 && Geo<N>::T >= 64;
         if (aligned && FUSE_TAIL) {
             launch(k_stft_pair<N, MODE, 0>, 0, 0LL, ppc);
         } else {
