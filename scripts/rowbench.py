@@ -227,6 +227,41 @@ def main():
                    note="compute-bound: 257 multiply-adds per sample in the reference's order, no FMA"))
     del xf, yf, fp
 
+    # ---- host-buffer (PCIe-inclusive) rate of the reference's own host-pointer API ------
+    # vv_dsp_stft_spectrogram / vv_dsp_fft_execute take host pointers: the library copies
+    # H2D, runs the kernel and copies D2H on the handle's stream (two-lane pipeline).
+    # Wall clock on the host thread, pageable numpy buffers as the reference's callers have.
+    amd = VvDsp(os.path.join(ROOT, "vv-dsp_amd", "lib", "libvvdsp_amd.so"))
+    import ctypes as C
+    fp = C.POINTER(C.c_float)
+    st_, h = amd.stft_create(1024, 256)
+    for sec in (60, 600):
+        x = rng.uniform(-1, 1, sec * 48000).astype(np.float32)
+        fr = 1 + (x.size - 1024 + 256) // 256
+        o = np.empty(fr * 1024, np.float32)
+        nf = C.c_size_t(0)
+        call = (lambda: amd.lib.vv_dsp_stft_spectrogram(h, x.ctypes.data_as(fp), x.size, o.ctypes.data_as(fp),
+                                                         C.byref(nf)))
+        assert call() == 0
+        sec_per, calls = cpu_time(call, budget=1.5, max_calls=200)
+        out.append(row(f"stft_mag_host_{sec}s", "a11 vv_dsp_stft_spectrogram, host buffers (PCIe-inclusive)",
+                       (f"1 ch x {sec} s, pageable host in/out", fr), sec_per * 1e3, x.size * 4 + fr * 4096, "frames",
+                       note=f"wall clock per reference-API call, {calls} calls; kernel-only rate in the rows above"))
+    amd.lib.vv_dsp_stft_destroy(h)
+    B = 8192
+    amd.lib.vv_dsp_fft_make_plan_many.argtypes = [C.c_size_t, C.c_int, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]
+    pl = C.c_void_p()
+    assert amd.lib.vv_dsp_fft_make_plan_many(1024, C2C, FWD, B, C.byref(pl)) == 0
+    xin = (rng.random((B, 1024)) + 1j * rng.random((B, 1024))).astype(np.complex64)
+    yo = np.empty_like(xin)
+    call = lambda: amd.lib.vv_dsp_fft_execute(pl, xin.ctypes.data, yo.ctypes.data)
+    assert call() == 0
+    sec_per, calls = cpu_time(call, budget=1.5, max_calls=200)
+    out.append(row("fft_c2c_1024_host", "a6 vv_dsp_fft_execute C2C, host buffers (PCIe-inclusive)",
+                   (f"{B} x 1024 c2c fwd, pageable host in/out", B), sec_per * 1e3, 16 * 1024 * B, "transforms",
+                   note=f"wall clock per call of a batch-{B} plan, {calls} calls"))
+    amd.lib.vv_dsp_fft_destroy(pl)
+
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"device": torch.cuda.get_device_name(0), "date": time.strftime("%Y-%m-%d"),
