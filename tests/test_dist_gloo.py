@@ -29,7 +29,9 @@ def _signals(nch):
     return rng.uniform(-1, 1, (nch, NS)).astype(np.float32)
 
 
-def _worker(rank, world, nch, port, q):
+def _worker(rank, world, nch, port, q, slab=None):
+    if slab is not None:   # gather in slabs of `slab` bytes (one channel's rows per collective)
+        vvdsp_dist.GATHER_SLAB_BYTES = slab
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -56,14 +58,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,nch", [(2, 5), (3, 5), (2, 6), (3, 6)])
-def test_sharded_spectrogram_gather_gloo(world, nch):
+@pytest.mark.parametrize("world,nch,slab", [(2, 5, None), (3, 5, None), (2, 6, None), (3, 6, None), (2, 6, 1),
+                                            (3, 9, 100000)])
+def test_sharded_spectrogram_gather_gloo(world, nch, slab):
     if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
         pytest.skip("oracle not built (make -C oracle)")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, nch, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, nch, port, q, slab)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

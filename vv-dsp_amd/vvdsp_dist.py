@@ -26,6 +26,9 @@ def shard_sizes(total, world):
     return [b - a for a, b in (channel_shard(total, world, r) for r in range(world))]
 
 
+GATHER_SLAB_BYTES = 1 << 30
+
+
 def gather_rows(local, total, dst=0, group=None, out=None):
     """Gather every rank's [ch_r, ...] block into one [total, ...] tensor on
     rank `dst` (None elsewhere).  Equal shards land directly in `out` (or a
@@ -38,14 +41,22 @@ def gather_rows(local, total, dst=0, group=None, out=None):
         raise ValueError(f"rank {rank} holds {local.shape[0]} channels, layout says {sizes[rank]}")
     cmax = max(sizes)
     if min(sizes) == cmax and cmax > 0:
+        # slabs of whole channels, at most ~1 GiB per rank per collective: keeps
+        # every message far below 2^31 elements (a config-5 shard is 14.7 GB)
+        row_bytes = max(1, local[0].numel() * local.element_size())
+        step = max(1, min(cmax, GATHER_SLAB_BYTES // row_bytes))
+        loc = local.contiguous()
         if rank == dst:
             if out is None:
                 out = torch.empty((total,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-            dist.gather(local.contiguous(), gather_list=list(out.view((world, cmax) + tuple(local.shape[1:]))
-                                                              .unbind(0)), dst=dst, group=group)
-            return out
-        dist.gather(local.contiguous(), dst=dst, group=group)
-        return None
+            ov = out.view((world, cmax) + tuple(local.shape[1:]))
+        for i0 in range(0, cmax, step):
+            i1 = min(cmax, i0 + step)
+            if rank == dst:
+                dist.gather(loc[i0:i1], gather_list=[ov[r, i0:i1] for r in range(world)], dst=dst, group=group)
+            else:
+                dist.gather(loc[i0:i1], dst=dst, group=group)
+        return out if rank == dst else None
     if local.shape[0] < cmax:
         pad = torch.zeros((cmax - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
                           device=local.device)
