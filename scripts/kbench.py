@@ -266,6 +266,7 @@ CASES = {
     "stftpow": lambda: case_stft_power(32, 600),
     "stftpowold": with_env(lambda: case_stft_power(32, 600), "VVHIP_POW_OLD", "1"),
     "stftc": lambda: case_stft(8, 600, complex_out=True),
+    "stftcold": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_POW_OLD", "1"),
     "fir": lambda: case_fir(8, 1 << 24),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "hilbert1024": lambda: case_hilbert(1024, 65536),

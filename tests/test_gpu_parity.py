@@ -583,6 +583,35 @@ def test_stft_power_rows(vdev, orc, nfft, hop, n, off):
     assert _normwise(pw, m2) <= 1e-5
 
 
+@pytest.mark.parametrize("nfft,hop,n,off", [(1024, 256, 48128, 0), (1024, 256, 48000, 1), (1024, 512, 20000, 3),
+                                            (1024, 256, 1280, 0), (1024, 256, 700, 1), (1024, 100, 9999, 0),
+                                            (1024, 768, 30001, 2), (512, 128, 10000, 1), (2048, 512, 30000, 0)])
+def test_stft_complex_rows(vdev, orc, nfft, hop, n, off):
+    """Complex STFT rows (vv_dsp_stft_process batched over frames, full nfft bins,
+    stft.c:74-92) per bin against NumPy f64 at the harness tolerance, with guard
+    regions around the rows (odd frame counts: the pair without a second frame)."""
+    import torch
+    nch = 3
+    g = torch.Generator(device="cuda").manual_seed(nfft * 3 + hop + n)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
+    st = vdev.Stft(nfft, hop)
+    fr = st.frames(n)
+    buf = torch.full((off + nch * fr * nfft + 64,), complex(-7.0, 3.0), dtype=torch.complex64, device="cuda")
+    out = buf[off:off + nch * fr * nfft].view(nch, fr, nfft)
+    y = st.spectrogram(sig, out=out, complex_out=True)
+    torch.cuda.synchronize()
+    b = buf.cpu().numpy()
+    assert np.all(b[:off] == complex(-7.0, 3.0)) and np.all(b[off + nch * fr * nfft:] == complex(-7.0, 3.0))
+    x = sig.cpu().numpy().astype(np.float64)
+    w = orc.window(1, nfft).astype(np.float64)
+    y = y.cpu().numpy()
+    r, a = tolerances()
+    for c in range(nch):
+        pad = np.concatenate([x[c], np.zeros(nfft + hop)])
+        ref = np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1)
+        np.testing.assert_allclose(y[c], ref, rtol=r, atol=4 * a)
+
+
 def test_golden_mel(amd, golden):
     g = golden("mel_512_26")
     st, fb = amd.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)

@@ -490,6 +490,14 @@ __device__ __forceinline__ void st4_nt_sbase(unsigned lane_off, float v, const v
     asm volatile("global_store_dword %0, %1, %2 offset:%3 nt" ::"v"(lane_off), "v"(v), "s"(base), "n"(IMM)
                  : "memory");
 }
+// 8 B (complex) streaming store at wave-uniform base + 32-bit lane offset + IMM
+template <int IMM>
+__device__ __forceinline__ void st8_nt_sbase(unsigned lane_off, float2 v, const void* base) {
+    static_assert(IMM >= -4096 && IMM <= 4095, "global offset range");
+    const vf2_t d = pk(v);
+    asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 nt" ::"v"(lane_off), "v"(d), "s"(base), "n"(IMM)
+                 : "memory");
+}
 // the same with a plain (write-back) store
 template <int IMM>
 __device__ __forceinline__ void st4_sbase(unsigned lane_off, float v, const void* base) {

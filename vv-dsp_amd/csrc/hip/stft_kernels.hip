@@ -108,7 +108,7 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
 //   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
 // N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
 template <int N, int MODE, int VAR>
-__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && VAR == 0 && MODE != 1) ? 3 : 1)
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && VAR == 0) ? 3 : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink) {
@@ -119,7 +119,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // power rows (N = 1024): the DIRECT stores below, keeping only the
     // 64-bin blocks under N/2 plus one lane for bin N/2
     constexpr bool POWD = VAR == 0 && MODE == 2 && G::T == 64 && G::NPASS > 1;
-    constexpr bool GLDS = (STAGE || POWD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
+    // complex rows (N = 1024): DIRECT with 8 B/lane stores, conj() for the mirror blocks
+    constexpr bool CPXD = VAR == 0 && MODE == 1 && G::T == 64 && G::NPASS > 1;
+    constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
     constexpr int SPAN = GLDS ? N + N / 2 : 1;   // floats per transform: hop <= N/2
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
@@ -282,7 +284,50 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
         char* rowb = rowa + ROW * ES;
         const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
-        if constexpr (DIRECT) {
+        if constexpr (DIRECT && MODE == 1) {
+            // as the DIRECT block below, with complex bins: a mirror block holds
+            // conj(X[k]) (real frames), lane 0's rotated partner conj of its own
+            // bin in slot j + 1, or in the last slot its self-mirrored bin as is.
+            // Byte offsets reach 8 KB: blocks past 4 KB use the base + 4096.
+            constexpr int J = G::NPT / 2, NB = G::NB, T = G::T;
+            const unsigned ve = 8u * (unsigned)t;
+            const unsigned vo = 8u * (unsigned)(t == 0 ? 0 : T - t);
+            const char* ra = rowa;
+            const char* rb = has_b ? rowb : reinterpret_cast<const char*>(sink);   // counted stores must all issue
+            const char* ra2 = ra + 4096;
+            const char* rb2 = rb + 4096;
+            auto st = [&](auto imm, unsigned off, float2 val, const char* b1, const char* b2) {
+                constexpr int I = decltype(imm)::value;
+                if constexpr (I < 4096) st8_nt_sbase<I>(off, val, b1);
+                else st8_nt_sbase<I - 4096>(off, val, b2);
+            };
+            float2 nxa[R], nxb[R];   // lane 0's partner values for slot j: conj of slot j+1's own bins
+            static_for<0, J>([&](auto jc) {
+                constexpr int j = J - 1 - decltype(jc)::value;   // last slot first: its partners are the specials
+                static_for<0, R>([&](auto rc) {
+                    constexpr int r = decltype(rc)::value;
+                    constexpr int q = 2 * j * R + r;
+                    float2 A, B;
+                    pair_post<1>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                    float2 pa, pb;
+                    if constexpr (j == J - 1) {
+                        const int qm = Mi::normal(r);
+                        pair_post<1>(v[qm], v[Mi::special(qm)], &pa, &pb);
+                    } else {
+                        pa = nxa[r];
+                        pb = nxb[r];
+                    }
+                    const float2 oa = select2(t == 0, pa, cconj(A)), ob = select2(t == 0, pb, cconj(B));
+                    nxa[r] = cconj(A);
+                    nxb[r] = cconj(B);
+                    constexpr int IE = 8 * (T * j + r * NB), IO = 8 * ((R - 1 - r) * NB - T * j + NB - T);
+                    st(std::integral_constant<int, IE>{}, ve, A, ra, ra2);
+                    st(std::integral_constant<int, IE>{}, ve, B, rb, rb2);
+                    st(std::integral_constant<int, IO>{}, vo, oa, ra, ra2);
+                    st(std::integral_constant<int, IO>{}, vo, ob, rb, rb2);
+                });
+            });
+        } else if constexpr (DIRECT) {
             // Even slot j holds bins k = t + T j + r NB (lane-contiguous, 256 B
             // aligned per store); its partner slot holds N - k, which for lanes
             // t >= 1 covers N - k of the same magnitude.  Lane 0's partner bins
@@ -556,19 +601,21 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                                cnt, win, out, out_ch_stride, pN, tN, chunk, sink);
         };
         // 16 B aligned output rows allow the staged 16 B/lane stores
-        // (power rows are n/2+1 floats: their staged stores are dwords, 4 B suffice)
-        bool aligned = MODE == 2 ? ((uintptr_t)out & 3) == 0
-                                 : ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0 && N >= 4;
+        // (power rows are n/2+1 floats: their direct stores are dwords, 4 B suffice;
+        // complex rows are stored 8 B per lane)
+        bool aligned = MODE == 2   ? ((uintptr_t)out & 3) == 0
+                       : MODE == 1 ? ((uintptr_t)out & 7) == 0
+                                   : ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0 && N >= 4;
         // T >= 64: VAR 0 also reads its input spans by 16 B LDS-DMA
         if (Geo<N>::T >= 64)
             aligned = aligned && hop % 4 == 0 && hop <= N / 2 && ((uintptr_t)sig & 15) == 0 && (ch_stride & 3) == 0;
-        if (MODE == 2) {   // A/B switch: the register-load variant with per-bin stores
+        if (MODE != 0) {   // A/B switch: the register-load variant with per-bin stores
             const char* e = getenv("VVHIP_POW_OLD");
             if (e && *e == '1') aligned = false;
         }
         // the VAR 0 kernels that read spans by LDS-DMA run the tail pairs too:
         // one launch for the whole job
-        constexpr bool FUSE_TAIL = (MODE == 0 || (MODE == 2 && Geo<N>::T == 64)) && Geo<N>::NPASS > 1 && Geo<N>::T >= 64;
+        constexpr bool FUSE_TAIL = (MODE == 0 || Geo<N>::T == 64) && Geo<N>::NPASS > 1 && Geo<N>::T >= 64;
         if (aligned && FUSE_TAIL) {
             launch(k_stft_pair<N, MODE, 0>, 0, 0LL, ppc);
         } else {
