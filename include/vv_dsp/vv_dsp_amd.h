@@ -44,6 +44,16 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_power_device(vv_dsp_stft* h, const vv
                                                         size_t n, size_t nch, size_t ch_stride,
                                                         vv_dsp_real* d_out_power, size_t out_ch_stride,
                                                         void* stream, size_t* out_frames);
+/* One shard of a long signal's frames: rows of frames [frame0, frame0 + nframes)
+ * of the same spectrogram, row of frame f at d_out + (f - frame0) * row.
+ * out_kind 0: magnitudes [fft_size] floats, 1: complex spectrum [fft_size]
+ * vv_dsp_cpx, 2: power [fft_size/2+1] floats.  Even frame0 gives rows
+ * bit-identical to the whole-signal call.  VV_DSP_ERROR_OUT_OF_RANGE when the
+ * range passes the last frame (stft.c:119 frame count). */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_frames_range_device(vv_dsp_stft* h, const vv_dsp_real* d_signal,
+                                                               size_t n, size_t nch, size_t ch_stride,
+                                                               size_t frame0, size_t nframes, void* d_out,
+                                                               size_t out_ch_stride, int out_kind, void* stream);
 /* count frames real[count][fft_size] -> cpx[count][fft_size] (vv_dsp_stft_process batched) */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_process_device(vv_dsp_stft* h, const vv_dsp_real* d_frames,
                                                           size_t count, vv_dsp_cpx* d_spec, void* stream);

@@ -78,6 +78,13 @@ int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, fl
 int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
                                   size_t ch_stride, void* d_out, size_t out_ch_stride,
                                   int out_kind, void* stream);
+/* Frames [frame0, frame0 + nframes) of the same spectrogram (the row of frame
+ * f is out + (f - frame0) * row): one shard of a long signal's frames.  With an
+ * even frame0 the rows are bit-identical to the whole-signal call (frames are
+ * transformed in pairs (2j, 2j+1)).  ST_RANGE if the range exceeds the frames. */
+int vvhip_stft_spectrogram_range_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
+                                        size_t ch_stride, size_t frame0, size_t nframes, void* d_out,
+                                        size_t out_ch_stride, int out_kind, void* stream);
 int vvhip_stft_process_host(vvhip_stft* h, const float* frame, float* spec_out);
 int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count, float* d_spec,
                               void* stream);

@@ -52,6 +52,32 @@ def _worker(rank, world, nch, port, q, slab=None):
         dist.destroy_process_group()
 
 
+def _frame_worker(rank, world, port, q):
+    """One long signal split by frame ranges (config 3 sharded): each rank
+    transforms its input slice (frame0's first sample on, as
+    vv_dsp_stft_frames_range_device does), rank 0 gathers the rows."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vvapi import Oracle
+        orc = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
+        x = _signals(1)[0]
+        frames = 1 + (NS - NFFT + HOP) // HOP
+        lo, hi = vvdsp_dist.frame_shard(frames, world, rank)
+        if hi > lo:
+            local = torch.from_numpy(np.ascontiguousarray(orc.spectrogram(x[lo * HOP:], NFFT, HOP)[:hi - lo]))
+        else:
+            local = torch.zeros((0, NFFT))
+        full = vvdsp_dist.gather_frames(local, frames, dst=0)
+        if rank == 0:
+            ref = orc.spectrogram(x, NFFT, HOP)
+            q.put(bool(np.array_equal(full.numpy(), ref)) and tuple(full.shape) == ref.shape)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -73,6 +99,32 @@ def test_sharded_spectrogram_gather_gloo(world, nch, slab):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_frame_sharded_spectrogram_gather_gloo(world):
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        pytest.skip("oracle not built (make -C oracle)")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_frame_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
+
+
+def test_frame_shard_layout():
+    for frames in (0, 1, 2, 5, 11247, 11248):
+        for world in (1, 2, 3, 8):
+            spans = [vvdsp_dist.frame_shard(frames, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == frames
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert all(lo % 2 == 0 for lo, hi in spans if hi > lo)   # whole frame pairs per rank
+    assert vvdsp_dist.frame_shard_sizes(11248, 8) == [1406] * 8
 
 
 def test_channel_shard_layout():

@@ -612,6 +612,34 @@ def test_stft_complex_rows(vdev, orc, nfft, hop, n, off):
         np.testing.assert_allclose(y[c], ref, rtol=r, atol=4 * a)
 
 
+@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("nfft,hop,n", [(1024, 256, 48000 + 333), (1024, 256, 96000), (512, 128, 20001)])
+def test_stft_frames_range(vdev, nfft, hop, n, kind):
+    """vv_dsp_stft_frames_range_device: frame-range shards of one long signal
+    (SURVEY 8e, config 3 sharded across GPUs).  Even frame0 (the frame_shard
+    layout): rows bit-identical to the whole-signal call.  Odd frame0: the pair
+    partners change, so within f32 rounding.  Ranges past the last frame fail."""
+    import torch
+    import vvdsp_dist
+    g = torch.Generator(device="cuda").manual_seed(n + kind)
+    sig = torch.rand(2, n, device="cuda", generator=g) * 2 - 1
+    st = vdev.Stft(nfft, hop)
+    fr = st.frames(n)
+    full = {0: lambda: st.spectrogram(sig), 1: lambda: st.spectrogram(sig, complex_out=True),
+            2: lambda: st.power(sig)}[kind]().cpu()
+    for world in (1, 3, 8):
+        parts = [st.frames_range(sig, lo, hi - lo, kind).cpu()
+                 for lo, hi in (vvdsp_dist.frame_shard(fr, world, r) for r in range(world)) if hi > lo]
+        assert torch.equal(torch.cat(parts, 1), full), world
+    for lo, cnt in ((1, 5), (fr - 3, 3), (7, fr - 7)):
+        y = st.frames_range(sig, lo, cnt, kind).cpu().numpy()
+        ref = full[:, lo:lo + cnt].numpy()
+        assert _normwise(y, ref) <= 2e-6, (lo, cnt)
+    with pytest.raises(vdev.VvError, match="status 3"):   # VV_DSP_ERROR_OUT_OF_RANGE
+        st.frames_range(sig, fr - 2, 3, kind)
+    assert st.frames_range(sig, fr, 0, kind).shape[1] == 0
+
+
 def test_golden_mel(amd, golden):
     g = golden("mel_512_26")
     st, fb = amd.mel_filterbank(512, 26, 16000.0, 0.0, 8000.0)

@@ -11,6 +11,7 @@
 #include "vvhip_internal.hpp"
 
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -377,11 +378,26 @@ struct vvhip_stft {
 
 // out_kind: 0 magnitude rows [frame][nfft], 1 complex rows [frame][nfft],
 // 2 power rows [frame][nfft/2+1]
+// frame0/nframes: rows of frames [frame0, frame0 + nframes) only (nframes =
+// SIZE_MAX: all).  The signal is viewed from frame0's first sample on: frame
+// f >= frame0 of the whole signal is frame f - frame0 of that view, and the
+// zero padding past n is the same.
 static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch, size_t ch_stride,
-                           void* out, size_t out_ch_stride, int out_kind, hipStream_t s) {
-    const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
-    const long long NF = (long long)h->nfft;
+                           void* out, size_t out_ch_stride, int out_kind, hipStream_t s, size_t frame0 = 0,
+                           size_t nframes = SIZE_MAX) {
+    size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
     if (out_kind < 0 || out_kind > 2) return fail(ST_RANGE, "stft output kind");
+    if (frame0 != 0 || nframes != SIZE_MAX) {
+        if (frame0 > frames || (nframes != SIZE_MAX && nframes > frames - frame0))
+            return fail(ST_RANGE, "stft frame range past the last frame");
+        if (nframes == SIZE_MAX) nframes = frames - frame0;
+        if (nframes == 0) return ST_OK;
+        const size_t off = frame0 * h->hop;   // < n for every existing frame but a wholly padded last one
+        sig += off < n ? off : n;
+        n -= off < n ? off : n;
+        frames = nframes;
+    }
+    const long long NF = (long long)h->nfft;
     if (stft_fused_supported(NF)) {
         HIPCHK(launch_stft(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch, (long long)ch_stride,
                            (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
@@ -468,6 +484,16 @@ int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n
     if (nch == 0) return ST_OK;
     return stft_frames_run(h, d_signal, n, nch, ch_stride, d_out, out_ch_stride, complex_out,
                            (hipStream_t)stream);
+}
+
+int vvhip_stft_spectrogram_range_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
+                                        size_t ch_stride, size_t frame0, size_t nframes, void* d_out,
+                                        size_t out_ch_stride, int out_kind, void* stream) {
+    if (!h || !d_signal || !d_out) return ST_NULL;
+    if (nch == 0) return ST_OK;
+    if (nframes == SIZE_MAX) return fail(ST_RANGE, "stft frame count");
+    return stft_frames_run(h, d_signal, n, nch, ch_stride, d_out, out_ch_stride, out_kind, (hipStream_t)stream,
+                           frame0, nframes);
 }
 
 int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, float* out_mag) {

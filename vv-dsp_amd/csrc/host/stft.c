@@ -118,6 +118,14 @@ vv_dsp_status vv_dsp_stft_power_device(vv_dsp_stft* h, const vv_dsp_real* d_sign
                                                         out_ch_stride, 2, stream);
 }
 
+vv_dsp_status vv_dsp_stft_frames_range_device(vv_dsp_stft* h, const vv_dsp_real* d_signal, size_t n, size_t nch,
+                                              size_t ch_stride, size_t frame0, size_t nframes, void* d_out,
+                                              size_t out_ch_stride, int out_kind, void* stream) {
+    if (!h || !d_signal || !d_out) return VV_DSP_ERROR_NULL_POINTER;
+    return (vv_dsp_status)vvhip_stft_spectrogram_range_device(h->dev, d_signal, n, nch, ch_stride, frame0, nframes,
+                                                              d_out, out_ch_stride, out_kind, stream);
+}
+
 vv_dsp_status vv_dsp_stft_process_device(vv_dsp_stft* h, const vv_dsp_real* d_frames, size_t count,
                                          vv_dsp_cpx* d_spec, void* stream) {
     if (!h || !d_frames || !d_spec) return VV_DSP_ERROR_NULL_POINTER;

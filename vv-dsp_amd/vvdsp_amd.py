@@ -53,6 +53,7 @@ def lib():
     L.vv_dsp_stft_spectrogram_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_spectrum_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_power_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_stft_frames_range_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _sz, _sz, _vp, _sz, C.c_int, _vp]
     L.vv_dsp_stft_process_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.vv_dsp_stft_reconstruct_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp]
     L.vv_dsp_fir_plan_create.argtypes = [_vp, _sz, C.POINTER(_vp)]
@@ -159,6 +160,22 @@ class Stft:
         _check(lib().vv_dsp_stft_power_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * nh,
                                                _stream(stream), C.byref(nf)), "stft_power_device")
         assert nf.value == fr
+        return out if sig.dim() == 2 else out[0]
+
+    def frames_range(self, sig, frame0, nframes, kind=0, out=None, stream=None):
+        """Rows of frames [frame0, frame0 + nframes) of sig's spectrogram (one shard
+        of a long signal): kind 0 magnitude, 1 complex, 2 power (nfft//2 + 1 bins)."""
+        sig2 = sig if sig.dim() == 2 else sig.unsqueeze(0)
+        nch, n = sig2.shape
+        width = self.nfft // 2 + 1 if kind == 2 else self.nfft
+        dt = torch.complex64 if kind == 1 else torch.float32
+        if out is None:
+            out = torch.empty((nch, nframes, width), dtype=dt, device=sig.device)
+        if nframes == 0 and frame0 <= self.frames(n):   # empty range: nothing to write (out has no storage)
+            return out if sig.dim() == 2 else out[0]
+        _check(lib().vv_dsp_stft_frames_range_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), frame0, nframes,
+                                                      _ptr(out), nframes * width, kind, _stream(stream)),
+               "stft_frames_range_device")
         return out if sig.dim() == 2 else out[0]
 
     def process(self, frames, stream=None):

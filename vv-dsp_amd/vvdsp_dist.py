@@ -26,17 +26,33 @@ def shard_sizes(total, world):
     return [b - a for a, b in (channel_shard(total, world, r) for r in range(world))]
 
 
+def frame_shard(frames, world, rank):
+    """Contiguous frame range [lo, hi) of `rank` for one long signal (SURVEY 8e,
+    config 3 sharded): whole frame pairs per rank, so every lo is even and each
+    rank's rows are bit-identical to the unsharded spectrogram (the kernels
+    transform frames (2j, 2j+1) together)."""
+    plo, phi = channel_shard((int(frames) + 1) // 2, world, rank)
+    return min(2 * plo, frames), min(2 * phi, frames)
+
+
+def frame_shard_sizes(frames, world):
+    return [b - a for a, b in (frame_shard(frames, world, r) for r in range(world))]
+
+
 GATHER_SLAB_BYTES = 1 << 30
 
 
-def gather_rows(local, total, dst=0, group=None, out=None):
+def gather_rows(local, total, dst=0, group=None, out=None, sizes=None):
     """Gather every rank's [ch_r, ...] block into one [total, ...] tensor on
     rank `dst` (None elsewhere).  Equal shards land directly in `out` (or a
     new tensor) with no extra copy; uneven shards are padded to the largest
-    one for the collective and trimmed on the destination."""
+    one for the collective and trimmed on the destination.  `sizes`: the
+    per-rank leading sizes (default: the channel_shard layout)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    sizes = shard_sizes(total, world)
+    sizes = shard_sizes(total, world) if sizes is None else list(sizes)
+    if len(sizes) != world or sum(sizes) != total:
+        raise ValueError(f"shard sizes {sizes} do not cover {total} rows on {world} ranks")
     if local.shape[0] != sizes[rank]:
         raise ValueError(f"rank {rank} holds {local.shape[0]} channels, layout says {sizes[rank]}")
     cmax = max(sizes)
@@ -69,3 +85,10 @@ def gather_rows(local, total, dst=0, group=None, out=None):
         return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0)
     dist.gather(send, dst=dst, group=group)
     return None
+
+
+def gather_frames(local, frames, dst=0, group=None):
+    """Gather a single signal's frame shards ([f_r, width] per rank, frame_shard
+    layout) into the whole [frames, width] spectrogram on rank `dst`."""
+    world = dist.get_world_size(group)
+    return gather_rows(local, frames, dst=dst, group=group, sizes=frame_shard_sizes(frames, world))
