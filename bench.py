@@ -77,13 +77,46 @@ def fft_c2c_roofline(reps=20):
     y = torch.empty_like(x)
     plan = vv.FftPlan(N, vv.C2C, vv.FWD, batch=B)
     avg, best = timed_launches(lambda: plan(x, out=y), reps)
+    planb = vv.FftPlan(N, vv.C2C, vv.BWD, batch=B)
+    bavg, bbest = timed_launches(lambda: planb(x, out=y), reps)
     byts = 2 * B * N * 8
     del x, y
     return {"workload": "config2: 65536 x 1024-pt c2c f32 forward", "bytes_per_launch": byts,
             "ms_avg": round(avg, 4), "ms_min": round(best, 4),
             "achieved_GBs": round(byts / (avg * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
             "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "ffts_per_s": round(B / (avg * 1e-3), 1)}
+            "ffts_per_s": round(B / (avg * 1e-3), 1),
+            "backward": {"ms_avg": round(bavg, 4), "ms_min": round(bbest, 4),
+                         "frac": round(byts / (bavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def stft_config3(reps=50, burst=100):
+    """Config 3: STFT magnitude of 60 s mono @ 48 kHz (11,248 frames), one call,
+    and `burst` calls back to back between one pair of events."""
+    n = 60 * 48000
+    g = torch.Generator(device="cuda").manual_seed(3)
+    sig = torch.rand(1, n, device="cuda", generator=g) * 2 - 1
+    st = vv.Stft(NFFT, HOP)
+    fr = st.frames(n)
+    out = torch.empty(1, fr, NFFT, device="cuda")
+    fn = lambda: st.spectrogram(sig, out=out)  # noqa: E731
+    avg, best = timed_launches(fn, reps)
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(burst):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    per = a.elapsed_time(b) / burst
+    byts = n * 4 + NFFT * 4 + fr * NFFT * 4
+    del sig, out
+    return {"workload": "config3: STFT 60 s mono @ 48 kHz, 1024 Hann, hop 256 (11,248 frames)",
+            "bytes_per_call": byts, "ms_avg": round(avg, 4), "ms_min": round(best, 4),
+            "frames_per_s": round(fr / (avg * 1e-3), 1),
+            "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            f"back_to_back_{burst}": {"ms_per_call": round(per, 4), "frames_per_s": round(fr / (per * 1e-3), 1),
+                                      "frac": round(byts / (per * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
 
 def fir_roofline(reps=10):
@@ -313,6 +346,8 @@ def main():
         res["fft_c2c_1024"] = fft_c2c_roofline()
         torch.cuda.empty_cache()
         res["fir_ols_257"] = fir_roofline()
+        torch.cuda.empty_cache()
+        res["stft_config3"] = stft_config3()
         torch.cuda.empty_cache()
     if rank == 0 and not args.no_extras and world == 1:
         res["cpu_baseline"] = cpu_baseline()
