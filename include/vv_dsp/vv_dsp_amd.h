@@ -54,6 +54,17 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_frames_range_device(vv_dsp_stft* h, c
                                                                size_t n, size_t nch, size_t ch_stride,
                                                                size_t frame0, size_t nframes, void* d_out,
                                                                size_t out_ch_stride, int out_kind, void* stream);
+/* Batched framing (vv_dsp_fetch_frame / vv_dsp_overlap_add, framing.c:71-146):
+ * frames [frame0, frame0 + count) into d_frames[count][frame_len]; and count
+ * frames added into d_out[output_len] at (frame0 + f) * hop_len, every output
+ * sample summed in frame order (bit-identical to the per-frame loop). */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_fetch_frames_device(const vv_dsp_real* d_signal, size_t signal_len,
+                                                          vv_dsp_real* d_frames, size_t frame_len, size_t hop_len,
+                                                          size_t frame0, size_t count, int center,
+                                                          const vv_dsp_real* d_window, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_overlap_add_device(const vv_dsp_real* d_frames, size_t count,
+                                                         vv_dsp_real* d_out, size_t output_len, size_t frame_len,
+                                                         size_t hop_len, size_t frame0, void* stream);
 /* count frames real[count][fft_size] -> cpx[count][fft_size] (vv_dsp_stft_process batched) */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_process_device(vv_dsp_stft* h, const vv_dsp_real* d_frames,
                                                           size_t count, vv_dsp_cpx* d_spec, void* stream);

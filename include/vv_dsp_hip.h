@@ -94,6 +94,21 @@ int vvhip_stft_reconstruct_host(vvhip_stft* h, const float* spec, float* out_add
 int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t count, size_t hop,
                                   float* d_out_add, float* d_norm_add, void* stream);
 
+/* ---- framing (src/core/framing.c:58-146) ----
+ * Device: frames [frame0, frame0 + count) of an n-sample signal into
+ * d_frames[count][frame_len] (zero padding, or reflection when center != 0;
+ * times d_window when not NULL), and the overlap-add of count frames into
+ * d_out[out_len] at (frame0 + f) * hop, each output sample summed in frame
+ * order.  Host: one frame, the reference's signatures (via the device). */
+int vvhip_fetch_frames_device(const float* d_signal, size_t n, float* d_frames, size_t frame_len, size_t hop,
+                              size_t frame0, size_t count, int center, const float* d_window, void* stream);
+int vvhip_overlap_add_device(const float* d_frames, size_t count, float* d_out, size_t out_len, size_t frame_len,
+                             size_t hop, size_t frame0, void* stream);
+int vvhip_fetch_frame_host(const float* signal, size_t n, float* frame, size_t frame_len, size_t hop,
+                           size_t frame_index, int center, const float* window);
+int vvhip_overlap_add_host(const float* frame, float* out, size_t out_len, size_t frame_len, size_t hop,
+                           size_t frame_index);
+
 /* ---- FIR (fir.c) ---- */
 int vvhip_fir_create(const float* h, size_t taps, vvhip_fir** out);
 void vvhip_fir_destroy(vvhip_fir* f);

@@ -471,3 +471,68 @@ int orc_mfcc(const float* log_mel, size_t frames, size_t n_mels, size_t n_coeffs
     free(d);
     return 0;
 }
+
+/* ------------------------------------------------------------------ framing
+ * src/core/framing.c.  Non-centred frames start at f*hop and are zero-padded
+ * outside the signal; centred frames start at f*hop - len/2 and mirror the
+ * signal about its ends (sample -1 -> 0, -2 -> 1, n -> n-1; repeated
+ * reflections with period 2n). */
+static size_t orc_reflect(long idx, size_t n) {   /* framing.c:21-56 */
+    if (n == 0) return 0;
+    if (idx < 0) {
+        long a = -idx - 1;
+        if (a >= (long)n) {
+            const long period = 2 * (long)n;
+            a %= period;
+            if (a >= (long)n) a = period - 1 - a;
+        }
+        return (size_t)a;
+    }
+    if (idx >= (long)n) {
+        long r = (long)n - 1 - (idx - (long)n);
+        if (r < 0) {
+            r = -r - 1;
+            if (r >= (long)n) {
+                const long period = 2 * (long)n;
+                r %= period;
+                if (r >= (long)n) r = period - 1 - r;
+            }
+        }
+        if (r < 0) r = 0;
+        if (r > (long)n - 1) r = (long)n - 1;
+        return (size_t)r;
+    }
+    return (size_t)idx;
+}
+
+size_t orc_get_num_frames(size_t signal_len, size_t frame_len, size_t hop_len, int center) {
+    if (hop_len == 0) return 0;
+    if (center) return (signal_len + hop_len - 1) / hop_len;
+    if (signal_len < frame_len) return 0;
+    return 1 + (signal_len - frame_len) / hop_len;
+}
+
+int orc_fetch_frame(const float* signal, size_t signal_len, float* frame, size_t frame_len,
+                    size_t hop_len, size_t frame_index, int center, const float* window) {
+    if (!signal || !frame) return 1;
+    if (signal_len == 0 || frame_len == 0 || hop_len == 0) return 2;
+    const long start = center ? (long)(frame_index * hop_len) - (long)(frame_len / 2) : (long)(frame_index * hop_len);
+    for (size_t i = 0; i < frame_len; ++i) {
+        const long k = start + (long)i;
+        float v;
+        if (center) v = signal[orc_reflect(k, signal_len)];
+        else v = (k < 0 || k >= (long)signal_len) ? 0.0f : signal[k];
+        frame[i] = window ? v * window[i] : v;
+    }
+    return 0;
+}
+
+int orc_overlap_add(const float* frame, float* out, size_t out_len, size_t frame_len,
+                    size_t hop_len, size_t frame_index) {
+    if (!frame || !out) return 1;
+    if (out_len == 0 || frame_len == 0 || hop_len == 0) return 2;
+    const size_t s0 = frame_index * hop_len;
+    for (size_t i = 0; i < frame_len; ++i)
+        if (s0 + i < out_len) out[s0 + i] += frame[i];
+    return 0;
+}

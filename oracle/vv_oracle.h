@@ -53,6 +53,13 @@ int orc_fir_apply(const float* h, size_t taps, float* history, size_t* hist_idx,
 int orc_fir_apply_fft(const float* h, size_t taps, const float* x, float* y, size_t n);
 
 /* Mel / MFCC (src/features/mel.c; HTK variant, the only one the reference builds) */
+/* ---- framing (src/core/framing.c) ---- */
+size_t orc_get_num_frames(size_t signal_len, size_t frame_len, size_t hop_len, int center); /* :58-69 */
+int orc_fetch_frame(const float* signal, size_t signal_len, float* frame, size_t frame_len,
+                    size_t hop_len, size_t frame_index, int center, const float* window); /* :71-121 */
+int orc_overlap_add(const float* frame, float* out, size_t out_len, size_t frame_len,
+                    size_t hop_len, size_t frame_index);                                 /* :123-146 */
+
 float orc_hz_to_mel(float hz);                                            /* :14-20 */
 float orc_mel_to_hz(float mel);                                           /* :22-28 */
 int orc_mel_filterbank(size_t n_fft, size_t n_mels, float sample_rate, float fmin, float fmax,

@@ -194,6 +194,37 @@ class VvDsp:
                 self.lib.vv_dsp_fir_state_free(C.byref(state))
         return y
 
+    # ---- framing (src/core/framing.c:58-146) ---------------------------------
+    def _framing_setup(self):
+        L = self.lib
+        if getattr(self, "_framing", False):
+            return
+        L.vv_dsp_get_num_frames.argtypes = [C.c_size_t, C.c_size_t, C.c_size_t, C.c_int]
+        L.vv_dsp_get_num_frames.restype = C.c_size_t
+        L.vv_dsp_fetch_frame.argtypes = [_f32p, C.c_size_t, _f32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int, _f32p]
+        L.vv_dsp_overlap_add.argtypes = [_f32p, _f32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t]
+        self._framing = True
+
+    def get_num_frames(self, n, frame_len, hop, center):
+        self._framing_setup()
+        return self.lib.vv_dsp_get_num_frames(n, frame_len, hop, center)
+
+    def fetch_frame(self, x, frame_len, hop, index, center, window=None):
+        """-> (status, frame)"""
+        self._framing_setup()
+        x = np.ascontiguousarray(x, np.float32)
+        fr = np.zeros(frame_len, np.float32)
+        w = None if window is None else _fp(np.ascontiguousarray(window, np.float32))
+        st = self.lib.vv_dsp_fetch_frame(_fp(x), len(x), _fp(fr), frame_len, hop, index, center, w)
+        return st, fr
+
+    def overlap_add(self, frame, out, hop, index):
+        """out (float32, modified in place) += frame at index*hop -> status"""
+        self._framing_setup()
+        frame = np.ascontiguousarray(frame, np.float32)
+        assert out.dtype == np.float32 and out.flags.c_contiguous
+        return self.lib.vv_dsp_overlap_add(_fp(frame), _fp(out), len(out), len(frame), hop, index)
+
     def hann(self, n):
         w = np.zeros(n, np.float32)
         assert self.lib.vv_dsp_window_hann(n, _fp(w)) == OK
@@ -383,6 +414,27 @@ class Oracle:
         out = np.zeros((log_mel.shape[0], n_coeffs), np.float32)
         assert self.lib.orc_mfcc(_fp(log_mel), log_mel.shape[0], log_mel.shape[1], n_coeffs, lifter, _fp(out)) == 0
         return out
+
+    def get_num_frames(self, n, frame_len, hop, center):
+        L = self.lib
+        L.orc_get_num_frames.argtypes = [C.c_size_t, C.c_size_t, C.c_size_t, C.c_int]
+        L.orc_get_num_frames.restype = C.c_size_t
+        return L.orc_get_num_frames(n, frame_len, hop, center)
+
+    def fetch_frame(self, x, frame_len, hop, index, center, window=None):
+        L = self.lib
+        L.orc_fetch_frame.argtypes = [_f32p, C.c_size_t, _f32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int, _f32p]
+        x = np.ascontiguousarray(x, np.float32)
+        fr = np.zeros(frame_len, np.float32)
+        w = None if window is None else _fp(np.ascontiguousarray(window, np.float32))
+        st = L.orc_fetch_frame(_fp(x), len(x), _fp(fr), frame_len, hop, index, center, w)
+        return st, fr
+
+    def overlap_add(self, frame, out, hop, index):
+        L = self.lib
+        L.orc_overlap_add.argtypes = [_f32p, _f32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t]
+        frame = np.ascontiguousarray(frame, np.float32)
+        return L.orc_overlap_add(_fp(frame), _fp(out), len(out), len(frame), hop, index)
 
     def fir_apply(self, h, x, fft=False):
         h = np.ascontiguousarray(h, np.float32)

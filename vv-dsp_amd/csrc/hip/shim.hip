@@ -802,6 +802,106 @@ int vvhip_hilbert_host(const float* x, size_t n, float* z_out) {
 }
 
 // ---------------------------------------------------------------------------
+// Framing (framing.c:58-146)
+// ---------------------------------------------------------------------------
+int vvhip_fetch_frames_device(const float* d_signal, size_t n, float* d_frames, size_t frame_len, size_t hop,
+                              size_t frame0, size_t count, int center, const float* d_window, void* stream) {
+    if (!d_signal || !d_frames) return ST_NULL;
+    if (n == 0 || frame_len == 0 || hop == 0) return ST_SIZE;
+    HIPCHK(launch_fetch_frames(d_signal, 0, (long long)n, d_frames, (long long)frame_len, (long long)hop,
+                               (long long)frame0, (long long)count, center, d_window, (hipStream_t)stream),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_overlap_add_device(const float* d_frames, size_t count, float* d_out, size_t out_len, size_t frame_len,
+                             size_t hop, size_t frame0, void* stream) {
+    if (!d_frames || !d_out) return ST_NULL;
+    if (out_len == 0 || frame_len == 0 || hop == 0) return ST_SIZE;
+    HIPCHK(launch_overlap_add(d_frames, (long long)count, d_out, (long long)out_len, (long long)frame_len,
+                              (long long)hop, (long long)frame0, (hipStream_t)stream),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+// One frame through the device: only the span of samples the frame reads
+// goes up (for a centred frame near an end, the reflected indices' span).
+int vvhip_fetch_frame_host(const float* signal, size_t n, float* frame, size_t frame_len, size_t hop,
+                           size_t frame_index, int center, const float* window) {
+    if (!signal || !frame) return ST_NULL;
+    if (n == 0 || frame_len == 0 || hop == 0) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    const long long N = (long long)n, L = (long long)frame_len;
+    const long long start = (long long)(frame_index * hop) - (center ? L / 2 : 0);
+    long long lo = N, hi = 0;   // sample span [lo, hi) the frame reads
+    if (center) {
+        for (long long i = 0; i < L; ++i) {
+            const long long k = reflect_sample(start + i, N);
+            lo = k < lo ? k : lo;
+            hi = k + 1 > hi ? k + 1 : hi;
+        }
+    } else {
+        lo = start < 0 ? 0 : (start < N ? start : N);
+        hi = start + L < N ? (start + L > lo ? start + L : lo) : N;
+    }
+    const long long span = hi > lo ? hi - lo : 0;
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), ST_INTERNAL);
+    int st = ST_OK;
+    {
+        Scratch dsig(s), dwin(s), dfr(s);
+        if (dsig.alloc(sizeof(float) * (span > 0 ? span : 1)) != hipSuccess || dfr.alloc(sizeof(float) * L) != hipSuccess ||
+            (window && dwin.alloc(sizeof(float) * L) != hipSuccess)) {
+            st = fail(ST_INTERNAL, "fetch_frame alloc");
+        } else if ((span > 0 && hipMemcpyAsync(dsig.p, signal + lo, sizeof(float) * span, hipMemcpyHostToDevice, s) !=
+                                    hipSuccess) ||
+                   (window && hipMemcpyAsync(dwin.p, window, sizeof(float) * L, hipMemcpyHostToDevice, s) != hipSuccess)) {
+            st = fail(ST_INTERNAL, "fetch_frame h2d");
+        } else if (launch_fetch_frames((const float*)dsig.p, lo, N, (float*)dfr.p, L, (long long)hop,
+                                       (long long)frame_index, 1, center, window ? (const float*)dwin.p : nullptr,
+                                       s) != hipSuccess ||
+                   hipMemcpyAsync(frame, dfr.p, sizeof(float) * L, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                   hipStreamSynchronize(s) != hipSuccess) {
+            st = fail(ST_INTERNAL, "fetch_frame run");
+        }
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+// One frame added into out[s0, s0 + frame_len) (clipped to out_len) on the device.
+int vvhip_overlap_add_host(const float* frame, float* out, size_t out_len, size_t frame_len, size_t hop,
+                           size_t frame_index) {
+    if (!frame || !out) return ST_NULL;
+    if (out_len == 0 || frame_len == 0 || hop == 0) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    const size_t s0 = frame_index * hop;
+    if (s0 >= out_len) return ST_OK;   // nothing lands inside the output (framing.c:137-144)
+    const size_t span = out_len - s0 < frame_len ? out_len - s0 : frame_len;
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), ST_INTERNAL);
+    int st = ST_OK;
+    {
+        Scratch dfr(s), dout(s);
+        if (dfr.alloc(sizeof(float) * frame_len) != hipSuccess || dout.alloc(sizeof(float) * span) != hipSuccess) {
+            st = fail(ST_INTERNAL, "overlap_add alloc");
+        } else if (hipMemcpyAsync(dfr.p, frame, sizeof(float) * frame_len, hipMemcpyHostToDevice, s) != hipSuccess ||
+                   hipMemcpyAsync(dout.p, out + s0, sizeof(float) * span, hipMemcpyHostToDevice, s) != hipSuccess) {
+            st = fail(ST_INTERNAL, "overlap_add h2d");
+        } else if (launch_overlap_add((const float*)dfr.p, 1, (float*)dout.p, (long long)span, (long long)frame_len,
+                                      (long long)hop, 0, s) != hipSuccess ||
+                   hipMemcpyAsync(out + s0, dout.p, sizeof(float) * span, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                   hipStreamSynchronize(s) != hipSuccess) {
+            st = fail(ST_INTERNAL, "overlap_add run");
+        }
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+// ---------------------------------------------------------------------------
 // DCT
 // ---------------------------------------------------------------------------
 int vvhip_dct_device(const float* d_in, float* d_out, size_t n, size_t batch, int type, int dir,

@@ -48,6 +48,13 @@ int mel_chunk_schedule(const int* meta, int n_mels, std::vector<int>* chunks, st
 // with nothing to write, in kernels that hand-count their memory operations.
 constexpr size_t SINK_FLOATS = 1u << 18;   // 1 MiB = 4096 waves x 64 lanes
 float* store_sink();
+// ---- batched framing (framing_kernels.hip), framing.c:58-146 semantics
+long long reflect_sample(long long idx, long long n);   // framing.c:21-56, host side (span bounds)
+hipError_t launch_fetch_frames(const float* sig, long long base, long long n, float* out, long long len,
+                               long long hop, long long frame0, long long count, int center, const float* win,
+                               hipStream_t s);
+hipError_t launch_overlap_add(const float* frames, long long count, float* out, long long out_len, long long len,
+                              long long hop, long long frame0, hipStream_t s);
 
 // Persistent-grid sizing: resident blocks for `kernel` x CUs, capped by work.
 // CUs x resident workgroups of `kernel` (capped at max_per_cu when > 0), at most work_blocks
