@@ -372,26 +372,30 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                     st4_nt_sbase<I>(off, val, base);
                 }
             };
-            static_for<0, J>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                static_for<0, R>([&](auto rc) {
-                    constexpr int r = decltype(rc)::value;
-                    constexpr int IE = 4 * (T * j + r * NB), IO = 4 * ((R - 1 - r) * NB - T * j);
-                    st(std::integral_constant<int, IE>{}, ve, ea[j][r], ra);
-                    st(std::integral_constant<int, IE>{}, ve, eb[j][r], rb);
-                    float oa, ob;
-                    if constexpr (j + 1 < J) {
-                        oa = t == 0 ? ea[j + 1][r] : ea[j][r];
-                        ob = t == 0 ? eb[j + 1][r] : eb[j][r];
-                    } else {
-                        oa = t == 0 ? sa[r] : ea[j][r];
-                        ob = t == 0 ? sb[r] : eb[j][r];
-                    }
-                    // mirror block: bins IO/4 + NB - 64 .. IO/4 + NB - 1
-                    st(std::integral_constant<int, IO + 4 * (NB - T)>{}, vo - 4u * (NB - T), oa, ra);
-                    st(std::integral_constant<int, IO + 4 * (NB - T)>{}, vo - 4u * (NB - T), ob, rb);
+            // The N/T blocks of a row in ascending address order, row a then
+            // row b (measured 0.5 % faster than interleaving the rows).  Block
+            // m is an even block (slot j = m % (NB/T) < J, r = m / (NB/T)) or
+            // the mirror block of (j, r) with (N/T - 1) - m = r (NB/T) + j.
+            auto val = [&](auto mc, const float (&e)[J][R], const float (&sp)[R]) -> float {
+                constexpr int m = decltype(mc)::value;
+                constexpr int je = m % (NB / T), re = m / (NB / T);
+                if constexpr (je < J) {
+                    return e[je][re];
+                } else {
+                    constexpr int mm = (N / T - 1) - m, rm = mm / (NB / T), jm = mm % (NB / T);
+                    if constexpr (jm + 1 < J) return t == 0 ? e[jm + 1][rm] : e[jm][rm];
+                    else return t == 0 ? sp[rm] : e[jm][rm];
+                }
+            };
+            auto row = [&](const float (&e)[J][R], const float (&sp)[R], const void* base) {
+                static_for<0, N / T>([&](auto mc) {
+                    constexpr int m = decltype(mc)::value;
+                    if constexpr (m % (NB / T) < J) st(std::integral_constant<int, 4 * T * m>{}, ve, val(mc, e, sp), base);
+                    else st(std::integral_constant<int, 4 * T * m>{}, vo - 4u * (NB - T), val(mc, e, sp), base);
                 });
-            });
+            };
+            row(ea, sa, ra);
+            row(eb, sb, rb);
             if constexpr (MODE == 2) {
                 // bin N/2 = NB * (R/2): even slot j = 0, r = R/2, lane 0; the
                 // other lanes' copies go to the sink (one store per row, counted)

@@ -14,7 +14,7 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libvvdsp_amd.so")
+LIB_PATH = os.environ.get("VVDSP_AMD_LIB") or os.path.join(HERE, "lib", "libvvdsp_amd.so")   # override: A/B builds
 
 OK = 0
 C2C, R2C, C2R = 0, 1, 2
