@@ -94,8 +94,8 @@ hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long lon
         const float2* pas = pass_twiddles(NN);                                                              \
         if (!tab || !pas) return hipErrorOutOfMemory;                                                       \
         constexpr int WG = Wg<NN>::value, F = Wg<NN>::F;                                                    \
-        static int cap = 0;                                                                                 \
-        if (!cap) cap = persistent_grid((const void*)k_hilbert_pair<NN>, WG, 0, 1LL << 40);                 \
+        static std::atomic<int> capc;                                                                                 \
+        const int cap = cached_grid(capc, (const void*)k_hilbert_pair<NN>, WG, 0, 1LL << 40);                 \
         const long long need = ((batch + 1) / 2 + F - 1) / F;                                               \
         const int grid = (int)(need < cap ? need : cap);                                                    \
         hipLaunchKernelGGL(k_hilbert_pair<NN>, dim3(grid), dim3(WG), 0, s, x, z, batch, n, n, pas, tab);    \
@@ -221,8 +221,8 @@ hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long ba
         const float2* pas = pass_twiddles(NN);                                                               \
         if (!tab || !pas) return hipErrorOutOfMemory;                                                        \
         constexpr int WG = Wg<NN>::value, F = Wg<NN>::F;                                                     \
-        static int cap = 0;                                                                                  \
-        if (!cap) cap = persistent_grid((const void*)k_dct2_pair<NN, 0>, WG, 0, 1LL << 40);                  \
+        static std::atomic<int> capc;                                                                                  \
+        const int cap = cached_grid(capc, (const void*)k_dct2_pair<NN, 0>, WG, 0, 1LL << 40);                  \
         const long long need = ((batch + 1) / 2 + F - 1) / F;                                                \
         const int grid = (int)(need < cap ? need : cap);                                                     \
         if (policy == 1)                                                                                     \

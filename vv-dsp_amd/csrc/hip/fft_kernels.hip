@@ -70,8 +70,8 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     const float2* pas = pass_twiddles(N);
     if (!tab || !pas) return hipErrorOutOfMemory;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
-    static int grid_cap = 0;
-    if (!grid_cap) grid_cap = persistent_grid((const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
+    static std::atomic<int> capc;
+    const int grid_cap = cached_grid(capc, (const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;
     const int grid = (int)(need < grid_cap ? need : grid_cap);
     if (grid < 1) return hipSuccess;
@@ -236,11 +236,11 @@ static hipError_t run_r2c(const float* in, float2* out, long long batch, long lo
     const float2* t2M = twiddle_table(2 * M);
     if (!tM || !t2M || !pM) return hipErrorOutOfMemory;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
-    static int cap = 0;
+    static std::atomic<int> capc;
     // one resident workgroup per CU: measured 15-20 % faster than the 3 the
     // LDS/VGPR budget allows (the partial-line n/2+1 rows combine better with
     // fewer concurrent writers; profiles/r01_kbench_occupancy.jsonl)
-    if (!cap) cap = persistent_grid((const void*)k_r2c<M>, WG, 0, 1LL << 40, 1);
+    const int cap = cached_grid(capc, (const void*)k_r2c<M>, WG, 0, 1LL << 40, 1);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < cap ? need : cap);
     if (grid < 1) return hipSuccess;
@@ -256,8 +256,8 @@ static hipError_t run_c2r(const float2* in, float* out, long long batch, long lo
     const float2* t2M = twiddle_table(2 * M);
     if (!tM || !t2M || !pM) return hipErrorOutOfMemory;
     constexpr int WG = Wg<M>::value, F = Wg<M>::F;
-    static int cap = 0;
-    if (!cap) cap = persistent_grid((const void*)k_c2r<M>, WG, 0, 1LL << 40);
+    static std::atomic<int> capc;
+    const int cap = cached_grid(capc, (const void*)k_c2r<M>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < cap ? need : cap);
     if (grid < 1) return hipSuccess;

@@ -331,13 +331,13 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     // below (2q+2)*lout without bounds checks: verify the range on the host
     if (ql > qf && (2 * qf * lout < le || 2 * ql * lout > n || N + lout > N + (3 * N) / 4))
         return hipErrorInvalidValue;
-    static int cap_b = 0, cap_e = 0, cap_v2 = 0;
+    static std::atomic<int> capc_b, capc_e, capc_v2;
     const char* eo = getenv("VVHIP_FIR_OLD");   // A/B switch (scripts/kbench.py), read per call
     const bool old = eo && *eo == '1';
     // le == N/4 holds for every filter fir_block gives N = 1024 (taps <= 257)
     if (ql > qf && le == N / 4 && !old) {
         if constexpr (FIR_BULK<N>) {
-            if (!cap_v2) cap_v2 = persistent_grid((const void*)k_fir_bulk<N, true>, 256, 0, 1LL << 40);
+            const int cap_v2 = cached_grid(capc_v2, (const void*)k_fir_bulk<N, true>, 256, 0, 1LL << 40);
             const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
             const int grid = (int)(need < cap_v2 ? need : cap_v2);
             hipLaunchKernelGGL((k_fir_bulk<N, true>), dim3(grid), dim3(256), 0, s, le, H, x, y, nch, x_stride,
@@ -345,7 +345,7 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
         }
     } else if (ql > qf) {
         if constexpr (FIR_BULK<N>) {
-            if (!cap_b) cap_b = persistent_grid((const void*)k_fir_pair<N, true>, WG, 0, 1LL << 40);
+            const int cap_b = cached_grid(capc_b, (const void*)k_fir_pair<N, true>, WG, 0, 1LL << 40);
             const long long cnt = ql - qf, need = (nch * cnt + F - 1) / F;
             const int grid = (int)(need < cap_b ? need : cap_b);   // persistent (chunked launches measured slower)
             hipLaunchKernelGGL((k_fir_pair<N, true>), dim3(grid), dim3(WG), 0, s, lm1, le, H, x, y, n, nch,
@@ -354,7 +354,7 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     }
     const long long ecnt = qf + (ppc - ql);   // edge pairs per channel: [0, qf) and [ql, ppc)
     if (ecnt > 0) {
-        if (!cap_e) cap_e = persistent_grid((const void*)k_fir_pair<N, false>, WG, 0, 1LL << 40);
+        const int cap_e = cached_grid(capc_e, (const void*)k_fir_pair<N, false>, WG, 0, 1LL << 40);
         const long long need = (nch * ecnt + F - 1) / F;
         const int grid = (int)(need < cap_e ? need : cap_e);
         hipLaunchKernelGGL((k_fir_pair<N, false>), dim3(grid), dim3(WG), 0, s, lm1, le, H, x, y, n, nch,

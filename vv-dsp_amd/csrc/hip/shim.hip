@@ -634,11 +634,13 @@ struct vvhip_fir {
 // VVHIP_FIR_BLOCK overrides the preferred size.  0 = no OLS block (long
 // filters use the direct form).
 static size_t fir_block(const vvhip_fir* f, size_t n) {
-    static size_t pref = 0;
+    static std::atomic<size_t> pref_cache{0};   // read once; concurrent first calls agree
+    size_t pref = pref_cache.load(std::memory_order_relaxed);
     if (!pref) {
         const char* e = getenv("VVHIP_FIR_BLOCK");
         pref = e ? (size_t)atol(e) : 1024;
         if (pref < 64 || pref > 8192 || (pref & (pref - 1))) pref = 1024;
+        pref_cache.store(pref, std::memory_order_relaxed);
     }
     const size_t lm1 = f->taps - 1;
     size_t nr = 64;

@@ -578,7 +578,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         long long mpc = (nfull < frames ? nfull : frames) / 2;
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
-        static int cap[3] = {0, 0, 0};
+        static std::atomic<int> capc[3];   // zero-initialised (static storage)
         // The bulk launch is NOT persistent: one workgroup per `cps` pairs per
         // transform slot, so the hardware dispatcher balances the CUs and the
         // launch has no straggler tail (measured 8-13 % faster than the
@@ -587,15 +587,15 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // resident workgroup slots once (one round, every wave pipelining its
         // pairs) instead of a few long chains or several short rounds.
         const long long bulk_pairs = nch * ppc;
-        if (!cap[0]) cap[0] = persistent_grid((const void*)k_stft_pair<N, MODE, 0>, WG, 0, 1LL << 40);
-        long long cps = (bulk_pairs + (long long)F * cap[0] - 1) / ((long long)F * cap[0]);
+        const int cap0 = cached_grid(capc[0], (const void*)k_stft_pair<N, MODE, 0>, WG, 0, 1LL << 40);
+        long long cps = (bulk_pairs + (long long)F * cap0 - 1) / ((long long)F * cap0);
         cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
         float* sink = store_sink();
         if (!sink) return hipErrorOutOfMemory;
         auto launch = [&](auto kern, int var, long long pair0, long long cnt) {
-            if (!cap[var]) cap[var] = persistent_grid((const void*)kern, WG, 0, 1LL << 40);
+            const int capv = cached_grid(capc[var], (const void*)kern, WG, 0, 1LL << 40);
             const long long need = (nch * cnt + F - 1) / F;
-            long long grid = need < cap[var] ? need : cap[var];
+            long long grid = need < capv ? need : capv;
             long long chunk = 0;
             if (var == 0) {
                 chunk = cps * F;
@@ -636,8 +636,8 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const float2* t2M = twiddle_table(N);
         if (!tM || !pM || !t2M) return hipErrorOutOfMemory;
         constexpr int WG = Wg<M>::value, F = Wg<M>::F;
-        static int cap = 0;
-        if (!cap) cap = persistent_grid((const void*)k_stft_half<M, MODE>, WG, 0, 1LL << 40);
+        static std::atomic<int> capc1;
+        const int cap = cached_grid(capc1, (const void*)k_stft_half<M, MODE>, WG, 0, 1LL << 40);
         const long long need = (items + F - 1) / F;
         const int grid = (int)(need < cap ? need : cap);
         if (grid < 1) return hipSuccess;

@@ -137,11 +137,12 @@ const float2* pass_twiddles(int n) {
 }
 
 int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks, int max_per_cu) {
-    static int cus = 0;
+    static std::atomic<int> cus_cache{0};
+    int cus = cus_cache.load(std::memory_order_relaxed);
     if (cus == 0) {
-        int dev = current_device();
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, current_device());
         if (cus <= 0) cus = 256;
+        cus_cache.store(cus, std::memory_order_relaxed);
     }
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess ||

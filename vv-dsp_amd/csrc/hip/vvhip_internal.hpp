@@ -2,6 +2,7 @@
 // and the extern "C" shim (shim.hip).  Not part of the public C ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <vector>
@@ -59,6 +60,17 @@ hipError_t launch_overlap_add(const float* frames, long long count, float* out, 
 // Persistent-grid sizing: resident blocks for `kernel` x CUs, capped by work.
 // CUs x resident workgroups of `kernel` (capped at max_per_cu when > 0), at most work_blocks
 int persistent_grid(const void* kernel, int block, size_t dyn_lds, long long work_blocks, int max_per_cu = 0);
+// persistent_grid computed once per call site (a launcher's static cache);
+// concurrent first calls compute the same value, the atomic keeps that race-free
+inline int cached_grid(std::atomic<int>& cache, const void* kernel, int block, size_t dyn_lds, long long work_blocks,
+                       int max_per_cu = 0) {
+    int g = cache.load(std::memory_order_relaxed);
+    if (g == 0) {
+        g = persistent_grid(kernel, block, dyn_lds, work_blocks, max_per_cu);
+        cache.store(g, std::memory_order_relaxed);
+    }
+    return g;
+}
 
 // ---- pow2 register/LDS FFTs (fft_kernels.hip) -----------------------------
 bool c2c_supported(long long n);           // pow2, 2..4096
