@@ -807,6 +807,7 @@ k_istft(const float2* __restrict__ spec, long long count, int hop, int K, const 
     const long long bend = fb == count ? count + K - 1 : fb;   // blocks this workgroup writes: [fa, bend)
     const long long g0 = fa - (K - 1);
     const float sc = 0.5f / (float)N;   // Hermitian half and the backward 1/N, exact (powers of two)
+    const int lh = 31 - __builtin_clz((unsigned)hop);   // hop is a power of two (istft_fused_supported)
     float* my = stage + 2 * wv * N;
     for (long long g = g0; g < fb; g += 8) {
         // ---- two frames per wave: Z = Ha + i Hb, inverse FFT, window -> stage
@@ -847,16 +848,22 @@ k_istft(const float2* __restrict__ spec, long long count, int hop, int K, const 
         }
         __syncthreads();
         // ---- combine: sum of block b's contributions of this step's frames, in frame order
-        auto combine = [&](long long b, int j, float acc, float nacc, float* acc_o, float* nacc_o) {
-            const long long i = b * hop + j;
-            long long flo = b - K + 1;
-            if (flo < g) flo = g;
-            if (flo < 0) flo = 0;
-            long long fhi = b < g + 7 ? b : g + 7;
-            if (fhi > fb - 1) fhi = fb - 1;
-            for (long long f = flo; f <= fhi; ++f) {
-                const int e = (int)(i - f * hop);
-                acc += stage[(f - g) * N + e];
+        // ---- combine: sum of block b's contributions of this step's frames, in
+        // frame order.  All per-sample index math is 32-bit and relative to the
+        // step (block bb = b - g, frame r = f - g; hop is a power of two), with
+        // the 64-bit bounds folded into uniform per-step limits.
+        auto clampi = [](long long v) { return (int)(v < -(1LL << 30) ? -(1LL << 30) : (v > (1LL << 30) ? (1LL << 30) : v)); };
+        const long long gh = g * hop;                           // sample index of block g
+        const int rflo = g < 0 ? (int)(-g) : 0;                  // frames f >= 0
+        const int rfhi = (int)(fb - 1 - g < 7 ? fb - 1 - g : 7);   // frames f < fb of this step
+        const int bb_fa = clampi(fa - g), bb_bend = clampi(bend - g), bb_tot = clampi(count + K - 1 - g);
+        auto combine = [&](int bb, int j, float acc, float nacc, float* acc_o, float* nacc_o) {
+            int rlo = bb - K + 1;
+            if (rlo < rflo) rlo = rflo;
+            const int rhi = bb < rfhi ? bb : rfhi;
+            for (int r = rlo; r <= rhi; ++r) {
+                const int e = ((bb - r) << lh) + j;
+                acc += stage[r * N + e];
                 const float w = lwin[e];
                 float w2 = w * w;
                 asm volatile("" : "+v"(w2));   // no FMA: w*w rounded, then added (stft.c)
@@ -865,31 +872,29 @@ k_istft(const float2* __restrict__ spec, long long count, int hop, int K, const 
             *acc_o = acc;
             *nacc_o = nacc;
         };
-        const long long total_blocks = count + K - 1;
         for (int idx = tid; idx < 8 * hop; idx += 256) {   // phase A: blocks [g, g+8) become final
-            const long long b = g + idx / hop;
-            const int j = idx % hop;
-            if (b < fa || b >= bend || b >= total_blocks) continue;
-            const bool fresh = g == g0 || b >= g + K - 1;
-            const float a0 = fresh ? out_add[b * hop + j] : carry[(b - g) * hop + j];
-            const float n0 = norm_add ? (fresh ? norm_add[b * hop + j] : ncarry[(b - g) * hop + j]) : 0.0f;
+            const int bb = idx >> lh, j = idx & (hop - 1);   // idx = bb * hop + j
+            if (bb < bb_fa || bb >= bb_bend || bb >= bb_tot) continue;
+            const bool fresh = g == g0 || bb >= K - 1;
+            const float a0 = fresh ? out_add[gh + idx] : carry[idx];
+            const float n0 = norm_add ? (fresh ? norm_add[gh + idx] : ncarry[idx]) : 0.0f;
             float acc, nacc;
-            combine(b, j, a0, n0, &acc, &nacc);
-            out_add[b * hop + j] = acc;
-            if (norm_add) norm_add[b * hop + j] = nacc;
+            combine(bb, j, a0, n0, &acc, &nacc);
+            out_add[gh + idx] = acc;
+            if (norm_add) norm_add[gh + idx] = nacc;
         }
         __syncthreads();   // phase A's carry reads before phase B's carry writes
         const bool last = g + 8 >= fb;
+        const long long gh8 = gh + 8LL * hop;
         for (int idx = tid; idx < (K - 1) * hop; idx += 256) {   // phase B: blocks [g+8, g+8+K-1), fresh
-            const long long b = g + 8 + idx / hop;
-            const int j = idx % hop;
-            if (b >= total_blocks) continue;
+            const int bb = 8 + (idx >> lh), j = idx & (hop - 1);
+            if (bb >= bb_tot) continue;
             float acc, nacc;
-            combine(b, j, out_add[b * hop + j], norm_add ? norm_add[b * hop + j] : 0.0f, &acc, &nacc);
+            combine(bb, j, out_add[gh8 + idx], norm_add ? norm_add[gh8 + idx] : 0.0f, &acc, &nacc);
             if (last) {
-                if (b >= fa && b < bend) {
-                    out_add[b * hop + j] = acc;
-                    if (norm_add) norm_add[b * hop + j] = nacc;
+                if (bb >= bb_fa && bb < bb_bend) {
+                    out_add[gh8 + idx] = acc;
+                    if (norm_add) norm_add[gh8 + idx] = nacc;
                 }
             } else {
                 carry[idx] = acc;   // = (b - (g+8)) * hop + j: next step's base
@@ -901,7 +906,7 @@ k_istft(const float2* __restrict__ spec, long long count, int hop, int K, const 
 }
 
 bool istft_fused_supported(long long nfft, long long hop) {
-    return nfft == 1024 && hop >= 256 && nfft % hop == 0;   // K = nfft/hop <= 4
+    return nfft == 1024 && hop >= 256 && nfft % hop == 0 && (hop & (hop - 1)) == 0;   // K = nfft/hop <= 4
 }
 
 hipError_t launch_istft_fused(long long nfft, long long hop, const float2* spec, long long count,
