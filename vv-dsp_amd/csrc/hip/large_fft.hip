@@ -163,11 +163,13 @@ k_fs_cols(const float2* __restrict__ in, float2* __restrict__ out, int N2, int c
     }
 }
 
-// Rows pass: X[b][k1 + N1 k2] = scale * FFT_N2(Y[b][k1][.])[k2]
+// Rows pass: X[b][k1 + N1 k2] = scale * FFT_N2(Y[b][k1][.])[k2], times mulv[k1 + N1 k2]
+// when mulv is given (Bluestein's pointwise product with the chirp spectrum,
+// the same n-vector for every transform of the batch)
 template <int N2, int G, bool RI, bool FWD>
 __global__ void __launch_bounds__(G * Geo<N2>::T)
 k_fs_rows(const float2* __restrict__ in, float2* __restrict__ out, int N1, int rpb, const float2* gpass,
-          const float2* gtab, float scale) {
+          const float2* gtab, float scale, const float2* __restrict__ mulv) {
     using Ge = Geo<N2>;
     using F = FsGeo<N2, G, RI>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[F::LDS_BYTES];
@@ -188,7 +190,9 @@ k_fs_rows(const float2* __restrict__ in, float2* __restrict__ out, int N1, int r
 #pragma unroll
     for (int q = 0; q < Ge::P; ++q) {
         const int k2 = out_pos<N2>(t2, q);
-        st_nt(FWD ? v[q] : cscale(v[q], scale), dst + (long long)k2 * N1);
+        float2 x = FWD ? v[q] : cscale(v[q], scale);
+        if (mulv) x = cmul(x, mulv[r0 + j2 + k2 * N1]);
+        st_nt(x, dst + (long long)k2 * N1);
     }
 }
 
@@ -210,7 +214,8 @@ hipError_t fs_cols_g(const float2* in, float2* out, int N2, long long batch, con
 }
 
 template <int N, int G, bool RI, bool FWD>
-hipError_t fs_rows_g(const float2* in, float2* out, int N1, long long batch, float scale, hipStream_t s) {
+hipError_t fs_rows_g(const float2* in, float2* out, int N1, long long batch, float scale, const float2* mulv,
+                     hipStream_t s) {
     const float2* tab = twiddle_table(N);
     const float2* pas = pass_twiddles(N);
     if (!tab || !pas) return hipErrorOutOfMemory;
@@ -218,7 +223,7 @@ hipError_t fs_rows_g(const float2* in, float2* out, int N1, long long batch, flo
     const long long blocks = (long long)rpb * batch;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_fs_rows<N, G, RI, FWD>), dim3((unsigned)blocks), dim3(FsGeo<N, G, RI>::THREADS), 0, s, in,
-                       out, N1, rpb, pas, tab, scale);
+                       out, N1, rpb, pas, tab, scale, mulv);
     return hipGetLastError();
 }
 
@@ -234,12 +239,13 @@ hipError_t fs_cols(int var, const float2* in, float2* out, int N2, long long bat
 }
 
 template <int N, bool FWD>
-hipError_t fs_rows(int var, const float2* in, float2* out, int N1, long long batch, float scale, hipStream_t s) {
+hipError_t fs_rows(int var, const float2* in, float2* out, int N1, long long batch, float scale, const float2* mulv,
+                   hipStream_t s) {
     switch (var) {
-        case 1: return fs_rows_g<N, 16, false, FWD>(in, out, N1, batch, scale, s);
-        case 2: return fs_rows_g<N, 8, false, FWD>(in, out, N1, batch, scale, s);
-        case 3: return fs_rows_g<N, 8, true, FWD>(in, out, N1, batch, scale, s);
-        default: return fs_rows_g<N, 16, true, FWD>(in, out, N1, batch, scale, s);
+        case 1: return fs_rows_g<N, 16, false, FWD>(in, out, N1, batch, scale, mulv, s);
+        case 2: return fs_rows_g<N, 8, false, FWD>(in, out, N1, batch, scale, mulv, s);
+        case 3: return fs_rows_g<N, 8, true, FWD>(in, out, N1, batch, scale, mulv, s);
+        default: return fs_rows_g<N, 16, true, FWD>(in, out, N1, batch, scale, mulv, s);
     }
 }
 
@@ -258,13 +264,13 @@ hipError_t fs_cols_any(int N1, int var, const float2* in, float2* out, int N2, l
 
 template <bool FWD>
 hipError_t fs_rows_any(int N2, int var, const float2* in, float2* out, int N1, long long batch, float scale,
-                       hipStream_t s) {
+                       const float2* mulv, hipStream_t s) {
     switch (N2) {
-        case 64: return fs_rows<64, FWD>(var, in, out, N1, batch, scale, s);
-        case 128: return fs_rows<128, FWD>(var, in, out, N1, batch, scale, s);
-        case 256: return fs_rows<256, FWD>(var, in, out, N1, batch, scale, s);
-        case 512: return fs_rows<512, FWD>(var, in, out, N1, batch, scale, s);
-        case 1024: return fs_rows<1024, FWD>(var, in, out, N1, batch, scale, s);
+        case 64: return fs_rows<64, FWD>(var, in, out, N1, batch, scale, mulv, s);
+        case 128: return fs_rows<128, FWD>(var, in, out, N1, batch, scale, mulv, s);
+        case 256: return fs_rows<256, FWD>(var, in, out, N1, batch, scale, mulv, s);
+        case 512: return fs_rows<512, FWD>(var, in, out, N1, batch, scale, mulv, s);
+        case 1024: return fs_rows<1024, FWD>(var, in, out, N1, batch, scale, mulv, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -276,7 +282,7 @@ long long env_ll(const char* name, long long dflt) {
 
 // n = N1*N2, 64 <= N1 <= N2 <= 1024
 hipError_t launch_c2c_twopass(long long n, int lg, int fwd, const float2* in, float2* out, long long batch,
-                              hipStream_t s) {
+                              hipStream_t s, const float2* mulv = nullptr) {
     const int N1 = 1 << (lg / 2), N2 = (int)(n / N1);
     int lo_bits = 0;
     const float2* split = twiddle_split(n, &lo_bits);
@@ -298,8 +304,8 @@ hipError_t launch_c2c_twopass(long long n, int lg, int fwd, const float2* in, fl
         e = fwd ? fs_cols_any<true>(N1, var, src, y, N2, nb, split, lo_bits, s)
                 : fs_cols_any<false>(N1, var, src, y, N2, nb, split, lo_bits, s);
         if (e == hipSuccess)
-            e = fwd ? fs_rows_any<true>(N2, var, y, dst, N1, nb, scale, s)
-                    : fs_rows_any<false>(N2, var, y, dst, N1, nb, scale, s);
+            e = fwd ? fs_rows_any<true>(N2, var, y, dst, N1, nb, scale, mulv, s)
+                    : fs_rows_any<false>(N2, var, y, dst, N1, nb, scale, mulv, s);
     }
     (void)hipFreeAsync(y, s);
     return e;
@@ -525,9 +531,15 @@ hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, f
         hipLaunchKernelGGL(k_bluestein_pre, dim3(grid_for(total)), dim3(256), 0, s, in, real_in, in_dist, p->chirp, u,
                            n, M, total);
         if ((e = hipGetLastError()) != hipSuccess) break;
-        if ((e = fft_pow2(M, 1, u, U, batch, s)) != hipSuccess) break;
-        hipLaunchKernelGGL(k_mul_bcast, dim3(grid_for(total)), dim3(256), 0, s, U, p->V, M, total);
-        if ((e = hipGetLastError()) != hipSuccess) break;
+        // FFT(u) * V: fused into the rows pass when M runs two-pass (8192..2^20)
+        const int lgM = ilog2((int)(M < (1LL << 30) ? M : (1LL << 30)));
+        if (!c2c_supported(M) && lgM <= 20 && env_ll("VVHIP_FS_OLD", 0) == 0 && env_ll("VVHIP_BLUE_UNFUSED", 0) == 0) {
+            if ((e = launch_c2c_twopass(M, lgM, 1, u, U, batch, s, p->V)) != hipSuccess) break;
+        } else {
+            if ((e = fft_pow2(M, 1, u, U, batch, s)) != hipSuccess) break;
+            hipLaunchKernelGGL(k_mul_bcast, dim3(grid_for(total)), dim3(256), 0, s, U, p->V, M, total);
+            if ((e = hipGetLastError()) != hipSuccess) break;
+        }
         if ((e = fft_pow2(M, 0, U, u, batch, s)) != hipSuccess) break;   // includes 1/M
         const long long tot_out = nout * batch;
         hipLaunchKernelGGL(k_bluestein_post, dim3(grid_for(tot_out)), dim3(256), 0, s, u, p->chirp, out, M, nout,
