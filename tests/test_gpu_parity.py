@@ -175,6 +175,36 @@ def test_large_pow2_chunked_batch(vdev, n, b, chunk_mb):
         assert _normwise(yb[i], np.fft.ifft(x64[i])) <= 2e-6, i
 
 
+@pytest.mark.parametrize("n,b", [(48000, 3), (3000, 5), (100003, 2)])
+def test_bluestein_fused_equals_unfused(vdev, n, b):
+    """The fused Bluestein chain (chirp pre-multiply in the columns pass, the
+    product with V and the post-multiply in the rows passes) performs the same
+    f32 operations as the separate-kernel chain: bit-identical outputs, for
+    complex input both ways and for real input (R2C, n/2+1 bins), batched."""
+    import os
+    import torch
+    rng = np.random.default_rng(n + b)
+    xc = torch.from_numpy((rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)).cuda()
+    xr = torch.from_numpy((rng.random((b, n)) - 0.5).astype(np.float32)).cuda()
+
+    def run():
+        return [vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xc).cpu().numpy(),
+                vdev.FftPlan(n, vdev.C2C, vdev.BWD, batch=b)(xc).cpu().numpy(),
+                vdev.FftPlan(n, vdev.R2C, vdev.FWD, batch=b)(xr).cpu().numpy()]
+    fused = run()
+    old = os.environ.get("VVHIP_BLUE_UNFUSED", "")
+    os.environ["VVHIP_BLUE_UNFUSED"] = "1"
+    try:
+        unfused = run()
+    finally:
+        os.environ["VVHIP_BLUE_UNFUSED"] = old
+    for f, u in zip(fused, unfused):
+        assert np.array_equal(f, u)
+    assert fused[2].shape == (b, n // 2 + 1)
+    ref = np.fft.fft(xc.cpu().numpy().astype(np.complex128), axis=1)
+    assert _normwise(fused[0], ref) <= 2e-6
+
+
 def test_impulse_known_answer(amd):
     """tests/fft_backend_tests.c:70-99 and spectral_tests.c:14-35 of the reference."""
     for n in (8, 16, 1024):

@@ -124,11 +124,29 @@ struct FsChain {
     }
 };
 
+// Optional fused element-wise stages of the two passes (Bluestein, below):
+//   pre  (columns pass input):  x[m] = m < nsig ? raw[b*in_dist + m] * pre_chirp[m] : 0
+//   mulv (rows pass output):    X[k] *= mulv[k]
+//   post (rows pass output):    post_out[b*out_dist + k] = post_scale * post_chirp[k] * X[k], k < nout
+// b counts from b0 (the chunk's first transform).  All null: the plain FFT.
+struct FsHooks {
+    const float2* mulv = nullptr;
+    const float2* pre_chirp = nullptr;
+    const void* raw = nullptr;
+    long long in_dist = 0, nsig = 0;
+    int real_in = 0;
+    const float2* post_chirp = nullptr;
+    float2* post_out = nullptr;
+    long long out_dist = 0, nout = 0;
+    float post_scale = 1.0f;
+    long long b0 = 0;
+};
+
 // Columns pass: Y[b][k1][n2] = W_n^(+-n2 k1) * FFT_N1(x[b][.][n2])[k1]
 template <int N1, int G, bool RI, bool FWD>
 __global__ void __launch_bounds__(G * Geo<N1>::T)
 k_fs_cols(const float2* __restrict__ in, float2* __restrict__ out, int N2, int cpb, const float2* gpass,
-          const float2* gtab, const float2* __restrict__ split, int lo_bits) {
+          const float2* gtab, const float2* __restrict__ split, int lo_bits, FsHooks hk) {
     using Ge = Geo<N1>;
     using F = FsGeo<N1, G, RI>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[F::LDS_BYTES];
@@ -143,10 +161,25 @@ k_fs_cols(const float2* __restrict__ in, float2* __restrict__ out, int N2, int c
     }
     const long long b = blockIdx.x / cpb;
     const int col = (blockIdx.x % cpb) * G + (int)(threadIdx.x % G), t = threadIdx.x / G;
-    const float2* src = in + b * n + col;
     float2 v[Ge::P];
+    if (hk.pre_chirp) {
+        const long long base = (hk.b0 + b) * hk.in_dist;
 #pragma unroll
-    for (int r = 0; r < Ge::P; ++r) v[r] = ld_nt(src + (long long)(t + r * Ge::T) * N2);
+        for (int r = 0; r < Ge::P; ++r) {
+            const long long m = (long long)(t + r * Ge::T) * N2 + col;
+            float2 x = make_float2(0.0f, 0.0f);
+            if (m < hk.nsig) {
+                x = hk.real_in ? make_float2(reinterpret_cast<const float*>(hk.raw)[base + m], 0.0f)
+                               : reinterpret_cast<const float2*>(hk.raw)[base + m];
+                x = cmul(x, hk.pre_chirp[m]);
+            }
+            v[r] = x;
+        }
+    } else {
+        const float2* src = in + b * n + col;
+#pragma unroll
+        for (int r = 0; r < Ge::P; ++r) v[r] = ld_nt(src + (long long)(t + r * Ge::T) * N2);
+    }
     __syncthreads();
     const int j = threadIdx.x % G;
     FsChain<N1, FWD, 0, F::S, RI, false>::run(v, lds, TwTab<N1>{ltab}, j, t, j, t);
@@ -169,7 +202,7 @@ k_fs_cols(const float2* __restrict__ in, float2* __restrict__ out, int N2, int c
 template <int N2, int G, bool RI, bool FWD>
 __global__ void __launch_bounds__(G * Geo<N2>::T)
 k_fs_rows(const float2* __restrict__ in, float2* __restrict__ out, int N1, int rpb, const float2* gpass,
-          const float2* gtab, float scale, const float2* __restrict__ mulv) {
+          const float2* gtab, float scale, FsHooks hk) {
     using Ge = Geo<N2>;
     using F = FsGeo<N2, G, RI>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[F::LDS_BYTES];
@@ -191,8 +224,13 @@ k_fs_rows(const float2* __restrict__ in, float2* __restrict__ out, int N1, int r
     for (int q = 0; q < Ge::P; ++q) {
         const int k2 = out_pos<N2>(t2, q);
         float2 x = FWD ? v[q] : cscale(v[q], scale);
-        if (mulv) x = cmul(x, mulv[r0 + j2 + k2 * N1]);
-        st_nt(x, dst + (long long)k2 * N1);
+        const long long k = r0 + j2 + (long long)k2 * N1;
+        if (hk.mulv) x = cmul(x, hk.mulv[k]);
+        if (hk.post_chirp) {
+            if (k < hk.nout) hk.post_out[(hk.b0 + b) * hk.out_dist + k] = cscale(cmul(x, hk.post_chirp[k]), hk.post_scale);
+        } else {
+            st_nt(x, dst + (long long)k2 * N1);
+        }
     }
 }
 
@@ -201,7 +239,7 @@ namespace {
 // profiles/r01_kbench_fourstep.jsonl); 2 = float2, G 8; 3 = RI, G 8
 template <int N, int G, bool RI, bool FWD>
 hipError_t fs_cols_g(const float2* in, float2* out, int N2, long long batch, const float2* split, int lo_bits,
-                     hipStream_t s) {
+                     const FsHooks& hk, hipStream_t s) {
     const float2* tab = twiddle_table(N);
     const float2* pas = pass_twiddles(N);
     if (!tab || !pas) return hipErrorOutOfMemory;
@@ -209,12 +247,12 @@ hipError_t fs_cols_g(const float2* in, float2* out, int N2, long long batch, con
     const long long blocks = (long long)cpb * batch;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_fs_cols<N, G, RI, FWD>), dim3((unsigned)blocks), dim3(FsGeo<N, G, RI>::THREADS), 0, s, in,
-                       out, N2, cpb, pas, tab, split, lo_bits);
+                       out, N2, cpb, pas, tab, split, lo_bits, hk);
     return hipGetLastError();
 }
 
 template <int N, int G, bool RI, bool FWD>
-hipError_t fs_rows_g(const float2* in, float2* out, int N1, long long batch, float scale, const float2* mulv,
+hipError_t fs_rows_g(const float2* in, float2* out, int N1, long long batch, float scale, const FsHooks& hk,
                      hipStream_t s) {
     const float2* tab = twiddle_table(N);
     const float2* pas = pass_twiddles(N);
@@ -223,54 +261,54 @@ hipError_t fs_rows_g(const float2* in, float2* out, int N1, long long batch, flo
     const long long blocks = (long long)rpb * batch;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_fs_rows<N, G, RI, FWD>), dim3((unsigned)blocks), dim3(FsGeo<N, G, RI>::THREADS), 0, s, in,
-                       out, N1, rpb, pas, tab, scale, mulv);
+                       out, N1, rpb, pas, tab, scale, hk);
     return hipGetLastError();
 }
 
 template <int N, bool FWD>
 hipError_t fs_cols(int var, const float2* in, float2* out, int N2, long long batch, const float2* split, int lo_bits,
-                   hipStream_t s) {
+                   const FsHooks& hk, hipStream_t s) {
     switch (var) {
-        case 1: return fs_cols_g<N, 16, false, FWD>(in, out, N2, batch, split, lo_bits, s);
-        case 2: return fs_cols_g<N, 8, false, FWD>(in, out, N2, batch, split, lo_bits, s);
-        case 3: return fs_cols_g<N, 8, true, FWD>(in, out, N2, batch, split, lo_bits, s);
-        default: return fs_cols_g<N, 16, true, FWD>(in, out, N2, batch, split, lo_bits, s);
+        case 1: return fs_cols_g<N, 16, false, FWD>(in, out, N2, batch, split, lo_bits, hk, s);
+        case 2: return fs_cols_g<N, 8, false, FWD>(in, out, N2, batch, split, lo_bits, hk, s);
+        case 3: return fs_cols_g<N, 8, true, FWD>(in, out, N2, batch, split, lo_bits, hk, s);
+        default: return fs_cols_g<N, 16, true, FWD>(in, out, N2, batch, split, lo_bits, hk, s);
     }
 }
 
 template <int N, bool FWD>
-hipError_t fs_rows(int var, const float2* in, float2* out, int N1, long long batch, float scale, const float2* mulv,
+hipError_t fs_rows(int var, const float2* in, float2* out, int N1, long long batch, float scale, const FsHooks& hk,
                    hipStream_t s) {
     switch (var) {
-        case 1: return fs_rows_g<N, 16, false, FWD>(in, out, N1, batch, scale, mulv, s);
-        case 2: return fs_rows_g<N, 8, false, FWD>(in, out, N1, batch, scale, mulv, s);
-        case 3: return fs_rows_g<N, 8, true, FWD>(in, out, N1, batch, scale, mulv, s);
-        default: return fs_rows_g<N, 16, true, FWD>(in, out, N1, batch, scale, mulv, s);
+        case 1: return fs_rows_g<N, 16, false, FWD>(in, out, N1, batch, scale, hk, s);
+        case 2: return fs_rows_g<N, 8, false, FWD>(in, out, N1, batch, scale, hk, s);
+        case 3: return fs_rows_g<N, 8, true, FWD>(in, out, N1, batch, scale, hk, s);
+        default: return fs_rows_g<N, 16, true, FWD>(in, out, N1, batch, scale, hk, s);
     }
 }
 
 template <bool FWD>
 hipError_t fs_cols_any(int N1, int var, const float2* in, float2* out, int N2, long long batch, const float2* split,
-                       int lo_bits, hipStream_t s) {
+                       int lo_bits, const FsHooks& hk, hipStream_t s) {
     switch (N1) {
-        case 64: return fs_cols<64, FWD>(var, in, out, N2, batch, split, lo_bits, s);
-        case 128: return fs_cols<128, FWD>(var, in, out, N2, batch, split, lo_bits, s);
-        case 256: return fs_cols<256, FWD>(var, in, out, N2, batch, split, lo_bits, s);
-        case 512: return fs_cols<512, FWD>(var, in, out, N2, batch, split, lo_bits, s);
-        case 1024: return fs_cols<1024, FWD>(var, in, out, N2, batch, split, lo_bits, s);
+        case 64: return fs_cols<64, FWD>(var, in, out, N2, batch, split, lo_bits, hk, s);
+        case 128: return fs_cols<128, FWD>(var, in, out, N2, batch, split, lo_bits, hk, s);
+        case 256: return fs_cols<256, FWD>(var, in, out, N2, batch, split, lo_bits, hk, s);
+        case 512: return fs_cols<512, FWD>(var, in, out, N2, batch, split, lo_bits, hk, s);
+        case 1024: return fs_cols<1024, FWD>(var, in, out, N2, batch, split, lo_bits, hk, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <bool FWD>
 hipError_t fs_rows_any(int N2, int var, const float2* in, float2* out, int N1, long long batch, float scale,
-                       const float2* mulv, hipStream_t s) {
+                       const FsHooks& hk, hipStream_t s) {
     switch (N2) {
-        case 64: return fs_rows<64, FWD>(var, in, out, N1, batch, scale, mulv, s);
-        case 128: return fs_rows<128, FWD>(var, in, out, N1, batch, scale, mulv, s);
-        case 256: return fs_rows<256, FWD>(var, in, out, N1, batch, scale, mulv, s);
-        case 512: return fs_rows<512, FWD>(var, in, out, N1, batch, scale, mulv, s);
-        case 1024: return fs_rows<1024, FWD>(var, in, out, N1, batch, scale, mulv, s);
+        case 64: return fs_rows<64, FWD>(var, in, out, N1, batch, scale, hk, s);
+        case 128: return fs_rows<128, FWD>(var, in, out, N1, batch, scale, hk, s);
+        case 256: return fs_rows<256, FWD>(var, in, out, N1, batch, scale, hk, s);
+        case 512: return fs_rows<512, FWD>(var, in, out, N1, batch, scale, hk, s);
+        case 1024: return fs_rows<1024, FWD>(var, in, out, N1, batch, scale, hk, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -281,8 +319,12 @@ long long env_ll(const char* name, long long dflt) {
 }
 
 // n = N1*N2, 64 <= N1 <= N2 <= 1024
-hipError_t launch_c2c_twopass(long long n, int lg, int fwd, const float2* in, float2* out, long long batch,
-                              hipStream_t s, const float2* mulv = nullptr) {
+// One two-pass transform chain over a batch in chunks.  With hooks, the
+// columns pass may read the raw Bluestein input (pre) instead of `in`, and the
+// rows pass may multiply by a vector (mulv) and/or write scaled, chirped and
+// truncated rows to another buffer (post) instead of `out`.
+hipError_t twopass_chain(long long n, int lg, int fwd, const float2* in, float2* out, long long batch, hipStream_t s,
+                         FsHooks hk) {
     const int N1 = 1 << (lg / 2), N2 = (int)(n / N1);
     int lo_bits = 0;
     const float2* split = twiddle_split(n, &lo_bits);
@@ -299,16 +341,22 @@ hipError_t launch_c2c_twopass(long long n, int lg, int fwd, const float2* in, fl
     const float scale = 1.0f / (float)n;
     for (long long c = 0; c < batch && e == hipSuccess; c += chunk) {
         const long long nb = batch - c < chunk ? batch - c : chunk;
-        const float2* src = in + c * n;
-        float2* dst = out + c * n;
-        e = fwd ? fs_cols_any<true>(N1, var, src, y, N2, nb, split, lo_bits, s)
-                : fs_cols_any<false>(N1, var, src, y, N2, nb, split, lo_bits, s);
+        const float2* src = hk.pre_chirp ? nullptr : in + c * n;
+        float2* dst = hk.post_chirp ? nullptr : out + c * n;
+        hk.b0 = c;
+        e = fwd ? fs_cols_any<true>(N1, var, src, y, N2, nb, split, lo_bits, hk, s)
+                : fs_cols_any<false>(N1, var, src, y, N2, nb, split, lo_bits, hk, s);
         if (e == hipSuccess)
-            e = fwd ? fs_rows_any<true>(N2, var, y, dst, N1, nb, scale, mulv, s)
-                    : fs_rows_any<false>(N2, var, y, dst, N1, nb, scale, mulv, s);
+            e = fwd ? fs_rows_any<true>(N2, var, y, dst, N1, nb, scale, hk, s)
+                    : fs_rows_any<false>(N2, var, y, dst, N1, nb, scale, hk, s);
     }
     (void)hipFreeAsync(y, s);
     return e;
+}
+
+hipError_t launch_c2c_twopass(long long n, int lg, int fwd, const float2* in, float2* out, long long batch,
+                              hipStream_t s) {
+    return twopass_chain(n, lg, fwd, in, out, batch, s, FsHooks{});
 }
 }  // namespace
 
@@ -519,6 +567,35 @@ hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, f
     const ChirpPlan* p = chirp_plan(n, fwd, s);
     if (!p) return hipErrorOutOfMemory;
     const long long M = p->M, total = M * batch;
+    const int lgM = ilog2((int)(M < (1LL << 30) ? M : (1LL << 30)));
+    if (!c2c_supported(M) && lgM <= 20 && env_ll("VVHIP_FS_OLD", 0) == 0 && env_ll("VVHIP_BLUE_UNFUSED", 0) == 0) {
+        // two-pass M (8192..2^20): chirp pre-multiply and zero padding in the forward
+        // columns pass, the product with V in its rows pass, and the post-multiply,
+        // scale and truncation to nout in the inverse rows pass -- four kernels,
+        // no u / padded-input pass and no full-length output pass
+        float2* U = nullptr;
+        hipError_t e = hipMallocAsync((void**)&U, sizeof(float2) * total, s);
+        if (e != hipSuccess) return e;
+        FsHooks f;
+        f.pre_chirp = p->chirp;
+        f.raw = in;
+        f.in_dist = in_dist;
+        f.nsig = n;
+        f.real_in = real_in;
+        f.mulv = p->V;
+        e = twopass_chain(M, lgM, 1, nullptr, U, batch, s, f);
+        if (e == hipSuccess) {
+            FsHooks b;
+            b.post_chirp = p->chirp;
+            b.post_out = out;
+            b.out_dist = out_dist;
+            b.nout = nout;
+            b.post_scale = scale;
+            e = twopass_chain(M, lgM, 0, U, nullptr, batch, s, b);
+        }
+        (void)hipFreeAsync(U, s);
+        return e;
+    }
     float2 *u = nullptr, *U = nullptr;
     hipError_t e = hipMallocAsync((void**)&u, sizeof(float2) * total, s);
     if (e != hipSuccess) return e;
@@ -531,15 +608,9 @@ hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, f
         hipLaunchKernelGGL(k_bluestein_pre, dim3(grid_for(total)), dim3(256), 0, s, in, real_in, in_dist, p->chirp, u,
                            n, M, total);
         if ((e = hipGetLastError()) != hipSuccess) break;
-        // FFT(u) * V: fused into the rows pass when M runs two-pass (8192..2^20)
-        const int lgM = ilog2((int)(M < (1LL << 30) ? M : (1LL << 30)));
-        if (!c2c_supported(M) && lgM <= 20 && env_ll("VVHIP_FS_OLD", 0) == 0 && env_ll("VVHIP_BLUE_UNFUSED", 0) == 0) {
-            if ((e = launch_c2c_twopass(M, lgM, 1, u, U, batch, s, p->V)) != hipSuccess) break;
-        } else {
-            if ((e = fft_pow2(M, 1, u, U, batch, s)) != hipSuccess) break;
-            hipLaunchKernelGGL(k_mul_bcast, dim3(grid_for(total)), dim3(256), 0, s, U, p->V, M, total);
-            if ((e = hipGetLastError()) != hipSuccess) break;
-        }
+        if ((e = fft_pow2(M, 1, u, U, batch, s)) != hipSuccess) break;
+        hipLaunchKernelGGL(k_mul_bcast, dim3(grid_for(total)), dim3(256), 0, s, U, p->V, M, total);
+        if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = fft_pow2(M, 0, U, u, batch, s)) != hipSuccess) break;   // includes 1/M
         const long long tot_out = nout * batch;
         hipLaunchKernelGGL(k_bluestein_post, dim3(grid_for(tot_out)), dim3(256), 0, s, u, p->chirp, out, M, nout,
