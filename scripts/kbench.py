@@ -307,7 +307,7 @@ def main():
         byts = built[k][1]
         ms = np.array(res[k])
         gbs = byts / (np.median(ms) * 1e-3) / 1e9
-        print(json.dumps({"case": k, "ms_median": round(float(np.median(ms)), 4),
+        print(json.dumps({"case": k, "ms_median": round(float(np.median(ms)), 4), "ms_mean": round(float(ms.mean()), 4),
                           "ms_min": round(float(ms.min()), 4), "GBs": round(gbs, 1),
                           "frac": round(gbs / PEAK, 4), "bytes": byts}))
 
