@@ -76,9 +76,9 @@ def fft_c2c_roofline(reps=20):
                       torch.rand(B, N, device="cuda", generator=g) - 0.5)
     y = torch.empty_like(x)
     plan = vv.FftPlan(N, vv.C2C, vv.FWD, batch=B)
-    avg, best = timed_launches(lambda: plan(x, out=y), reps)
+    avg, best = timed_launches(lambda: plan(x, out=y), reps, warm=10)
     planb = vv.FftPlan(N, vv.C2C, vv.BWD, batch=B)
-    bavg, bbest = timed_launches(lambda: planb(x, out=y), reps)
+    bavg, bbest = timed_launches(lambda: planb(x, out=y), reps, warm=10)
     byts = 2 * B * N * 8
     del x, y
     return {"workload": "config2: 65536 x 1024-pt c2c f32 forward", "bytes_per_launch": byts,
@@ -132,7 +132,7 @@ def fir_roofline(reps=10):
     x = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
     y = torch.empty_like(x)
     plan = vv.FirPlan(torch.from_numpy(h))
-    avg, best = timed_launches(lambda: plan(x, out=y), reps)
+    avg, best = timed_launches(lambda: plan(x, out=y), reps, warm=10)
     byts = 2 * nch * n * 4
     del x, y
     return {"workload": "config4: FIR overlap-save 257 taps, 8 ch x 2^24 f32", "bytes_per_launch": byts,
