@@ -111,15 +111,18 @@ k_mel_grp(const float* __restrict__ in, long long frames, int in_len, int n_mels
     float* sW = smem;                                                   // nnz
     int* sCh = reinterpret_cast<int*>(sW + (FILT ? nnz : 0));           // 3*nc: lo, len, off
     int* sCb = sCh + (FILT ? 3 * nc : 0);                               // M+1
-    float* sD = reinterpret_cast<float*>(sCb + (FILT ? M + 1 : 0));     // C*M
+    // the DCT table, the per-wave areas and the log-mel rows start 16 B aligned
+    // (float4 reads in the DCT); the host sizes the shared part the same way
+    const int dpos = ((FILT ? nnz + 3 * nc + M + 1 : 0) + 3) & ~3;
+    float* sD = smem + dpos;                                            // C*M
     float* sL = sD + (DCT ? C * M : 0);                                 // C
-    // per-wave areas start 16 B aligned (the host rounds the shared part up)
-    float* wave_base = smem + ((((FILT ? nnz + 3 * nc + M + 1 : 0) + (DCT ? C * M + C : 0)) + 3) & ~3);
+    float* wave_base = smem + ((dpos + (DCT ? C * M + C : 0) + 3) & ~3);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int per_wave = row_floats + (FILT ? FR * nc : 0) + (MODE == 1 ? FR * M : 0);
+    const int part_floats = FILT ? (FR * nc + 3) & ~3 : 0;
+    const int per_wave = row_floats + part_floats + (MODE == 1 ? FR * M : 0);
     float* row = wave_base + wv * per_wave;                             // FR input rows (row_floats >= FR*in_len)
     float* part = row + row_floats;                                     // [FR][nc] chunk sums
-    float* lm = MODE == 2 ? row : part + (FILT ? FR * nc : 0);          // [FR][M] log-mel rows
+    float* lm = MODE == 2 ? row : part + part_floats;                   // [FR][M] log-mel rows
     if constexpr (FILT) {
         for (int i = threadIdx.x; i < nnz; i += blockDim.x) sW[i] = W[i];
         for (int i = threadIdx.x; i < 3 * nc; i += blockDim.x) sCh[i] = chunks[i];
@@ -200,14 +203,25 @@ k_mel_grp(const float* __restrict__ in, long long frames, int in_len, int n_mels
                 const int f = idx / C, i = idx - f * C;
                 const float* l = lm + f * M;
                 const float* d = sD + i * M;
-                float c0 = 0.0f, c1 = 0.0f;
+                float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
                 int m = 0;
-                for (; m + 1 < M; m += 2) {
-                    c0 = __builtin_fmaf(l[m], d[m], c0);
-                    c1 = __builtin_fmaf(l[m + 1], d[m + 1], c1);
+                if ((M & 3) == 0) {   // 16 B LDS reads: a quarter of the read instructions
+                    for (; m < M; m += 4) {
+                        const vf4_t a = *reinterpret_cast<const vf4_t*>(l + m);
+                        const vf4_t b = *reinterpret_cast<const vf4_t*>(d + m);
+                        c0 = __builtin_fmaf(a[0], b[0], c0);
+                        c1 = __builtin_fmaf(a[1], b[1], c1);
+                        c2 = __builtin_fmaf(a[2], b[2], c2);
+                        c3 = __builtin_fmaf(a[3], b[3], c3);
+                    }
+                } else {
+                    for (; m + 1 < M; m += 2) {
+                        c0 = __builtin_fmaf(l[m], d[m], c0);
+                        c1 = __builtin_fmaf(l[m + 1], d[m + 1], c1);
+                    }
+                    if (m < M) c0 = __builtin_fmaf(l[m], d[m], c0);
                 }
-                if (m < M) c0 = __builtin_fmaf(l[m], d[m], c0);
-                out[f0 * C + idx] = (c0 + c1) * sL[i];
+                out[f0 * C + idx] = ((c0 + c1) + (c2 + c3)) * sL[i];
             }
         }
         xsync<64>();   // the next group overwrites this wave's rows
@@ -253,14 +267,15 @@ hipError_t launch_mel_grp(int mode, const float* in, long long frames, int nbins
     if (frames <= 0) return hipSuccess;
     const bool filt = mode != 2, dct = mode != 0;
     const int in_len = mode == 2 ? n_mels : nbins;
-    const size_t shared = sizeof(float) * ((((filt ? (size_t)nnz + 3 * (size_t)nc + n_mels + 1 : 0) +
-                                             (dct ? (size_t)n_coeffs * n_mels + n_coeffs : 0)) + 3) & ~(size_t)3);
+    // layout as in k_mel_grp: DCT table and per-wave areas 16 B aligned
+    const size_t dpos = ((filt ? (size_t)nnz + 3 * (size_t)nc + n_mels + 1 : 0) + 3) & ~(size_t)3;
+    const size_t shared = sizeof(float) * ((dpos + (dct ? (size_t)n_coeffs * n_mels + n_coeffs : 0) + 3) & ~(size_t)3);
     // frames per wave step: 4, fewer when the rows are long
     int fr = 4;
     // row area: whole 256-float LDS-DMA pieces
     auto row_floats = [&](int f) { return (f * in_len + 255) / 256 * 256; };
     auto per_wave = [&](int f) {
-        return sizeof(float) * (size_t)(row_floats(f) + (filt ? f * nc : 0) + (mode == 1 ? f * n_mels : 0));
+        return sizeof(float) * (size_t)(row_floats(f) + (filt ? (f * nc + 3) & ~3 : 0) + (mode == 1 ? f * n_mels : 0));
     };
     while (fr > 1 && per_wave(fr) > 16 * 1024) fr >>= 1;
     int wpb = 4;
