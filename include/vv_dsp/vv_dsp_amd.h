@@ -89,6 +89,14 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_fir_apply_direct_device(vv_dsp_fir_plan* p
 /* Hilbert analytic signal of `batch` contiguous real[N] rows -> cpx[batch][N] */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_hilbert_analytic_device(const vv_dsp_real* d_x, size_t N, size_t batch,
                                                               vv_dsp_cpx* d_z, void* stream);
+/* Instantaneous phase (unwrapped, radians) of `batch` contiguous analytic rows
+ * cpx[batch][N] -> real[batch][N]; instantaneous frequency (Hz) of phase rows
+ * real[batch][N] -> real[batch][N], element 0 of each row = 0 (hilbert.c:77-113). */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_instantaneous_phase_device(const vv_dsp_cpx* d_analytic, size_t N,
+                                                                 size_t batch, vv_dsp_real* d_phase, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_instantaneous_frequency_device(const vv_dsp_real* d_phase, size_t N,
+                                                                     size_t batch, double sample_rate,
+                                                                     vv_dsp_real* d_freq, void* stream);
 /* DCT of `batch` contiguous rows with the plan's type/direction */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dct_execute_device(const vv_dsp_dct_plan* plan, const vv_dsp_real* d_in,
                                                          vv_dsp_real* d_out, size_t batch, void* stream);

@@ -140,6 +140,13 @@ size_t vvhip_fir_block_size(vvhip_fir* f, size_t n);
 /* ---- Hilbert analytic signal (hilbert.c:14-75) ---- */
 int vvhip_hilbert_host(const float* x, size_t n, float* z_out);
 int vvhip_hilbert_device(const float* d_x, size_t n, size_t batch, float* d_z, void* stream);
+/* Instantaneous phase / frequency (hilbert.c:77-113) of `batch` contiguous rows
+ * of n samples: z complex[batch][n] -> unwrapped phase real[batch][n];
+ * phase -> frequency in Hz (freq[row][0] = 0), fs the sample rate. */
+int vvhip_inst_phase_host(const float* z, size_t n, float* phase);
+int vvhip_inst_phase_device(const float* d_z, size_t n, size_t batch, float* d_phase, void* stream);
+int vvhip_inst_freq_host(const float* phase, size_t n, double fs, float* freq);
+int vvhip_inst_freq_device(const float* d_phase, size_t n, size_t batch, double fs, float* d_freq, void* stream);
 
 /* ---- DCT (dct.c:86-136); nan_policy as core/nan_policy.h (0..3) ---- */
 int vvhip_dct_host(const float* in, float* out, size_t n, int type, int dir, int nan_policy);

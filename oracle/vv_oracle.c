@@ -232,6 +232,33 @@ int orc_hilbert_analytic(const float* x, size_t n, float* z_out) {
     return 0;
 }
 
+/* hilbert.c:77-96: principal phase of z[0], then f64 increments
+ * atan2(Im(z_i conj z_{i-1}), Re(z_i conj z_{i-1})) summed left to right */
+int orc_inst_phase(const float* z, size_t n, float* phase) {
+    if (!z || !phase) return 1;
+    if (n == 0) return 2;
+    double acc = atan2((double)z[1], (double)z[0]);
+    phase[0] = (float)acc;
+    for (size_t i = 1; i < n; ++i) {
+        const double cr = z[2 * i], ci = z[2 * i + 1], pr = z[2 * i - 2], pi = z[2 * i - 1];
+        const double re = cr * pr + ci * pi;
+        const double im = ci * pr - cr * pi;
+        acc += atan2(im, re);
+        phase[i] = (float)acc;
+    }
+    return 0;
+}
+
+/* hilbert.c:98-113: freq[0] = 0, freq[i] = (p[i] - p[i-1]) * fs / (2 pi) in f64 */
+int orc_inst_freq(const float* phase, size_t n, double fs, float* freq) {
+    if (!phase || !freq) return 1;
+    if (n == 0) return 2;
+    const double scale = fs / (2.0 * 3.141592653589793238462643383279502884);
+    freq[0] = 0.0f;
+    for (size_t i = 1; i < n; ++i) freq[i] = (float)(((double)phase[i] - (double)phase[i - 1]) * scale);
+    return 0;
+}
+
 /* dct.c:21-68 naive kernels; :86-136 dispatch (NaN policy PROPAGATE = identity) */
 int orc_dct(const float* in, float* out, size_t n, int type, int dir) {
     if (!in || !out) return 1;

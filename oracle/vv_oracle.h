@@ -40,6 +40,10 @@ int orc_stft_reconstruct(const float* win, size_t nfft, const float* spec,
 /* Hilbert analytic signal (src/spectral/hilbert.c:14-75) */
 int orc_hilbert_analytic(const float* x, size_t n, float* z_out);
 
+/* Instantaneous phase / frequency (src/spectral/hilbert.c:77-113) */
+int orc_inst_phase(const float* z, size_t n, float* phase);                         /* :77-96 */
+int orc_inst_freq(const float* phase, size_t n, double fs, float* freq);           /* :98-113 */
+
 /* DCT (src/spectral/dct.c). type 2/3/4, dir +1/-1 (NaN policy: PROPAGATE). */
 int orc_dct(const float* in, float* out, size_t n, int type, int dir);    /* :86-136 */
 

@@ -87,6 +87,10 @@ def test_argument_validation_matches_reference(cpu_lib, ref):
         assert L.vv_dsp_fir_state_init(C.byref(st), 0) == ERR_SIZE
         assert L.vv_dsp_fir_apply_fft(C.byref(st), hp, hp, hp, 8) == ERR_SIZE   # num_taps == 0
         assert L.vv_dsp_hilbert_analytic(hp, 0, hp) == ERR_SIZE
+        assert L.vv_dsp_instantaneous_phase(None, 4, hp) == ERR_NULL
+        assert L.vv_dsp_instantaneous_phase(hp, 0, hp) == ERR_SIZE
+        assert L.vv_dsp_instantaneous_frequency(hp, 4, 1000.0, None) == ERR_NULL
+        assert L.vv_dsp_instantaneous_frequency(hp, 0, 1000.0, hp) == ERR_SIZE
 
 
 def test_fir_design_bitexact_host_setup(cpu_lib, orc):
@@ -149,6 +153,8 @@ def test_no_gpu_fails_loudly(cpu_lib):
     fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
     assert L.vv_dsp_hilbert_analytic(fp(x), 64, fp(z)) == ERR_UNSUPPORTED
     assert L.vv_dsp_dct_forward(64, 2, fp(x), fp(z)) == ERR_UNSUPPORTED
+    assert L.vv_dsp_instantaneous_phase(fp(z), 64, fp(x)) == ERR_UNSUPPORTED
+    assert L.vv_dsp_instantaneous_frequency(fp(x), 64, 1000.0, fp(z)) == ERR_UNSUPPORTED
     st = FirState()
     assert L.vv_dsp_fir_state_init(C.byref(st), 4) == OK
     assert L.vv_dsp_fir_apply(C.byref(st), fp(x), fp(x), fp(z), 64) == ERR_UNSUPPORTED

@@ -793,3 +793,63 @@ def test_fft_host_pipeline_matches_device(amd_lib_path, vdev, monkeypatch):
         d = vdev.FftPlan(n, vdev.C2C if kind == C2C else vdev.R2C, vdev.FWD, batch=b)(
             torch.from_numpy(x).cuda()).cpu().numpy()
         assert np.array_equal(y, d), (kind, n, b)
+
+
+def test_dct_error_policy_input_nan_leaves_output(amd, ref):
+    """ERROR policy with a NaN input: status NAN and the output buffer untouched,
+    as the reference returns before writing it (dct.c:96-100); with finite input
+    but an overflowing output the output IS written (dct.c:128-131)."""
+    import ctypes as C
+    x = np.ones(64, np.float32)
+    x[5] = np.nan
+    for lib in (amd, ref):
+        lib.lib.vv_dsp_set_nan_policy.argtypes = [C.c_int]
+        lib.lib.vv_dsp_set_nan_policy(2)
+        try:
+            y = np.full(64, 7.0, np.float32)
+            fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+            assert lib.lib.vv_dsp_dct_forward(64, 2, fp(x), fp(y)) == 5
+            assert np.all(y == 7.0)
+        finally:
+            lib.lib.vv_dsp_set_nan_policy(0)
+
+
+def test_nan_policy_is_per_thread(amd):
+    """nan_policy.c:11-31 keeps the policy _Thread_local: another thread's setting
+    does not leak into this one."""
+    import ctypes as C
+    import threading
+    L = amd.lib
+    L.vv_dsp_set_nan_policy.argtypes = [C.c_int]
+    L.vv_dsp_get_nan_policy.restype = C.c_int
+    L.vv_dsp_set_nan_policy(0)
+    seen = []
+
+    def other():
+        L.vv_dsp_set_nan_policy(2)
+        seen.append(L.vv_dsp_get_nan_policy())
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen == [2] and L.vv_dsp_get_nan_policy() == 0
+
+
+def test_device_wrappers_check_shapes(vdev):
+    """The Python device API checks tensors against the plan before handing
+    pointers to the kernels (a wrong dtype or a short tensor would be read or
+    written past its allocation)."""
+    import torch
+    p = vdev.FftPlan(1024, vdev.C2C, vdev.FWD, batch=4)
+    with pytest.raises(vdev.VvError):
+        p(torch.zeros(4, 1024, device="cuda"))                        # float32 into a C2C plan
+    with pytest.raises(vdev.VvError):
+        p(torch.zeros(3, 1024, dtype=torch.complex64, device="cuda"))   # too few rows
+    with pytest.raises(vdev.VvError):
+        p(torch.zeros(4, 1024, dtype=torch.complex64, device="cuda"),
+          out=torch.zeros(4, 1000, dtype=torch.complex64, device="cuda"))
+    st = vdev.Stft(1024, 256)
+    with pytest.raises(vdev.VvError):
+        st.reconstruct(torch.zeros(5, 1024, dtype=torch.complex64, device="cuda"),
+                       torch.zeros(100, device="cuda"))
+    with pytest.raises(vdev.VvError):
+        st.spectrogram(torch.zeros(2, 4096, device="cuda"), out=torch.zeros(2, 3, 1024, device="cuda"))

@@ -45,6 +45,33 @@ def test_oracle_stft_hilbert_dct_fir_bitexact(orc, ref):
                               equal_nan=True)
 
 
+def _sine_analytic(n, fs, f0, ref):
+    """the reference hilbert_tests.c:16-48 input: a bin-centred sine's analytic signal"""
+    t = np.arange(n) / fs
+    return ref.hilbert(np.sin(2 * np.pi * f0 * t).astype(np.float32))
+
+
+def test_oracle_inst_phase_freq_bitexact(orc, ref):
+    """hilbert.c:77-113 restated: phase (f64 increments summed left to right) and
+    frequency (f64 difference x fs/2pi) bit-identical to the compiled reference."""
+    rng = np.random.default_rng(21)
+    cases = [_sine_analytic(256, 1000.0, 31 * 1000.0 / 256, ref), _sine_analytic(16384, 48000.0, 440.0, ref)]
+    for n in (1, 2, 3, 255, 4096, 20000):
+        cases.append((rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64))
+    z = np.zeros(64, np.complex64)   # atan2(0, 0) = 0 increments
+    z[10] = 1 + 1j
+    cases.append(z)
+    for z in cases:
+        pa, pb = orc.inst_phase(z), ref.inst_phase(z)
+        assert np.array_equal(pa, pb), len(z)
+        for fs in (1000.0, 48000.0, 1.0):
+            assert np.array_equal(orc.inst_freq(pa, fs), ref.inst_freq(pb, fs)), (len(z), fs)
+    # the reference test's acceptance (hilbert_tests.c:40-43): mean frequency within 0.5 Hz of f0
+    f0 = 31 * 1000.0 / 256
+    fr = orc.inst_freq(orc.inst_phase(_sine_analytic(256, 1000.0, f0, ref)), 1000.0)
+    assert abs(fr[1:].astype(np.float64).mean() - f0) < 0.5
+
+
 MEL_CASES = [(512, 26, 16000.0, 0.0, 8000.0), (1024, 40, 48000.0, 20.0, 20000.0), (2048, 128, 44100.0, 0.0,
                                                                                    22050.0), (256, 10, 8000.0, 300.0, 3400.0)]
 

@@ -64,6 +64,8 @@ class VvDsp:
         L.vv_dsp_stft_reconstruct.argtypes = [_vp, _f32p, _f32p, _f32p]
         L.vv_dsp_stft_spectrogram.argtypes = [_vp, _f32p, C.c_size_t, _f32p, C.POINTER(C.c_size_t)]
         L.vv_dsp_hilbert_analytic.argtypes = [_f32p, C.c_size_t, _f32p]
+        L.vv_dsp_instantaneous_phase.argtypes = [_f32p, C.c_size_t, _f32p]
+        L.vv_dsp_instantaneous_frequency.argtypes = [_f32p, C.c_size_t, C.c_double, _f32p]
         L.vv_dsp_dct_forward.argtypes = [C.c_size_t, C.c_int, _f32p, _f32p]
         L.vv_dsp_dct_inverse.argtypes = [C.c_size_t, C.c_int, _f32p, _f32p]
         L.vv_dsp_fir_design_lowpass.argtypes = [_f32p, C.c_size_t, C.c_float, C.c_int]
@@ -125,17 +127,21 @@ class VvDsp:
         st, h = self.stft_create(nfft, hop, window)
         if st != OK:
             raise RuntimeError(f"stft_create status {st}")
+        try:
+            return self.spectrogram_h(h, x, nfft, hop)
+        finally:
+            self.lib.vv_dsp_stft_destroy(h)
+
+    def spectrogram_h(self, h, x, nfft, hop):
+        """vv_dsp_stft_spectrogram on an existing handle"""
         x = np.ascontiguousarray(x, np.float32)
         n = len(x)
         frames = 1 if n < nfft else 1 + (n - nfft + hop) // hop
         out = np.zeros(frames * nfft, np.float32)
         nf = C.c_size_t(0)
-        try:
-            st = self.lib.vv_dsp_stft_spectrogram(h, _fp(x), n, _fp(out), C.byref(nf))
-            if st != OK:
-                raise RuntimeError(f"spectrogram status {st}")
-        finally:
-            self.lib.vv_dsp_stft_destroy(h)
+        st = self.lib.vv_dsp_stft_spectrogram(h, _fp(x), n, _fp(out), C.byref(nf))
+        if st != OK:
+            raise RuntimeError(f"spectrogram status {st}")
         assert nf.value == frames
         return out.reshape(frames, nfft)
 
@@ -154,6 +160,24 @@ class VvDsp:
         if st != OK:
             raise RuntimeError(f"hilbert status {st}")
         return z.view(np.complex64)
+
+    def inst_phase(self, z):
+        """vv_dsp_instantaneous_phase (hilbert.c:77-96): complex[N] -> unwrapped phase[N]"""
+        zf = _cplx_view(z)
+        out = np.zeros(len(z), np.float32)
+        st = self.lib.vv_dsp_instantaneous_phase(_fp(zf), len(z), _fp(out))
+        if st != OK:
+            raise RuntimeError(f"instantaneous_phase status {st}{self._err()}")
+        return out
+
+    def inst_freq(self, phase, fs):
+        """vv_dsp_instantaneous_frequency (hilbert.c:98-113)"""
+        phase = np.ascontiguousarray(phase, np.float32)
+        out = np.zeros_like(phase)
+        st = self.lib.vv_dsp_instantaneous_frequency(_fp(phase), len(phase), fs, _fp(out))
+        if st != OK:
+            raise RuntimeError(f"instantaneous_frequency status {st}{self._err()}")
+        return out
 
     def dct(self, x, dct_type=DCT_II, inverse=False):
         st, y = self.dct_status(x, dct_type, inverse)
@@ -326,6 +350,8 @@ class Oracle:
         L.orc_stft_process.argtypes = [_f32p, C.c_size_t, _f32p, _f32p]
         L.orc_stft_reconstruct.argtypes = [_f32p, C.c_size_t, _f32p, _f32p, _f32p]
         L.orc_hilbert_analytic.argtypes = [_f32p, C.c_size_t, _f32p]
+        L.orc_inst_phase.argtypes = [_f32p, C.c_size_t, _f32p]
+        L.orc_inst_freq.argtypes = [_f32p, C.c_size_t, C.c_double, _f32p]
         L.orc_dct.argtypes = [_f32p, _f32p, C.c_size_t, C.c_int, C.c_int]
         L.orc_fir_design_lowpass.argtypes = [_f32p, C.c_size_t, C.c_float, C.c_int]
         L.orc_fir_apply.argtypes = [_f32p, C.c_size_t, _f32p, C.POINTER(C.c_size_t), _f32p,
@@ -370,6 +396,18 @@ class Oracle:
         z = np.zeros(2 * len(x), np.float32)
         assert self.lib.orc_hilbert_analytic(_fp(x), len(x), _fp(z)) == 0
         return z.view(np.complex64)
+
+    def inst_phase(self, z):
+        zf = _cplx_view(z)
+        out = np.zeros(len(z), np.float32)
+        assert self.lib.orc_inst_phase(_fp(zf), len(z), _fp(out)) == 0
+        return out
+
+    def inst_freq(self, phase, fs):
+        phase = np.ascontiguousarray(phase, np.float32)
+        out = np.zeros_like(phase)
+        assert self.lib.orc_inst_freq(_fp(phase), len(phase), fs, _fp(out)) == 0
+        return out
 
     def dct(self, x, dct_type=DCT_II, inverse=False):
         x = np.ascontiguousarray(x, np.float32)

@@ -384,48 +384,63 @@ hipError_t launch_fir_ols(long long nfft, long long taps, const float2* H, const
 //   acc = 0; acc += h[0]*x[i]; acc += h[t]*x[i-t] for t = 1..L-1 (newest first)
 // with every product and sum rounded separately (no FMA contraction), so the
 // f32 result equals the reference's.  Samples before x[0] come from `prefix`.
-// A block stages its input window (DIRECT_TILE + L - 1 samples) and h in LDS.
+// A block owns DIRECT_TILE outputs; the taps go through LDS in tiles of
+// DIRECT_TAPS (with the matching input window, DIRECT_TILE + DIRECT_TAPS - 1
+// samples), the accumulators stay in registers across tiles, so any filter
+// length keeps the reference's summation order in 37 KB of LDS.
 // ------------------------------------------------------------------------
 constexpr int DIRECT_TILE = 1024;
+constexpr int DIRECT_TAPS = 4096;
+constexpr int DIRECT_OPT = DIRECT_TILE / 256;   // outputs per thread
 
 __global__ void __launch_bounds__(256)
 k_fir_direct(const float* __restrict__ h, long long taps, const float* __restrict__ x,
              float* __restrict__ y, long long n, long long x_stride, long long y_stride,
              const float* __restrict__ prefix, long long tiles_per_ch) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* hs = smem;                          // taps
-    float* xs = smem + ((taps + 3) & ~3LL);    // DIRECT_TILE + taps - 1
+    __shared__ float hs[DIRECT_TAPS];
+    __shared__ float xs[DIRECT_TILE + DIRECT_TAPS];
     const long long c = blockIdx.x / tiles_per_ch;
     const long long i0 = (blockIdx.x % tiles_per_ch) * DIRECT_TILE;
     const long long lm1 = taps - 1;
     const float* xc = x + c * x_stride;
     const float* pc = prefix ? prefix + c * lm1 : nullptr;
-    for (long long t = threadIdx.x; t < taps; t += blockDim.x) hs[t] = h[t];
-    for (long long e = threadIdx.x; e < DIRECT_TILE + lm1; e += blockDim.x) {
-        const long long idx = i0 - lm1 + e;
-        float v;
-        if (idx < 0) v = pc ? pc[lm1 + idx] : 0.0f;
-        else v = (idx < n) ? xc[idx] : 0.0f;
-        xs[e] = v;
-    }
-    __syncthreads();
-    float* yc = y + c * y_stride;
-    for (int o = threadIdx.x; o < DIRECT_TILE; o += blockDim.x) {
-        const long long i = i0 + o;
-        if (i >= n) break;
-        const float* xi = xs + lm1 + o;        // xi[-t] = x[i - t]
-        // hipcc contracts a*b+c into v_fma regardless of pragmas; an empty asm on
-        // the product keeps the multiply and the add separately rounded.
-        float acc = 0.0f;
-        float p0 = hs[0] * xi[0];
-        asm volatile("" : "+v"(p0));
-        acc = acc + p0;
-        for (long long t = 1; t < taps; ++t) {
-            float pt = hs[t] * xi[-t];
-            asm volatile("" : "+v"(pt));
-            acc = acc + pt;
+    float acc[DIRECT_OPT];
+#pragma unroll
+    for (int j = 0; j < DIRECT_OPT; ++j) acc[j] = 0.0f;
+    for (long long t0 = 0; t0 < taps; t0 += DIRECT_TAPS) {
+        const int tt = (int)(taps - t0 < DIRECT_TAPS ? taps - t0 : DIRECT_TAPS);
+        __syncthreads();   // the previous tile's reads are done
+        for (int u = threadIdx.x; u < tt; u += 256) hs[u] = h[t0 + u];
+        // xs[e] = x[i0 - t0 - (tt - 1) + e], e < DIRECT_TILE + tt - 1
+        const long long base = i0 - t0 - (tt - 1);
+        for (int e = threadIdx.x; e < DIRECT_TILE + tt - 1; e += 256) {
+            const long long idx = base + e;   // >= -lm1
+            float v;
+            if (idx < 0) v = pc ? pc[lm1 + idx] : 0.0f;
+            else v = (idx < n) ? xc[idx] : 0.0f;
+            xs[e] = v;
         }
-        yc[i] = acc;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < DIRECT_OPT; ++j) {
+            const int o = threadIdx.x + 256 * j;
+            const float* xi = xs + (tt - 1) + o;   // xi[-u] = x[i0 + o - (t0 + u)]
+            float a = acc[j];
+            // hipcc contracts a*b+c into v_fma regardless of pragmas; an empty asm on
+            // the product keeps the multiply and the add separately rounded.
+            for (int u = 0; u < tt; ++u) {
+                float pt = hs[u] * xi[-u];
+                asm volatile("" : "+v"(pt));
+                a = a + pt;
+            }
+            acc[j] = a;
+        }
+    }
+    float* yc = y + c * y_stride;
+#pragma unroll
+    for (int j = 0; j < DIRECT_OPT; ++j) {
+        const long long i = i0 + threadIdx.x + 256 * j;
+        if (i < n) yc[i] = acc[j];
     }
 }
 
@@ -434,10 +449,82 @@ hipError_t launch_fir_direct(const float* h, long long taps, const float* x, flo
                              const float* prefix, hipStream_t s) {
     const long long tiles = (n + DIRECT_TILE - 1) / DIRECT_TILE;
     if (tiles * nch <= 0) return hipSuccess;
-    const size_t lds = sizeof(float) * (((taps + 3) & ~3LL) + DIRECT_TILE + taps - 1);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_fir_direct, dim3((unsigned)(tiles * nch)), dim3(256), lds, s, h, taps, x, y, n,
+    if (taps < 1 || tiles * nch > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_fir_direct, dim3((unsigned)(tiles * nch)), dim3(256), 0, s, h, taps, x, y, n,
                        x_stride, y_stride, prefix, tiles);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------
+// Overlap-save for filters longer than the fused kernels take (N > 8192):
+// blocks j (2 per complex row: z = a + i b, as k_fir_pair) gathered into rows
+// of an N-point batch, FFT, x H (FFT(h) unscaled; the inverse applies 1/N),
+// inverse FFT, and the block outputs LE..N-1 scattered back.  The FFTs are the
+// four-step kernels (large_fft.hip); these three kernels are the glue.
+// Row q of a chunk is pair p = p0 + q over (channel, pair) items.
+// ------------------------------------------------------------------------
+__global__ void k_fir_long_gather(const float* x, long long n, long long x_stride, long long nfft, long long le,
+                                  long long lout, long long ppc, long long p0, long long rows, float2* z) {
+    const long long total = rows * nfft;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long q = i / nfft, e = i - q * nfft, p = p0 + q;
+        const long long c = p / ppc, j = 2 * (p - c * ppc);
+        const float* xc = x + c * x_stride;
+        const long long ia = j * lout - le + e, ib = ia + lout;
+        const float a = (ia >= 0 && ia < n) ? xc[ia] : 0.0f;
+        const float b = (ib >= 0 && ib < n) ? xc[ib] : 0.0f;
+        z[i] = make_float2(a, b);
+    }
+}
+
+__global__ void k_fir_long_mul(float2* Z, const float2* H, long long nfft, long long total) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x)
+        Z[i] = cmul(Z[i], H[i % nfft]);
+}
+
+__global__ void k_fir_long_scatter(const float2* z, float* y, long long n, long long y_stride, long long nfft,
+                                   long long le, long long lout, long long ppc, long long p0, long long rows) {
+    const long long total = rows * lout;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long q = i / lout, k = i - q * lout, p = p0 + q;
+        const long long c = p / ppc, j = 2 * (p - c * ppc);
+        const float2 v = z[q * nfft + le + k];
+        float* yc = y + c * y_stride;
+        const long long oa = j * lout + k, ob = oa + lout;
+        if (oa < n) yc[oa] = v.x;
+        if (ob < n) yc[ob] = v.y;
+    }
+}
+
+static unsigned glue_grid(long long total) {
+    long long b = (total + 255) / 256;
+    return (unsigned)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
+}
+
+hipError_t launch_fir_long_gather(const float* x, long long n, long long x_stride, long long nfft, long long le,
+                                  long long lout, long long ppc, long long p0, long long rows, float2* z,
+                                  hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fir_long_gather, dim3(glue_grid(rows * nfft)), dim3(256), 0, s, x, n, x_stride, nfft, le,
+                       lout, ppc, p0, rows, z);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir_long_mul(float2* Z, const float2* H, long long nfft, long long rows, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fir_long_mul, dim3(glue_grid(rows * nfft)), dim3(256), 0, s, Z, H, nfft, rows * nfft);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir_long_scatter(const float2* z, float* y, long long n, long long y_stride, long long nfft,
+                                   long long le, long long lout, long long ppc, long long p0, long long rows,
+                                   hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fir_long_scatter, dim3(glue_grid(rows * lout)), dim3(256), 0, s, z, y, n, y_stride, nfft,
+                       le, lout, ppc, p0, rows);
     return hipGetLastError();
 }
 

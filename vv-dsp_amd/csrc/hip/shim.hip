@@ -161,6 +161,10 @@ struct vvhip_fft {
     hipStream_t stream = nullptr;
     DevBuf din, dout;
     HostLane lanes[2];
+    // The host-buffer path's stream, staging buffers and lanes are per plan:
+    // calls on one plan from several threads take turns (the reference's
+    // execute takes a const plan and Kiss is reentrant, fft.h:227).
+    std::mutex host_mu;
 };
 
 static size_t fft_in_elems_bytes(const vvhip_fft* p) {
@@ -318,6 +322,7 @@ int vvhip_fft_exec_device(vvhip_fft* p, const void* d_in, void* d_out, size_t ba
 
 int vvhip_fft_exec_host(vvhip_fft* p, const void* in, void* out) {
     if (!p || !in || !out) return ST_NULL;
+    std::lock_guard<std::mutex> host_lock(p->host_mu);
     const size_t ie = fft_in_elems_bytes(p), oe = fft_out_elems_bytes(p);
     const size_t chunk_b = host_chunk_bytes();
     if ((ie + oe) * p->batch >= 2 * chunk_b && p->batch >= 2) {
@@ -374,6 +379,7 @@ struct vvhip_stft {
     hipStream_t stream = nullptr;
     DevBuf b0, b1, b2;
     HostLane lanes[2];
+    std::mutex host_mu;   // host-buffer calls on one handle take turns (staging buffers, stream)
 };
 
 // out_kind: 0 magnitude rows [frame][nfft], 1 complex rows [frame][nfft],
@@ -498,6 +504,7 @@ int vvhip_stft_spectrogram_range_device(vvhip_stft* h, const float* d_signal, si
 
 int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, float* out_mag) {
     if (!h || !signal || !out_mag) return ST_NULL;
+    std::lock_guard<std::mutex> host_lock(h->host_mu);
     if (int st = stft_stream(h)) return st;
     const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
     const size_t ob = sizeof(float) * frames * h->nfft;
@@ -556,6 +563,7 @@ int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count
 
 int vvhip_stft_process_host(vvhip_stft* h, const float* frame, float* spec_out) {
     if (!h || !frame || !spec_out) return ST_NULL;
+    std::lock_guard<std::mutex> host_lock(h->host_mu);
     if (int st = stft_stream(h)) return st;
     HIPCHK(h->b0.ensure(sizeof(float) * h->nfft), ST_INTERNAL);
     HIPCHK(h->b1.ensure(8 * h->nfft), ST_INTERNAL);
@@ -592,6 +600,7 @@ int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t cou
 
 int vvhip_stft_reconstruct_host(vvhip_stft* h, const float* spec, float* out_add, float* norm_add) {
     if (!h || !spec || !out_add) return ST_NULL;
+    std::lock_guard<std::mutex> host_lock(h->host_mu);
     if (int st = stft_stream(h)) return st;
     const size_t nb = sizeof(float) * h->nfft;
     HIPCHK(h->b0.ensure(2 * nb), ST_INTERNAL);
@@ -625,6 +634,7 @@ struct vvhip_fir {
     std::mutex mu;
     hipStream_t stream = nullptr;
     DevBuf bx, by, bp;
+    std::mutex host_mu;   // host-buffer calls on one handle take turns (staging buffers, stream)
 };
 
 // Overlap-save block N (= complex FFT size of k_fir_pair): the smallest power
@@ -650,6 +660,20 @@ static size_t fir_block(const vvhip_fir* f, size_t n) {
     return nr;
 }
 
+// Overlap-save block for filters the fused kernels cannot take (taps > 6145):
+// N = pow2 >= max(4 (L-1), 16384), at most 2^22, so >= 3/4 of a block is output.
+// 0 = none (longer filters than that use the direct form).
+static size_t fir_long_block(size_t taps) {
+    const size_t lm1 = taps - 1;
+    size_t nr = 16384;
+    while (nr < 4 * lm1 && nr < ((size_t)1 << 22)) nr <<= 1;
+    if (nr <= lm1 || nr - lm1 < nr / 4) return 0;
+    return nr;
+}
+
+// H for block nr: FFT(h zero-padded to nr) over all nr bins, cached per nr.
+// nr <= 8192 (fused kernels): scaled by 1/nr.  nr > 8192 (fir_long_block, the
+// four-step path whose inverse applies 1/nr itself): unscaled.
 static int fir_spectrum(vvhip_fir* f, size_t nr, const float2** H, hipStream_t s) {
     std::lock_guard<std::mutex> lk(f->mu);
     for (auto& sp : f->specs)
@@ -657,23 +681,67 @@ static int fir_spectrum(vvhip_fir* f, size_t nr, const float2** H, hipStream_t s
             *H = sp.H;
             return ST_OK;
         }
-    // H = FFT(h zero-padded to nr) / nr over all nr bins (R2C, Hermitian expand)
-    float* hp = nullptr;
-    float2* Hh = nullptr;
     float2* Hd = nullptr;
-    HIPCHK(hipMalloc(&hp, sizeof(float) * nr), ST_INTERNAL);
-    HIPCHK(hipMalloc(&Hh, sizeof(float2) * (nr / 2 + 1)), ST_INTERNAL);
-    HIPCHK(hipMalloc(&Hd, sizeof(float2) * nr), ST_INTERNAL);
-    HIPCHK(hipMemsetAsync(hp, 0, sizeof(float) * nr, s), ST_INTERNAL);
-    HIPCHK(hipMemcpyAsync(hp, f->d_h, sizeof(float) * f->taps, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
-    HIPCHK(launch_r2c((long long)nr, hp, Hh, 1, (long long)nr, (long long)(nr / 2 + 1), s), ST_INTERNAL);
-    HIPCHK(launch_hermitian_expand((long long)nr, Hh, Hd, 1, (long long)(nr / 2 + 1), 0, s), ST_INTERNAL);
-    HIPCHK(launch_scale_cpx(Hd, (long long)nr, 1.0f / (float)nr, s), ST_INTERNAL);
-    HIPCHK(hipStreamSynchronize(s), ST_INTERNAL);
-    (void)hipFree(hp);
-    (void)hipFree(Hh);
+    void* t1 = nullptr;
+    void* t2 = nullptr;
+    hipError_t e = hipMalloc(&Hd, sizeof(float2) * nr);
+    if (nr > 8192) {   // promote h, zero pad, four-step FFT
+        if (e == hipSuccess) e = hipMalloc(&t1, sizeof(float2) * nr);
+        if (e == hipSuccess) e = hipMemsetAsync(t1, 0, sizeof(float2) * nr, s);
+        if (e == hipSuccess) e = launch_promote_real(f->d_h, (float2*)t1, (long long)f->taps, s);
+        if (e == hipSuccess) e = launch_c2c_large((long long)nr, 1, (const float2*)t1, Hd, 1, s);
+    } else {           // R2C of h zero-padded, Hermitian expand, 1/nr
+        if (e == hipSuccess) e = hipMalloc(&t1, sizeof(float) * nr);
+        if (e == hipSuccess) e = hipMalloc(&t2, sizeof(float2) * (nr / 2 + 1));
+        if (e == hipSuccess) e = hipMemsetAsync(t1, 0, sizeof(float) * nr, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(t1, f->d_h, sizeof(float) * f->taps, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess)
+            e = launch_r2c((long long)nr, (const float*)t1, (float2*)t2, 1, (long long)nr, (long long)(nr / 2 + 1), s);
+        if (e == hipSuccess)
+            e = launch_hermitian_expand((long long)nr, (const float2*)t2, Hd, 1, (long long)(nr / 2 + 1), 0, s);
+        if (e == hipSuccess) e = launch_scale_cpx(Hd, (long long)nr, 1.0f / (float)nr, s);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (t1) (void)hipFree(t1);
+    if (t2) (void)hipFree(t2);
+    if (e != hipSuccess) {
+        if (Hd) (void)hipFree(Hd);
+        return fail(ST_INTERNAL, "fir filter spectrum", e);
+    }
     f->specs.push_back({nr, Hd});
     *H = Hd;
+    return ST_OK;
+}
+
+// Zero-state linear convolution (first n outputs) for long filters: overlap-save
+// with N = fir_long_block(taps), two blocks per complex row, in chunks of rows
+// whose two scratch buffers stay within ~512 MiB.
+static int fir_ols_long(vvhip_fir* f, size_t nr, const float* d_x, float* d_y, size_t n, size_t nch,
+                        size_t x_stride, size_t y_stride, hipStream_t s) {
+    const float2* H = nullptr;
+    if (int st = fir_spectrum(f, nr, &H, s)) return st;
+    const long long N = (long long)nr, le = (long long)f->taps - 1, lout = N - le;
+    const long long nblk = ((long long)n + lout - 1) / lout, ppc = (nblk + 1) / 2;
+    const long long items = ppc * (long long)nch;
+    long long rows = (256LL << 20) / (8 * N);
+    if (rows < 1) rows = 1;
+    if (rows > items) rows = items;
+    Scratch za(s), zb(s);
+    HIPCHK(za.alloc(sizeof(float2) * (size_t)(rows * N)), ST_INTERNAL);
+    HIPCHK(zb.alloc(sizeof(float2) * (size_t)(rows * N)), ST_INTERNAL);
+    float2* A = (float2*)za.p;
+    float2* B = (float2*)zb.p;
+    for (long long p0 = 0; p0 < items; p0 += rows) {
+        const long long r = items - p0 < rows ? items - p0 : rows;
+        HIPCHK(launch_fir_long_gather(d_x, (long long)n, (long long)x_stride, N, le, lout, ppc, p0, r, A, s),
+               ST_INTERNAL);
+        HIPCHK(launch_c2c_large(N, 1, A, B, r, s), ST_INTERNAL);
+        HIPCHK(launch_fir_long_mul(B, H, N, r, s), ST_INTERNAL);
+        HIPCHK(launch_c2c_large(N, 0, B, A, r, s), ST_INTERNAL);
+        HIPCHK(launch_fir_long_scatter(A, d_y, (long long)n, (long long)y_stride, N, le, lout, ppc, p0, r, s),
+               ST_INTERNAL);
+    }
     return ST_OK;
 }
 
@@ -728,6 +796,10 @@ int vvhip_fir_apply_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n,
                ST_INTERNAL);
         return ST_OK;
     }
+    if (mode == 0) {   // long filters: overlap-save over the four-step FFTs
+        const size_t nl = fir_long_block(f->taps);
+        if (nl) return fir_ols_long(f, nl, d_x, d_y, n, nch, x_stride, y_stride, s);
+    }
     HIPCHK(launch_fir_direct(f->d_h, L, d_x, d_y, (long long)n, (long long)nch, (long long)x_stride,
                              (long long)y_stride, d_prefix, s),
            ST_INTERNAL);
@@ -736,6 +808,7 @@ int vvhip_fir_apply_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n,
 
 int vvhip_fir_apply_host(vvhip_fir* f, const float* x, float* y, size_t n, const float* prefix, int mode) {
     if (!f || !x || !y) return ST_NULL;
+    std::lock_guard<std::mutex> host_lock(f->host_mu);
     if (n == 0) return ST_OK;
     if (!f->stream) HIPCHK(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking), ST_INTERNAL);
     HIPCHK(f->bx.ensure(sizeof(float) * n), ST_INTERNAL);
@@ -801,6 +874,70 @@ int vvhip_hilbert_host(const float* x, size_t n, float* z_out) {
     if (dz) (void)hipFree(dz);
     (void)hipStreamDestroy(s);
     return st;
+}
+
+// Instantaneous phase / frequency (hilbert.c:77-113)
+static constexpr double kTwoPiD = 2.0 * 3.141592653589793238462643383279502884;   // 2 * VV_DSP_PI_D
+
+int vvhip_inst_phase_device(const float* d_z, size_t n, size_t batch, float* d_phase, void* stream) {
+    if (!d_z || !d_phase) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (batch == 0) return ST_OK;
+    if (batch > 65535) return fail(ST_RANGE, "instantaneous phase: more than 65535 rows per call");
+    HIPCHK(launch_inst_phase((const float2*)d_z, (long long)n, (long long)batch, d_phase, (hipStream_t)stream),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_inst_freq_device(const float* d_phase, size_t n, size_t batch, double fs, float* d_freq, void* stream) {
+    if (!d_phase || !d_freq) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    HIPCHK(launch_inst_freq(d_phase, (long long)n, (long long)batch, fs / kTwoPiD, d_freq, (hipStream_t)stream),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+}  // extern "C"
+
+// one row through the device: in (in_bytes) up, kernel, n floats down
+template <class F>
+static int host_row(const void* in, size_t in_bytes, float* out, size_t n, const char* what, F&& run) {
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), ST_INTERNAL);
+    int st = ST_OK;
+    {
+        Scratch din(s), dout(s);
+        if (din.alloc(in_bytes) != hipSuccess || dout.alloc(sizeof(float) * n) != hipSuccess ||
+            hipMemcpyAsync(din.p, in, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess) {
+            st = fail(ST_INTERNAL, what);
+        } else if ((st = run(din.p, (float*)dout.p, s)) == ST_OK &&
+                   (hipMemcpyAsync(out, dout.p, sizeof(float) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess)) {
+            st = fail(ST_INTERNAL, what);
+        }
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+extern "C" {
+
+int vvhip_inst_phase_host(const float* z, size_t n, float* phase) {
+    if (!z || !phase) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    return host_row(z, 8 * n, phase, n, "instantaneous phase", [&](void* dz, float* dp, hipStream_t s) {
+        return vvhip_inst_phase_device((const float*)dz, n, 1, dp, s);
+    });
+}
+
+int vvhip_inst_freq_host(const float* phase, size_t n, double fs, float* freq) {
+    if (!phase || !freq) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    return host_row(phase, 4 * n, freq, n, "instantaneous frequency", [&](void* dp, float* df, hipStream_t s) {
+        return vvhip_inst_freq_device((const float*)dp, n, 1, fs, df, s);
+    });
 }
 
 // ---------------------------------------------------------------------------
@@ -906,15 +1043,27 @@ int vvhip_overlap_add_host(const float* frame, float* out, size_t out_len, size_
 // ---------------------------------------------------------------------------
 // DCT
 // ---------------------------------------------------------------------------
+// *out_written: whether d_out was written (the ERROR policy stops at a NaN/Inf
+// input before anything is written, as dct.c:96-100 returns before the output)
+static int dct_run(const float* d_in, float* d_out, size_t n, size_t batch, int type, int dir, int nan_policy,
+                   hipStream_t s, bool* out_written);
+
 int vvhip_dct_device(const float* d_in, float* d_out, size_t n, size_t batch, int type, int dir,
                      int nan_policy, void* stream) {
+    bool wrote = false;
+    return dct_run(d_in, d_out, n, batch, type, dir, nan_policy, (hipStream_t)stream, &wrote);
+}
+
+static int dct_run(const float* d_in, float* d_out, size_t n, size_t batch, int type, int dir, int nan_policy,
+                   hipStream_t s, bool* out_written) {
+    *out_written = false;
     if (!d_in || !d_out) return ST_NULL;
     if (n == 0) return ST_SIZE;
     if ((type != 2 && type != 3 && type != 4) || (dir != 1 && dir != -1)) return ST_RANGE;
-    hipStream_t s = (hipStream_t)stream;
     const long long N = (long long)n, B = (long long)batch;
     if (type == 2 && dir > 0 && nan_policy != 2 && dct2_fused_supported(N)) {   // one pass, policy on read
         HIPCHK(launch_dct2_fused(N, d_in, d_out, B, nan_policy, s), ST_INTERNAL);
+        *out_written = true;
         return ST_OK;
     }
     Scratch xin(s), flag(s), v(s), V(s);
@@ -955,6 +1104,7 @@ int vvhip_dct_device(const float* d_in, float* d_out, size_t n, size_t batch, in
     } else {
         HIPCHK(launch_dct_naive(N, type, dir, (const float*)xin.p, d_out, B, s), ST_INTERNAL);
     }
+    *out_written = true;
     if (nan_policy != 0) {
         if (nan_policy == 2) HIPCHK(hipMemsetAsync(dflag, 0, sizeof(int), s), ST_INTERNAL);
         HIPCHK(launch_nan_policy(d_out, N * B, nan_policy, dflag, s), ST_INTERNAL);
@@ -982,9 +1132,11 @@ int vvhip_dct_host(const float* in, float* out, size_t n, int type, int dir, int
     } else if (hipMemcpyAsync(di, in, sizeof(float) * n, hipMemcpyHostToDevice, s) != hipSuccess) {
         st = fail(ST_INTERNAL, "dct h2d");
     } else {
-        st = vvhip_dct_device(di, dout, n, 1, type, dir, nan_policy, s);
-        // the reference writes the output buffer even when the output check fails
-        if ((st == ST_OK || st == ST_NAN) &&
+        bool wrote = false;
+        st = dct_run(di, dout, n, 1, type, dir, nan_policy, s, &wrote);
+        // the reference writes the output buffer even when the OUTPUT check fails
+        // (dct.c:128-131), and leaves it untouched when the input check does (:96-100)
+        if (wrote && (st == ST_OK || st == ST_NAN) &&
             (hipMemcpyAsync(out, dout, sizeof(float) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
              hipStreamSynchronize(s) != hipSuccess))
             st = fail(ST_INTERNAL, "dct d2h");
@@ -1013,6 +1165,7 @@ struct vvhip_mel {
     float* lift = nullptr;  // lifter factors [n_coeffs]
     hipStream_t stream = nullptr;
     DevBuf bin, bout;
+    std::mutex host_mu;   // host-buffer calls on one handle take turns (staging buffers, stream)
 };
 
 extern "C" {
@@ -1118,6 +1271,7 @@ int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_ou
 
 int vvhip_mel_host(vvhip_mel* m, const float* in, size_t frames, float* out, int kind) {
     if (!m || !in || !out) return ST_NULL;
+    std::lock_guard<std::mutex> host_lock(m->host_mu);
     if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
     if (frames == 0) return ST_OK;
     if (!m->stream) HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking), ST_INTERNAL);

@@ -127,6 +127,16 @@ hipError_t launch_fir_ols(long long nfft, long long taps, const float2* H, const
 hipError_t launch_fir_direct(const float* h, long long taps, const float* x, float* y, long long n,
                              long long nch, long long x_stride, long long y_stride,
                              const float* prefix, hipStream_t s);
+// overlap-save glue for filters beyond the fused kernels (N > 8192, four-step FFTs):
+// rows q < rows of pair p0 + q over (channel, pair) items, ppc pairs per channel,
+// row = z[e] = (x[2j*lout - le + e], x[(2j+1)*lout - le + e]) zero outside [0, n)
+hipError_t launch_fir_long_gather(const float* x, long long n, long long x_stride, long long nfft, long long le,
+                                  long long lout, long long ppc, long long p0, long long rows, float2* z,
+                                  hipStream_t s);
+hipError_t launch_fir_long_mul(float2* Z, const float2* H, long long nfft, long long rows, hipStream_t s);
+hipError_t launch_fir_long_scatter(const float2* z, float* y, long long n, long long y_stride, long long nfft,
+                                   long long le, long long lout, long long ppc, long long p0, long long rows,
+                                   hipStream_t s);
 hipError_t launch_scale_real(float* p, long long count, float s, hipStream_t st);
 hipError_t launch_scale_cpx(float2* p, long long count, float s, hipStream_t st);
 
@@ -134,6 +144,10 @@ hipError_t launch_scale_cpx(float2* p, long long count, float s, hipStream_t st)
 // single-pass analytic signal / DCT-II (analytic_kernels.hip): rows [batch][n]
 bool hilbert_fused_supported(long long n);
 hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long long batch, hipStream_t s);
+// instantaneous phase / frequency rows (phase_kernels.hip, hilbert.c:77-113)
+hipError_t launch_inst_phase(const float2* z, long long n, long long batch, float* phase, hipStream_t s);
+hipError_t launch_inst_freq(const float* phase, long long n, long long batch, double scale, float* freq,
+                            hipStream_t s);
 bool dct2_fused_supported(long long n);
 hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long batch, int policy, hipStream_t s);
 hipError_t launch_hilbert_mask(long long n, const float2* half, float2* full, long long batch,

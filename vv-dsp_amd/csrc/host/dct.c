@@ -15,9 +15,10 @@ struct vv_dsp_dct_plan {
     vv_dsp_dct_dir dir;
 };
 
-/* NaN policy global (reference src/core/nan_policy.c:14-31).  Weak so that the
- * reference's core module, when linked too, provides the single definition. */
-static vv_dsp_nan_policy_e g_policy = VV_DSP_NAN_POLICY_PROPAGATE;
+/* NaN policy, per thread as the reference's (src/core/nan_policy.c:11-31,
+ * _Thread_local under gnu99).  Weak so that the reference's core module, when
+ * linked too, provides the single definition. */
+static __thread vv_dsp_nan_policy_e g_policy = VV_DSP_NAN_POLICY_PROPAGATE;
 __attribute__((weak)) void vv_dsp_set_nan_policy(vv_dsp_nan_policy_e policy) {
     if (policy >= VV_DSP_NAN_POLICY_PROPAGATE && policy <= VV_DSP_NAN_POLICY_CLAMP) g_policy = policy;
 }

@@ -56,6 +56,8 @@ def lib():
     L.vv_dsp_stft_frames_range_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _sz, _sz, _vp, _sz, C.c_int, _vp]
     L.vv_dsp_stft_process_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.vv_dsp_stft_reconstruct_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp]
+    L.vv_dsp_instantaneous_phase_device.argtypes = [_vp, _sz, _sz, _vp, _vp]
+    L.vv_dsp_instantaneous_frequency_device.argtypes = [_vp, _sz, _sz, C.c_double, _vp, _vp]
     L.vv_dsp_fir_plan_create.argtypes = [_vp, _sz, C.POINTER(_vp)]
     L.vv_dsp_fir_plan_destroy.argtypes = [_vp]
     L.vv_dsp_fir_apply_fft_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]
@@ -91,6 +93,18 @@ def _stream(stream=None):
     return C.c_void_p(s.cuda_stream)
 
 
+def _expect(t, dtype, numel, what):
+    """A kernel trusts the sizes it is given: check a tensor against the plan
+    before its pointer goes down (too few elements would be read or written
+    past the allocation)."""
+    if t.dtype != dtype:
+        raise VvError(f"{what}: dtype {t.dtype}, expected {dtype}")
+    if t.numel() < numel:
+        raise VvError(f"{what}: {t.numel()} elements, the plan needs {numel}")
+    if not (t.is_cuda and t.is_contiguous()):
+        raise VvError(f"{what}: must be a contiguous device tensor")
+
+
 def device_count():
     return lib().vvhip_available()
 
@@ -106,13 +120,15 @@ class FftPlan:
     def __call__(self, x, out=None, stream=None):
         n, b = self.n, self.batch
         if self.kind == C2C:
-            shape, dt = (b, n), torch.complex64
+            shape, dt, in_dt, in_len = (b, n), torch.complex64, torch.complex64, n
         elif self.kind == R2C:
-            shape, dt = (b, n // 2 + 1), torch.complex64
+            shape, dt, in_dt, in_len = (b, n // 2 + 1), torch.complex64, torch.float32, n
         else:
-            shape, dt = (b, n), torch.float32
+            shape, dt, in_dt, in_len = (b, n), torch.float32, torch.complex64, n // 2 + 1
+        _expect(x, in_dt, b * in_len, "fft input")
         if out is None:
             out = torch.empty(shape, dtype=dt, device=x.device)
+        _expect(out, dt, shape[0] * shape[1], "fft output")
         _check(lib().vv_dsp_fft_execute_device(self.h, _ptr(x), _ptr(out), _stream(stream)), "fft_execute_device")
         return out
 
@@ -140,8 +156,11 @@ class Stft:
         nch, n = sig2.shape
         fr = self.frames(n)
         dt = torch.complex64 if complex_out else torch.float32
+        if sig2.dtype != torch.float32 or sig2.stride(1) != 1:
+            raise VvError("stft signal: float32 rows with unit sample stride")
         if out is None:
             out = torch.empty((nch, fr, self.nfft), dtype=dt, device=sig.device)
+        _expect(out, dt, nch * fr * self.nfft, "stft output")
         nf = _sz(0)
         f = lib().vv_dsp_stft_spectrum_device if complex_out else lib().vv_dsp_stft_spectrogram_device
         _check(f(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * self.nfft, _stream(stream),
@@ -154,8 +173,11 @@ class Stft:
         sig2 = sig if sig.dim() == 2 else sig.unsqueeze(0)
         nch, n = sig2.shape
         fr, nh = self.frames(n), self.nfft // 2 + 1
+        if sig2.dtype != torch.float32 or sig2.stride(1) != 1:
+            raise VvError("stft signal: float32 rows with unit sample stride")
         if out is None:
             out = torch.empty((nch, fr, nh), dtype=torch.float32, device=sig.device)
+        _expect(out, torch.float32, nch * fr * nh, "stft power output")
         nf = _sz(0)
         _check(lib().vv_dsp_stft_power_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * nh,
                                                _stream(stream), C.byref(nf)), "stft_power_device")
@@ -169,8 +191,11 @@ class Stft:
         nch, n = sig2.shape
         width = self.nfft // 2 + 1 if kind == 2 else self.nfft
         dt = torch.complex64 if kind == 1 else torch.float32
+        if sig2.dtype != torch.float32 or sig2.stride(1) != 1:
+            raise VvError("stft signal: float32 rows with unit sample stride")
         if out is None:
             out = torch.empty((nch, nframes, width), dtype=dt, device=sig.device)
+        _expect(out, dt, nch * nframes * width, "stft frames_range output")
         if nframes == 0 and frame0 <= self.frames(n):   # empty range: nothing to write (out has no storage)
             return out if sig.dim() == 2 else out[0]
         _check(lib().vv_dsp_stft_frames_range_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), frame0, nframes,
@@ -180,12 +205,21 @@ class Stft:
 
     def process(self, frames, stream=None):
         """frames: (count, nfft) float32 -> (count, nfft) complex64 (vv_dsp_stft_process batched)."""
+        _expect(frames, torch.float32, frames.shape[0] * self.nfft, "stft_process frames")
         out = torch.empty((frames.shape[0], self.nfft), dtype=torch.complex64, device=frames.device)
         _check(lib().vv_dsp_stft_process_device(self.h, _ptr(frames), frames.shape[0], _ptr(out),
                                                 _stream(stream)), "stft_process_device")
         return out
 
     def reconstruct(self, spec, out_add, norm_add=None, stream=None):
+        """spec: (count, nfft) complex64 frames at this handle's hop; adds into
+        out_add (and norm_add), each at least (count - 1) * hop + nfft long."""
+        count = spec.shape[0]
+        _expect(spec, torch.complex64, count * self.nfft, "stft_reconstruct spectra")
+        need = (count - 1) * self.hop + self.nfft if count else 0
+        _expect(out_add, torch.float32, need, "stft_reconstruct out_add")
+        if norm_add is not None:
+            _expect(norm_add, torch.float32, need, "stft_reconstruct norm_add")
         _check(lib().vv_dsp_stft_reconstruct_device(self.h, _ptr(spec), spec.shape[0], _ptr(out_add),
                                                     _ptr(norm_add) if norm_add is not None else None,
                                                     _stream(stream)), "stft_reconstruct_device")
@@ -257,6 +291,28 @@ def hilbert(x, stream=None):
     z = torch.empty((b, n), dtype=torch.complex64, device=x.device)
     _check(lib().vv_dsp_hilbert_analytic_device(_ptr(x2), n, b, _ptr(z), _stream(stream)), "hilbert_device")
     return z if x.dim() == 2 else z[0]
+
+
+def instantaneous_phase(z, stream=None):
+    """z: (batch, N) or (N,) complex64 analytic rows -> unwrapped phase float32 (hilbert.c:77-96)."""
+    z2 = z if z.dim() == 2 else z.unsqueeze(0)
+    b, n = z2.shape
+    _expect(z2, torch.complex64, b * n, "instantaneous_phase input")
+    p = torch.empty((b, n), dtype=torch.float32, device=z.device)
+    _check(lib().vv_dsp_instantaneous_phase_device(_ptr(z2), n, b, _ptr(p), _stream(stream)),
+           "instantaneous_phase_device")
+    return p if z.dim() == 2 else p[0]
+
+
+def instantaneous_frequency(phase, sample_rate, stream=None):
+    """phase: (batch, N) or (N,) float32 -> frequency in Hz, element 0 of a row = 0 (hilbert.c:98-113)."""
+    p2 = phase if phase.dim() == 2 else phase.unsqueeze(0)
+    b, n = p2.shape
+    _expect(p2, torch.float32, b * n, "instantaneous_frequency input")
+    f = torch.empty_like(p2)
+    _check(lib().vv_dsp_instantaneous_frequency_device(_ptr(p2), n, b, float(sample_rate), _ptr(f),
+                                                       _stream(stream)), "instantaneous_frequency_device")
+    return f if phase.dim() == 2 else f[0]
 
 
 def dct(x, dct_type=2, inverse=False, stream=None):
