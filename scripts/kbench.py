@@ -160,6 +160,25 @@ def case_stft_exp(e, nch=32, seconds=600):
         byts, (sig, win, out, lib)
 
 
+def case_lab(e, nch=32, seconds=600, fn="stftlab_run"):
+    """the product STFT kernel with parts switched off (scripts/stftlab.hip, EXP bits:
+    1 no FFT exchanges, 2 no FFT, 4 no row stores, 8 no span loads); bytes = the real job's"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
+    run = getattr(lib, fn)
+    run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
+                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    n = seconds * 48000
+    sig = torch.rand(nch, n, device="cuda") * 2 - 1
+    win = torch.hann_window(1024, periodic=False, device="cuda")
+    fr = (n - 1024 + 256) // 256 + 1
+    out = torch.empty(nch, fr, 1024, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    byts = nch * n * 4 + nch * fr * 1024 * 4
+    return (lambda: run(e, sig.data_ptr(), n, nch, win.data_ptr(), out.data_ptr(), s)), \
+        byts, (sig, win, out, lib)
+
+
 def case_rw(w, in_bytes=3686400000, blocks=4096):
     """streaming read 1 : write w (scripts/membench.hip k_rw), 16 B/lane, nt"""
     import ctypes
@@ -263,6 +282,8 @@ CASES = {
     "r2c1024": lambda: case_r2c(1024, 131072),
     "c2r1024": lambda: case_c2r(1024, 131072),
     "stft": lambda: case_stft(32, 600),
+    **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
+                                                                         128, 256, 512, 1024, 640, 1152]},
     "stft60": lambda: case_stft(1, 60),
     "stftpow": lambda: case_stft_power(32, 600),
     "stftpowold": with_env(lambda: case_stft_power(32, 600), "VVHIP_POW_OLD", "1"),
@@ -285,7 +306,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw", "lab", "model"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

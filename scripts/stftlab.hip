@@ -1,0 +1,39 @@
+// stftlab.hip -- timing ablations of the product STFT kernel (not part of the
+// product; built into scripts/libstftlab.so by `make -C vv-dsp_amd lab`).
+// Includes the product sources so the kernel under test is byte-for-byte the
+// library's k_stft_pair<1024, 0, 0, EXP>; EXP bits (stft_kernels.hip): 1 FFT
+// without LDS exchanges, 2 no FFT, 4 no row stores, 8 no span loads,
+// 16 rows as 16 B/lane stores (garbage values), 32 plain instead of streaming stores.
+#include "../vv-dsp_amd/csrc/hip/tables.hip"
+#include "../vv-dsp_amd/csrc/hip/stft_kernels.hip"
+
+namespace vvh {
+template <int EXP>
+static hipError_t lab_launch(const float* sig, long long n, long long nch, const float* win, float* out,
+                             hipStream_t s) {
+    constexpr int N = 1024, F = Wg<N>::F;
+    const long long hop = 256, frames = n < N ? 1 : 1 + (n - N + hop) / hop, ppc = (frames + 1) / 2;
+    static std::atomic<int> cap;
+    const int cap0 = cached_grid(cap, (const void*)k_stft_pair<N, 0, 0, EXP>, 256, 0, 1LL << 40);
+    const long long pairs = nch * ppc;
+    long long cps = (pairs + (long long)F * cap0 - 1) / ((long long)F * cap0);
+    cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
+    const long long chunk = cps * F, grid = (pairs + chunk - 1) / chunk;
+    hipLaunchKernelGGL((k_stft_pair<N, 0, 0, EXP>), dim3((unsigned)grid), dim3(256), 0, s, sig, n, nch, n, frames, hop,
+                       0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, store_sink());
+    return hipGetLastError();
+}
+}  // namespace vvh
+
+extern "C" int stftlab_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
+                           void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (exp) {
+#define C(E) case E: return (int)vvh::lab_launch<E>(sig, n, nch, win, out, s);
+        C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
+        C(16) C(18) C(24) C(26) C(32) C(34) C(40) C(42) C(64) C(66) C(68) C(80) C(82)
+        C(128) C(256) C(512) C(1024) C(640) C(1152)
+#undef C
+        default: return -1;
+    }
+}

@@ -71,6 +71,18 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return upk(pk(a) *
 __device__ __forceinline__ float2 cmul_mi(float2 a) { return upk(pk(a).yx * vf2_t{1.0f, -1.0f}); }
 __device__ __forceinline__ float2 cmul_pi(float2 a) { return upk(pk(a).yx * vf2_t{-1.0f, 1.0f}); }
 
+// x * (w.lo, w.lo) (HI = 0) or x * (w.hi, w.hi) (HI = 1) as one v_pk_mul_f32
+// with op_sel: a packed pair of per-register constants (two window values)
+// then costs one VGPR each.  Written out because the SLP vectorizer otherwise
+// materialises (w, w) duplicates -- 16 extra VGPRs for a 16-point window.
+template <int HI>
+__device__ __forceinline__ vf2_t pk_mul_bcast(vf2_t x, vf2_t w) {
+    vf2_t r;
+    if constexpr (HI) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(x), "v"(w));
+    else asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(x), "v"(w));
+    return r;
+}
+
 // Streaming (non-temporal) global accesses: data touched exactly once.
 __device__ __forceinline__ float2 ld_nt(const float2* p) {
     const vf2_t v = __builtin_nontemporal_load(reinterpret_cast<const vf2_t*>(p));
@@ -379,15 +391,83 @@ __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
 // groups; the b64 padding G::pad costs 2x on every read), and keep all
 // compile-time offsets additive.  Largest index 1075 < G::LDS.
 template <int N, int p>
-__device__ __forceinline__ constexpr int ri_pad(int e) {
+__host__ __device__ constexpr int ri_pad(int e) {
     if constexpr (N == 1024 && p == 0) return e + (e >> 5);
     else if constexpr (N == 1024 && p == 1) return e + 4 * (e >> 7) + 8 * (e >> 8);
     else return Geo<N>::pad(e);
 }
 
+// N = 1024 (passes 16, 16, 4): ri_pad<1024, p> of every exchange access as a
+// lane base plus a compile-time offset, so each access is one ds_write/ds_read
+// with an immediate offset off a few base registers.  (Left to itself the
+// compiler keeps one padded address per access live across the loop: 16+
+// VGPRs.)  Derivations (b: the butterfly, r: its register):
+//   p 0 writes  16b + r             -> (16b + (b>>1)) + r
+//   p 0 reads   b + 64r   (b < 64)  -> (b + (b>>5)) + 66r
+//   p 1 writes  256(b>>4) + (b&15) + 16r -> (272(b>>4) + (b&15)) + 16r + 4[r>=8]
+//   p 1 reads   b + 256r  (b < 256) -> (b + 4(b>>7)) + 272r
+struct Ri1024 {
+    template <int p>
+    __device__ __forceinline__ static int wbase(int b) {
+        return p == 0 ? 16 * b + (b >> 1) : 272 * (b >> 4) + (b & 15);
+    }
+    template <int p>
+    __host__ __device__ static constexpr int woff(int r) {
+        return p == 0 ? r : 16 * r + (r >= 8 ? 4 : 0);
+    }
+    template <int p>
+    __device__ __forceinline__ static int rbase(int b) {
+        return p == 0 ? b + (b >> 5) : b + 4 * (b >> 7);
+    }
+    template <int p>
+    __host__ __device__ static constexpr int roff(int r) {
+        return p == 0 ? 66 * r : 272 * r;
+    }
+};
+__host__ __device__ constexpr bool ri1024_check() {
+    for (int b = 0; b < 64; ++b)
+        for (int r = 0; r < 16; ++r) {
+            if (ri_pad<1024, 0>(16 * b + r) != 16 * b + (b >> 1) + Ri1024::woff<0>(r)) return false;
+            if (ri_pad<1024, 0>(b + 64 * r) != b + (b >> 5) + Ri1024::roff<0>(r)) return false;
+            const int e = 256 * (b >> 4) + (b & 15) + 16 * r;
+            if (ri_pad<1024, 1>(e) != 272 * (b >> 4) + (b & 15) + Ri1024::woff<1>(r)) return false;
+        }
+    for (int b = 0; b < 256; ++b)
+        for (int r = 0; r < 4; ++r)
+            if (ri_pad<1024, 1>(b + 256 * r) != b + 4 * (b >> 7) + Ri1024::roff<1>(r)) return false;
+    return true;
+}
+static_assert(ri1024_check(), "Ri1024 decomposition of ri_pad");
+
 template <int N, int p, bool PAIRED>
 __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
     using G = Geo<N>;
+    if constexpr (N == 1024) {
+        constexpr int R = G::radix(p), R2 = G::radix(p + 1);
+        static_assert(R == 16 && G::P / R == 1, "N = 1024: one radix-16 butterfly per thread before the exchange");
+        float nx[G::P];
+        const int wb = Ri1024::wbase<p>(bfly<N, p, PAIRED>(t, 0));
+        int rb[G::P / R2];
+#pragma unroll
+        for (int i = 0; i < G::P / R2; ++i) rb[i] = Ri1024::rbase<p>(bfly<N, p + 1, PAIRED>(t, i));
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[wb + Ri1024::woff<p>(r)] = v[r].x;
+        xsync<G::T>();
+#pragma unroll
+        for (int i = 0; i < G::P / R2; ++i)
+#pragma unroll
+            for (int r = 0; r < R2; ++r) nx[i * R2 + r] = lds[rb[i] + Ri1024::roff<p>(r)];
+        xsync<G::T>();
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[wb + Ri1024::woff<p>(r)] = v[r].y;
+        xsync<G::T>();
+#pragma unroll
+        for (int i = 0; i < G::P / R2; ++i)
+#pragma unroll
+            for (int r = 0; r < R2; ++r)
+                v[i * R2 + r] = make_float2(nx[i * R2 + r], lds[rb[i] + Ri1024::roff<p>(r)]);
+        return;
+    }
     constexpr int R = G::radix(p), Ns = G::ns(p), R2 = G::radix(p + 1);
     float nx[G::P];
 #pragma unroll
@@ -422,15 +502,18 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
     if constexpr (G::T > 64) xsync<G::T>();
 }
 
-template <int N, bool FWD, int p, bool PAIRED, bool RI = false>
+// NOX: timing ablation only (scripts/membench.hip) -- the passes without their
+// exchanges, i.e. a wrong transform with the FFT's arithmetic but no LDS traffic.
+template <int N, bool FWD, int p, bool PAIRED, bool RI = false, bool NOX = false>
 struct PassChain {
     template <class TW>
     __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TW& tw) {
         pass_compute<N, FWD, p, PAIRED>(v, t, tw);
         if constexpr (p + 1 < Geo<N>::NPASS) {
-            if constexpr (RI) pass_exchange_ri<N, p, PAIRED>(v, t, reinterpret_cast<float*>(lds));
+            if constexpr (NOX) asm volatile("" ::: "memory");
+            else if constexpr (RI) pass_exchange_ri<N, p, PAIRED>(v, t, reinterpret_cast<float*>(lds));
             else pass_exchange<N, p, PAIRED>(v, t, lds);
-            PassChain<N, FWD, p + 1, PAIRED, RI>::run(v, t, lds, tw);
+            PassChain<N, FWD, p + 1, PAIRED, RI, NOX>::run(v, t, lds, tw);
         }
     }
 };
@@ -438,10 +521,10 @@ struct PassChain {
 // Full transform.  On entry v[r] = x[t + r*T] (r < P).  On exit register q
 // holds X[out_pos<N, PAIRED>(t, q)].  RI: `lds` needs only Geo<N>::LDS floats
 // (pass_exchange_ri) instead of Geo<N>::LDS float2.
-template <int N, bool FWD, bool PAIRED = false, bool RI = false, class TW = TwTab<N>>
+template <int N, bool FWD, bool PAIRED = false, bool RI = false, class TW = TwTab<N>, bool NOX = false>
 __device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TW& tw) {
     static_assert(!PAIRED || Geo<N>::CAN_PAIR, "mirror pairing needs >= 2 last-pass butterflies per thread");
-    PassChain<N, FWD, 0, PAIRED, RI>::run(v, t, lds, tw);
+    PassChain<N, FWD, 0, PAIRED, RI, NOX>::run(v, t, lds, tw);
 }
 
 // ---- shared pieces of the persistent streaming kernels ---------------------
@@ -473,6 +556,26 @@ __device__ __forceinline__ void glds16(const float* gsrc, float* lds_dst) {
                  : "=&s"(keep)
                  : "v"(gsrc), "s"(l)
                  : "memory");
+}
+// the same with a cache-policy suffix (timing ablations: "nt", "sc1", "sc0 sc1 nt")
+template <int POL>
+__device__ __forceinline__ void glds16_pol(const float* gsrc, float* lds_dst) {
+    const unsigned l = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_dst);
+    unsigned keep;
+    if constexpr (POL == 1)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(l) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(l) : "memory");
+}
+template <int IMM, int POL>
+__device__ __forceinline__ void st4_pol_sbase(unsigned lane_off, float v, const void* base) {
+    if constexpr (POL == 1)
+        asm volatile("global_store_dword %0, %1, %2 offset:%3 sc1" ::"v"(lane_off), "v"(v), "s"(base), "n"(IMM) : "memory");
+    else
+        asm volatile("global_store_dword %0, %1, %2 offset:%3 sc0 sc1 nt" ::"v"(lane_off), "v"(v), "s"(base), "n"(IMM)
+                     : "memory");
 }
 // The trailing s_nop covers the gfx9 hazard "VALU write of a >8-byte VMEM
 // store's data VGPRs right after the store", which hipcc does not model for asm.

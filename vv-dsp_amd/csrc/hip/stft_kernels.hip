@@ -99,6 +99,166 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
     } else *(reinterpret_cast<float2*>(row) + k) = X;
 }
 
+// Rows of one frame pair straight from the FFT registers (N = 1024: one wave
+// per transform, mirror-paired last pass; see k_stft_pair).  Issues exactly
+// the kernel's NST stores per pair (rows of a missing second frame go to the
+// sink), so the caller's hand-counted vmcnt stays exact.
+template <int N, int MODE, int EXP>
+__device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, char* rowb, bool has_b,
+                                            float* sink) {
+    using G = Geo<N>;
+    using Mi = Mirror<N>;
+    constexpr int R = G::RL;
+    if constexpr (MODE == 1) {
+        // as the DIRECT block below, with complex bins: a mirror block holds
+        // conj(X[k]) (real frames), lane 0's rotated partner conj of its own
+        // bin in slot j + 1, or in the last slot its self-mirrored bin as is.
+        // Byte offsets reach 8 KB: blocks past 4 KB use the base + 4096.
+        constexpr int J = G::NPT / 2, NB = G::NB, T = G::T;
+        const unsigned ve = 8u * (unsigned)t;
+        const unsigned vo = 8u * (unsigned)(t == 0 ? 0 : T - t);
+        const char* ra = rowa;
+        const char* rb = has_b ? rowb : reinterpret_cast<const char*>(sink);   // counted stores must all issue
+        const char* ra2 = ra + 4096;
+        const char* rb2 = rb + 4096;
+        auto st = [&](auto imm, unsigned off, float2 val, const char* b1, const char* b2) {
+            constexpr int I = decltype(imm)::value;
+            if constexpr (I < 4096) st8_nt_sbase<I>(off, val, b1);
+            else st8_nt_sbase<I - 4096>(off, val, b2);
+        };
+        float2 nxa[R], nxb[R];   // lane 0's partner values for slot j: conj of slot j+1's own bins
+        static_for<0, J>([&](auto jc) {
+            constexpr int j = J - 1 - decltype(jc)::value;   // last slot first: its partners are the specials
+            static_for<0, R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                constexpr int q = 2 * j * R + r;
+                float2 A, B;
+                pair_post<1>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                float2 pa, pb;
+                if constexpr (j == J - 1) {
+                    const int qm = Mi::normal(r);
+                    pair_post<1>(v[qm], v[Mi::special(qm)], &pa, &pb);
+                } else {
+                    pa = nxa[r];
+                    pb = nxb[r];
+                }
+                const float2 oa = select2(t == 0, pa, cconj(A)), ob = select2(t == 0, pb, cconj(B));
+                nxa[r] = cconj(A);
+                nxb[r] = cconj(B);
+                constexpr int IE = 8 * (T * j + r * NB), IO = 8 * ((R - 1 - r) * NB - T * j + NB - T);
+                st(std::integral_constant<int, IE>{}, ve, A, ra, ra2);
+                st(std::integral_constant<int, IE>{}, ve, B, rb, rb2);
+                st(std::integral_constant<int, IO>{}, vo, oa, ra, ra2);
+                st(std::integral_constant<int, IO>{}, vo, ob, rb, rb2);
+            });
+        });
+    } else {
+        // Even slot j holds bins k = t + T j + r NB (lane-contiguous, 256 B
+        // aligned per store); its partner slot holds N - k, which for lanes
+        // t >= 1 covers N - k of the same magnitude.  Lane 0's partner bins
+        // are shifted by one slot (lane 0 writes the mirror of its own bin in
+        // slot j + 1, or its self-mirrored bin NB/2 + .. in the last slot), so
+        // that every store instruction covers one aligned 256 B block: full
+        // 128 B lines for the streaming stores, no LDS staging.
+        constexpr int J = G::NPT / 2, NB = G::NB, T = G::T;
+        constexpr int PM = MODE == 2 ? 2 : 0;   // magnitude or power post
+        float ea[J][R], eb[J][R], sa[R], sb[R];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int q = 2 * j * R + r;
+                float2 A, B;
+                pair_post<PM>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                ea[j][r] = A.x;
+                eb[j][r] = B.x;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {   // lane 0's odd slot 1: bins NB/2 + (R-1-r) NB, their own mirrors
+            const int qm = Mi::normal(r);
+            float2 A2, B2;
+            pair_post<PM>(v[qm], v[Mi::special(qm)], &A2, &B2);
+            sa[r] = A2.x;
+            sb[r] = B2.x;
+        }
+        const unsigned ve = 4u * (unsigned)t;
+        const unsigned vo = 4u * (unsigned)(t == 0 ? NB - T : NB - t);
+        const void* ra = rowa;
+        const void* rb = has_b ? rowb : (void*)sink;   // counted stores must all issue
+        // Power rows (n/2+1 floats, so not line-aligned): a block is stored
+        // only if it lies below N/2, with plain stores (partial lines merge
+        // in L2; streaming stores of partial lines measured 1.65x slower)
+        auto st = [&](auto imm, unsigned off, float val, const void* base) {
+            constexpr int I = decltype(imm)::value;
+            if constexpr (EXP & 4) {
+                asm volatile("" ::"v"(val));
+            } else if constexpr (MODE == 2) {
+                if constexpr (I < 4 * (N / 2)) st4_sbase<I>(off, val, base);
+            } else {
+                if constexpr (EXP & 512) st4_pol_sbase<I, 1>(off, val, base);
+                else if constexpr (EXP & 1024) st4_pol_sbase<I, 2>(off, val, base);
+                else st4_nt_sbase<I>(off, val, base);
+            }
+        };
+        // The N/T blocks of a row in ascending address order, row a then
+        // row b (measured 0.5 % faster than interleaving the rows).  Block
+        // m is an even block (slot j = m % (NB/T) < J, r = m / (NB/T)) or
+        // the mirror block of (j, r) with (N/T - 1) - m = r (NB/T) + j.
+        auto val = [&](auto mc, const float (&e)[J][R], const float (&sp)[R]) -> float {
+            constexpr int m = decltype(mc)::value;
+            constexpr int je = m % (NB / T), re = m / (NB / T);
+            if constexpr (je < J) {
+                return e[je][re];
+            } else {
+                constexpr int mm = (N / T - 1) - m, rm = mm / (NB / T), jm = mm % (NB / T);
+                if constexpr (jm + 1 < J) return t == 0 ? e[jm + 1][rm] : e[jm][rm];
+                else return t == 0 ? sp[rm] : e[jm][rm];
+            }
+        };
+        auto row = [&](const float (&e)[J][R], const float (&sp)[R], const void* base) {
+            static_for<0, N / T>([&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                if constexpr (m % (NB / T) < J) st(std::integral_constant<int, 4 * T * m>{}, ve, val(mc, e, sp), base);
+                else st(std::integral_constant<int, 4 * T * m>{}, vo - 4u * (NB - T), val(mc, e, sp), base);
+            });
+        };
+        if constexpr (EXP & 16) {
+            // ablation: the same 8 KB as 8 x 16 B/lane streaming stores (values garbage)
+            static_assert(MODE == 0, "store-count bookkeeping (NST = 8)");
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const vf4_t va = {ea[0][u], ea[1][u], sa[u], eb[0][u]};
+                const vf4_t vb = {eb[1][u], sb[u], ea[0][u], eb[0][u]};
+                st16_nt_counted(reinterpret_cast<vf4_t*>(const_cast<void*>(ra)) + u * 64 + t, va);
+                st16_nt_counted(reinterpret_cast<vf4_t*>(const_cast<void*>(rb)) + u * 64 + t, vb);
+            }
+        } else if constexpr (EXP & 32) {
+            // ablation: plain (write-back) dword stores instead of streaming ones
+            auto rowp = [&](const float (&e)[J][R], const float (&sp)[R], const void* base) {
+                static_for<0, N / T>([&](auto mc) {
+                    constexpr int m = decltype(mc)::value;
+                    if constexpr (m % (NB / T) < J) st4_sbase<4 * T * m>(ve, val(mc, e, sp), base);
+                    else st4_sbase<4 * T * m>(vo - 4u * (NB - T), val(mc, e, sp), base);
+                });
+            };
+            rowp(ea, sa, ra);
+            rowp(eb, sb, rb);
+        } else {
+            row(ea, sa, ra);
+            row(eb, sb, rb);
+        }
+        if constexpr (MODE == 2) {
+            // bin N/2 = NB * (R/2): even slot j = 0, r = R/2, lane 0; the
+            // other lanes' copies go to the sink (one store per row, counted)
+            static_assert(N / 2 == NB * (R / 2), "Nyquist bin in lane 0 of an even block");
+            float* const sk = sink + 8192 + t;
+            st4_counted(t == 0 ? (float*)ra + N / 2 : sk, ea[0][R / 2]);
+            st4_counted(t == 0 ? (float*)rb + N / 2 : sk, eb[0][R / 2]);
+        }
+    }
+}
+
 // Frame pairs (2j, 2j+1) of one channel, j in [pair0, pair0 + ppc): pairs never
 // span channels, so a channel's rows do not depend on how channels are grouped
 // into calls or shards.
@@ -107,7 +267,14 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
 //   VAR 1: bulk, stores straight from registers
 //   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
 // N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
-template <int N, int MODE, int VAR>
+// EXP: timing ablations for scripts/membench.hip only (the library instantiates
+// EXP = 0): bit 0 FFT without its LDS exchanges, bit 1 no FFT, bit 2 no row
+// stores, bit 3 no span loads, bit 4 the rows as 16 B/lane stores, bit 5 plain
+// instead of streaming row stores, bit 6 only the 2 hop new samples of a span
+// (the HBM traffic of a ring, the LDS-DMA count of one), bits 7/8 span DMA
+// with nt / sc1, bits 9/10 row stores with sc1 / sc0 sc1 nt.  Results are
+// wrong under bits 0-4 and 6.
+template <int N, int MODE, int VAR, int EXP = 0>
 __global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && VAR == 0) ? 3 : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
@@ -115,12 +282,13 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     using G = Geo<N>;
     using Mi = Mirror<N>;
     constexpr bool TAIL = VAR == 2;
-    constexpr bool STAGE = VAR == 0 && MODE == 0 && G::NPASS > 1 && G::T > 1;
+    constexpr bool BULK = VAR == 0;
+    constexpr bool STAGE = BULK && MODE == 0 && G::NPASS > 1 && G::T > 1;
     // power rows (N = 1024): the DIRECT stores below, keeping only the
     // 64-bin blocks under N/2 plus one lane for bin N/2
-    constexpr bool POWD = VAR == 0 && MODE == 2 && G::T == 64 && G::NPASS > 1;
+    constexpr bool POWD = BULK && MODE == 2 && G::T == 64 && G::NPASS > 1;
     // complex rows (N = 1024): DIRECT with 8 B/lane stores, conj() for the mirror blocks
-    constexpr bool CPXD = VAR == 0 && MODE == 1 && G::T == 64 && G::NPASS > 1;
+    constexpr bool CPXD = BULK && MODE == 1 && G::T == 64 && G::NPASS > 1;
     constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
     constexpr int SPAN = GLDS ? N + N / 2 : 1;   // floats per transform: hop <= N/2
     // T == 64 (one wave per transform): magnitudes go straight from registers as
@@ -128,7 +296,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // written as 16 B/lane stores
     constexpr bool DIRECT = GLDS && G::T == 64;
     // stores per pair (both rows): power rows keep half the blocks + bin N/2
-    constexpr int NST = DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
+    constexpr int NST = (EXP & 4) ? 0 : (EXP & 16) ? 8 : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
@@ -141,9 +309,14 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
-    float w[G::P];
+    // window values 0.5 w[t + r T], packed two per VGPR pair (pk_mul_bcast)
+    vf2_t wp[(G::P + 1) / 2];
 #pragma unroll
-    for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * G::T];
+    for (int r = 0; r < G::P; ++r) {
+        const float wr = 0.5f * win[t + r * G::T];
+        if (r & 1) wp[r / 2].y = wr;
+        else wp[r / 2] = vf2_t{wr, 0.0f};
+    }
 
     int kb[G::NPT];   // last-pass butterfly of each slot (loop invariant)
 #pragma unroll
@@ -216,9 +389,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         const float* s0 = sig + cc * ch_stride + ff * hop;
         const int len = (int)(N + hop), lane = t & 63;
         if (ff * hop + len <= n) {
-            for (int u = t >> 6; u * 256 < len; u += G::T / 64) {
+            for (int u = t >> 6; u * 256 < ((EXP & 64) ? 2 * (int)hop : len); u += G::T / 64) {
                 const int e = u * 256 + lane * 4;
-                glds16(s0 + (e < len ? e : 0), span + u * 256);
+                if constexpr (EXP & 128) glds16_pol<1>(s0 + (e < len ? e : 0), span + u * 256);
+                else if constexpr (EXP & 256) glds16_pol<2>(s0 + (e < len ? e : 0), span + u * 256);
+                else glds16(s0 + (e < len ? e : 0), span + u * 256);
             }
         } else {
             const long long left = n - ff * hop;   // samples of this span inside the signal
@@ -232,7 +407,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         }
     };
     auto load_pair = [&](long long cc, long long ff) {
-        if constexpr (GLDS) {
+        if constexpr (EXP & 8) {
+        } else if constexpr (GLDS) {
             issue_span(cc, ff);
         } else if constexpr (TAIL) {
             const float* s = sig + cc * ch_stride;
@@ -273,137 +449,22 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         }
         float2 v[G::P];
 #pragma unroll
-        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
+        for (int r = 0; r < G::P; ++r) {
+            const vf2_t x = {xa[r], xb[r]};
+            v[r] = upk((r & 1) ? pk_mul_bcast<1>(x, wp[r / 2]) : pk_mul_bcast<0>(x, wp[r / 2]));
+        }
         if constexpr (GLDS) {
         } else if constexpr (TAIL) {
             if (more) load_pair(cn, fn);
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
-        fft_regs<N, true, true, RI>(v, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, true, true, RI, TwTab<N>, (EXP & 1) != 0>(v, t, my, tw);
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
         char* rowb = rowa + ROW * ES;
         const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
-        if constexpr (DIRECT && MODE == 1) {
-            // as the DIRECT block below, with complex bins: a mirror block holds
-            // conj(X[k]) (real frames), lane 0's rotated partner conj of its own
-            // bin in slot j + 1, or in the last slot its self-mirrored bin as is.
-            // Byte offsets reach 8 KB: blocks past 4 KB use the base + 4096.
-            constexpr int J = G::NPT / 2, NB = G::NB, T = G::T;
-            const unsigned ve = 8u * (unsigned)t;
-            const unsigned vo = 8u * (unsigned)(t == 0 ? 0 : T - t);
-            const char* ra = rowa;
-            const char* rb = has_b ? rowb : reinterpret_cast<const char*>(sink);   // counted stores must all issue
-            const char* ra2 = ra + 4096;
-            const char* rb2 = rb + 4096;
-            auto st = [&](auto imm, unsigned off, float2 val, const char* b1, const char* b2) {
-                constexpr int I = decltype(imm)::value;
-                if constexpr (I < 4096) st8_nt_sbase<I>(off, val, b1);
-                else st8_nt_sbase<I - 4096>(off, val, b2);
-            };
-            float2 nxa[R], nxb[R];   // lane 0's partner values for slot j: conj of slot j+1's own bins
-            static_for<0, J>([&](auto jc) {
-                constexpr int j = J - 1 - decltype(jc)::value;   // last slot first: its partners are the specials
-                static_for<0, R>([&](auto rc) {
-                    constexpr int r = decltype(rc)::value;
-                    constexpr int q = 2 * j * R + r;
-                    float2 A, B;
-                    pair_post<1>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
-                    float2 pa, pb;
-                    if constexpr (j == J - 1) {
-                        const int qm = Mi::normal(r);
-                        pair_post<1>(v[qm], v[Mi::special(qm)], &pa, &pb);
-                    } else {
-                        pa = nxa[r];
-                        pb = nxb[r];
-                    }
-                    const float2 oa = select2(t == 0, pa, cconj(A)), ob = select2(t == 0, pb, cconj(B));
-                    nxa[r] = cconj(A);
-                    nxb[r] = cconj(B);
-                    constexpr int IE = 8 * (T * j + r * NB), IO = 8 * ((R - 1 - r) * NB - T * j + NB - T);
-                    st(std::integral_constant<int, IE>{}, ve, A, ra, ra2);
-                    st(std::integral_constant<int, IE>{}, ve, B, rb, rb2);
-                    st(std::integral_constant<int, IO>{}, vo, oa, ra, ra2);
-                    st(std::integral_constant<int, IO>{}, vo, ob, rb, rb2);
-                });
-            });
-        } else if constexpr (DIRECT) {
-            // Even slot j holds bins k = t + T j + r NB (lane-contiguous, 256 B
-            // aligned per store); its partner slot holds N - k, which for lanes
-            // t >= 1 covers N - k of the same magnitude.  Lane 0's partner bins
-            // are shifted by one slot (lane 0 writes the mirror of its own bin in
-            // slot j + 1, or its self-mirrored bin NB/2 + .. in the last slot), so
-            // that every store instruction covers one aligned 256 B block: full
-            // 128 B lines for the streaming stores, no LDS staging.
-            constexpr int J = G::NPT / 2, NB = G::NB, T = G::T;
-            constexpr int PM = MODE == 2 ? 2 : 0;   // magnitude or power post
-            float ea[J][R], eb[J][R], sa[R], sb[R];
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int q = 2 * j * R + r;
-                    float2 A, B;
-                    pair_post<PM>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
-                    ea[j][r] = A.x;
-                    eb[j][r] = B.x;
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {   // lane 0's odd slot 1: bins NB/2 + (R-1-r) NB, their own mirrors
-                const int qm = Mi::normal(r);
-                float2 A2, B2;
-                pair_post<PM>(v[qm], v[Mi::special(qm)], &A2, &B2);
-                sa[r] = A2.x;
-                sb[r] = B2.x;
-            }
-            const unsigned ve = 4u * (unsigned)t;
-            const unsigned vo = 4u * (unsigned)(t == 0 ? NB - T : NB - t);
-            const void* ra = rowa;
-            const void* rb = has_b ? rowb : (void*)sink;   // counted stores must all issue
-            // Power rows (n/2+1 floats, so not line-aligned): a block is stored
-            // only if it lies below N/2, with plain stores (partial lines merge
-            // in L2; streaming stores of partial lines measured 1.65x slower)
-            auto st = [&](auto imm, unsigned off, float val, const void* base) {
-                constexpr int I = decltype(imm)::value;
-                if constexpr (MODE == 2) {
-                    if constexpr (I < 4 * (N / 2)) st4_sbase<I>(off, val, base);
-                } else {
-                    st4_nt_sbase<I>(off, val, base);
-                }
-            };
-            // The N/T blocks of a row in ascending address order, row a then
-            // row b (measured 0.5 % faster than interleaving the rows).  Block
-            // m is an even block (slot j = m % (NB/T) < J, r = m / (NB/T)) or
-            // the mirror block of (j, r) with (N/T - 1) - m = r (NB/T) + j.
-            auto val = [&](auto mc, const float (&e)[J][R], const float (&sp)[R]) -> float {
-                constexpr int m = decltype(mc)::value;
-                constexpr int je = m % (NB / T), re = m / (NB / T);
-                if constexpr (je < J) {
-                    return e[je][re];
-                } else {
-                    constexpr int mm = (N / T - 1) - m, rm = mm / (NB / T), jm = mm % (NB / T);
-                    if constexpr (jm + 1 < J) return t == 0 ? e[jm + 1][rm] : e[jm][rm];
-                    else return t == 0 ? sp[rm] : e[jm][rm];
-                }
-            };
-            auto row = [&](const float (&e)[J][R], const float (&sp)[R], const void* base) {
-                static_for<0, N / T>([&](auto mc) {
-                    constexpr int m = decltype(mc)::value;
-                    if constexpr (m % (NB / T) < J) st(std::integral_constant<int, 4 * T * m>{}, ve, val(mc, e, sp), base);
-                    else st(std::integral_constant<int, 4 * T * m>{}, vo - 4u * (NB - T), val(mc, e, sp), base);
-                });
-            };
-            row(ea, sa, ra);
-            row(eb, sb, rb);
-            if constexpr (MODE == 2) {
-                // bin N/2 = NB * (R/2): even slot j = 0, r = R/2, lane 0; the
-                // other lanes' copies go to the sink (one store per row, counted)
-                static_assert(N / 2 == NB * (R / 2), "Nyquist bin in lane 0 of an even block");
-                float* const sk = sink + 8192 + t;
-                st4_counted(t == 0 ? (float*)ra + N / 2 : sk, ea[0][R / 2]);
-                st4_counted(t == 0 ? (float*)rb + N / 2 : sk, eb[0][R / 2]);
-            }
+        if constexpr (DIRECT) {
+            direct_rows<N, MODE, EXP>(v, t, rowa, rowb, has_b, sink);
         } else if constexpr (STAGE) {
             // both magnitude rows through the (now idle) exchange buffer, then
             // full-line 16 B/lane streaming stores: 2N/(4T) instead of 2P per lane
