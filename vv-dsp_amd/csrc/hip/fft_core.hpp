@@ -387,12 +387,20 @@ __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
 // instead of b64), half the LDS footprint -- for kernels whose occupancy is
 // bounded by LDS.
 // Per-exchange padding of the dword layout: for N = 1024 (passes 16, 16, 4)
-// these make both b32 exchanges bank-conflict-free (64 banks of 4 B, 32-lane
-// groups; the b64 padding G::pad costs 2x on every read), and keep all
-// compile-time offsets additive.  Largest index 1075 < G::LDS.
+// these make both exchanges bank-conflict-free and keep all compile-time
+// offsets additive.  After pass 0 a thread's 16 outputs are contiguous, so
+// they go out as four ds_write_b128 (8-lane groups, 32 banks: the pad
+// 4 (e >> 5) puts the 8 lanes' 16 B chunks on distinct banks) and are read
+// back as b32 (32-lane groups, conflict-free for the same pad).  Largest index
+// 1147: the buffer is ri_floats<N>() floats, 16 B aligned.
+// floats of one transform's pass_exchange_ri buffer
+template <int N>
+__host__ __device__ constexpr int ri_floats() {
+    return N == 1024 ? 1148 : Geo<N>::LDS;
+}
 template <int N, int p>
 __host__ __device__ constexpr int ri_pad(int e) {
-    if constexpr (N == 1024 && p == 0) return e + (e >> 5);
+    if constexpr (N == 1024 && p == 0) return e + 4 * (e >> 5);
     else if constexpr (N == 1024 && p == 1) return e + 4 * (e >> 7) + 8 * (e >> 8);
     else return Geo<N>::pad(e);
 }
@@ -402,14 +410,14 @@ __host__ __device__ constexpr int ri_pad(int e) {
 // with an immediate offset off a few base registers.  (Left to itself the
 // compiler keeps one padded address per access live across the loop: 16+
 // VGPRs.)  Derivations (b: the butterfly, r: its register):
-//   p 0 writes  16b + r             -> (16b + (b>>1)) + r
-//   p 0 reads   b + 64r   (b < 64)  -> (b + (b>>5)) + 66r
+//   p 0 writes  16b + r             -> (16b + 4(b>>1)) + r   (16 B aligned base)
+//   p 0 reads   b + 64r   (b < 64)  -> (b + 4(b>>5)) + 72r
 //   p 1 writes  256(b>>4) + (b&15) + 16r -> (272(b>>4) + (b&15)) + 16r + 4[r>=8]
 //   p 1 reads   b + 256r  (b < 256) -> (b + 4(b>>7)) + 272r
 struct Ri1024 {
     template <int p>
     __device__ __forceinline__ static int wbase(int b) {
-        return p == 0 ? 16 * b + (b >> 1) : 272 * (b >> 4) + (b & 15);
+        return p == 0 ? 16 * b + 4 * (b >> 1) : 272 * (b >> 4) + (b & 15);
     }
     template <int p>
     __host__ __device__ static constexpr int woff(int r) {
@@ -417,25 +425,28 @@ struct Ri1024 {
     }
     template <int p>
     __device__ __forceinline__ static int rbase(int b) {
-        return p == 0 ? b + (b >> 5) : b + 4 * (b >> 7);
+        return p == 0 ? b + 4 * (b >> 5) : b + 4 * (b >> 7);
     }
     template <int p>
     __host__ __device__ static constexpr int roff(int r) {
-        return p == 0 ? 66 * r : 272 * r;
+        return p == 0 ? 72 * r : 272 * r;
     }
 };
 __host__ __device__ constexpr bool ri1024_check() {
     for (int b = 0; b < 64; ++b)
         for (int r = 0; r < 16; ++r) {
-            if (ri_pad<1024, 0>(16 * b + r) != 16 * b + (b >> 1) + Ri1024::woff<0>(r)) return false;
-            if (ri_pad<1024, 0>(b + 64 * r) != b + (b >> 5) + Ri1024::roff<0>(r)) return false;
+            if (ri_pad<1024, 0>(16 * b + r) != 16 * b + 4 * (b >> 1) + Ri1024::woff<0>(r)) return false;
+            if (ri_pad<1024, 0>(b + 64 * r) != b + 4 * (b >> 5) + Ri1024::roff<0>(r)) return false;
             const int e = 256 * (b >> 4) + (b & 15) + 16 * r;
             if (ri_pad<1024, 1>(e) != 272 * (b >> 4) + (b & 15) + Ri1024::woff<1>(r)) return false;
         }
     for (int b = 0; b < 256; ++b)
         for (int r = 0; r < 4; ++r)
             if (ri_pad<1024, 1>(b + 256 * r) != b + 4 * (b >> 7) + Ri1024::roff<1>(r)) return false;
-    return true;
+    // each layout is one-to-one (strictly increasing) and fits ri_floats
+    for (int e = 1; e < 1024; ++e)
+        if (ri_pad<1024, 0>(e) <= ri_pad<1024, 0>(e - 1) || ri_pad<1024, 1>(e) <= ri_pad<1024, 1>(e - 1)) return false;
+    return ri_pad<1024, 0>(1023) < 1148 && ri_pad<1024, 1>(1023) < 1148;
 }
 static_assert(ri1024_check(), "Ri1024 decomposition of ri_pad");
 
@@ -450,16 +461,30 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
         int rb[G::P / R2];
 #pragma unroll
         for (int i = 0; i < G::P / R2; ++i) rb[i] = Ri1024::rbase<p>(bfly<N, p + 1, PAIRED>(t, i));
+        if constexpr (p == 0) {   // 16 contiguous floats: four 16 B stores
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[wb + Ri1024::woff<p>(r)] = v[r].x;
+            for (int u = 0; u < R / 4; ++u)
+                *reinterpret_cast<vf4_t*>(lds + wb + 4 * u) =
+                    vf4_t{v[4 * u].x, v[4 * u + 1].x, v[4 * u + 2].x, v[4 * u + 3].x};
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) lds[wb + Ri1024::woff<p>(r)] = v[r].x;
+        }
         xsync<G::T>();
 #pragma unroll
         for (int i = 0; i < G::P / R2; ++i)
 #pragma unroll
             for (int r = 0; r < R2; ++r) nx[i * R2 + r] = lds[rb[i] + Ri1024::roff<p>(r)];
         xsync<G::T>();
+        if constexpr (p == 0) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[wb + Ri1024::woff<p>(r)] = v[r].y;
+            for (int u = 0; u < R / 4; ++u)
+                *reinterpret_cast<vf4_t*>(lds + wb + 4 * u) =
+                    vf4_t{v[4 * u].y, v[4 * u + 1].y, v[4 * u + 2].y, v[4 * u + 3].y};
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) lds[wb + Ri1024::woff<p>(r)] = v[r].y;
+        }
         xsync<G::T>();
 #pragma unroll
         for (int i = 0; i < G::P / R2; ++i)

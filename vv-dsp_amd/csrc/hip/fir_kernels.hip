@@ -212,7 +212,8 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
     constexpr int SPAN = N + (3 * N) / 4;
     constexpr int NST = LQ ? 2 * (G::P - G::P / RL) : 2 * G::P;   // stores per pair
     constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
-    __shared__ float xch[F * G::LDS];
+    constexpr int XW = ri_floats<N>();   // exchange floats per transform (a multiple of 4)
+    __shared__ __attribute__((aligned(16))) float xch[F * XW];   // 16 B: pass_exchange_ri's b128 writes
     __shared__ float2 ltab[TWL];
     __shared__ float2 lH[N / 2 + 1];
     __shared__ float span_all[F * SPAN];
@@ -223,7 +224,7 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
     tw.tab = ltab;
     tw.load(gpass, t);
     __syncthreads();
-    float2* my = reinterpret_cast<float2*>(xch + slot * G::LDS);
+    float2* my = reinterpret_cast<float2*>(xch + slot * XW);
     float* span = span_all + slot * SPAN;
     const long long lout = N - le;
     long long p, p_end, p_step;
@@ -272,19 +273,31 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
         tw.opaque();
         fft_regs<N, false, false, true>(u, t, my, tw);
         float* ya = y + c * y_stride + j * lout - le;   // + e: block j output (e >= le)
+        if constexpr (LQ) {
+            // le = N/4, lout = 3N/4: register q (q % RL != 0) holds outputs
+            // e = t + 64 m of both blocks, m = out_pos' slot; streaming dword
+            // stores at the wave-uniform row base + 4t + immediate (block b's
+            // from a second base 4 KB on, the immediate is 13-bit)
+            const unsigned lo = 4u * (unsigned)t;
+            const float* yb = ya + 1024;
+            static_for<0, G::P>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                constexpr int m = q / RL + G::NPT * (q % RL);
+                if constexpr (q % RL != 0) {
+                    st4_nt_sbase<256 * m>(lo, u[q].x, ya);
+                    st4_nt_sbase<256 * m + 4 * (3 * N / 4) - 4096>(lo, u[q].y, yb);
+                }
+            });
+        } else {
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
             const long long e = out_pos<N>(t, q);
-            if constexpr (LQ) {
-                if (q % RL != 0) {
-                    st4_counted(ya + e, u[q].x);
-                    st4_counted(ya + e + lout, u[q].y);
-                }
-            } else {
+            {
                 const bool ok = e >= le;
                 st4_counted(ok ? ya + e : snk, u[q].x);
                 st4_counted(ok ? ya + e + lout : snk, u[q].y);
             }
+        }
         }
         c = cn;
         j = jn;

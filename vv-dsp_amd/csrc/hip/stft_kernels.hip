@@ -301,9 +301,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
     constexpr bool RI = DIRECT;
-    constexpr int XF = RI ? (G::LDS + 1) / 2 : G::LDS;   // float2 per transform
+    constexpr int XF = RI ? (ri_floats<N>() + 3) / 4 * 2 : G::LDS;   // float2 per transform (16 B multiple)
     constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
-    __shared__ float2 lds[LDSN];
+    __shared__ __attribute__((aligned(16))) float2 lds[LDSN];   // 16 B: pass_exchange_ri's b128 writes
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
     const TwTab<N> tw{ltab};
@@ -850,7 +850,7 @@ __global__ void __launch_bounds__(256, 3)
 k_istft(const float2* __restrict__ spec, long long count, int hop, int K, const float* __restrict__ win,
         float* __restrict__ out_add, float* __restrict__ norm_add, long long run, const float2* gpass) {
     using G = Geo<N>;
-    static_assert(G::T == 64 && G::LDS <= 2 * N, "one wave per transform; exchange fits two frames");
+    static_assert(G::T == 64 && ri_floats<N>() <= 2 * N, "one wave per transform; exchange fits two frames");
     constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
     __shared__ __attribute__((aligned(16))) float stage[8 * N];
     __shared__ float carry[N], ncarry[N];
