@@ -179,6 +179,21 @@ def case_lab(e, nch=32, seconds=600, fn="stftlab_run"):
         byts, (sig, win, out, lib)
 
 
+def case_firlab(e, nch=8, n=1 << 24):
+    """k_fir_bulk (config 4's bulk pairs) with parts switched off (scripts/stftlab.hip firlab_run,
+    EXP bits: 1 no FFT exchanges, 2 no FFTs, 4 no stores, 8 no span loads); H = a unit impulse's spectrum"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
+    lib.firlab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                               ctypes.c_longlong, ctypes.c_void_p]
+    x = torch.rand(nch, n, device="cuda") * 2 - 1
+    y = torch.empty_like(x)
+    H = torch.zeros(1024, dtype=torch.complex64, device="cuda") + (1.0 / 1024)
+    s = torch.cuda.current_stream().cuda_stream
+    return (lambda: lib.firlab_run(e, H.data_ptr(), x.data_ptr(), y.data_ptr(), n, nch, s)), 2 * nch * n * 4, \
+        (x, y, H, lib)
+
+
 def case_rw(w, in_bytes=3686400000, blocks=4096):
     """streaming read 1 : write w (scripts/membench.hip k_rw), 16 B/lane, nt"""
     import ctypes
@@ -282,6 +297,7 @@ CASES = {
     "r2c1024": lambda: case_r2c(1024, 131072),
     "c2r1024": lambda: case_c2r(1024, 131072),
     "stft": lambda: case_stft(32, 600),
+    **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152]},
     "stft60": lambda: case_stft(1, 60),
@@ -290,6 +306,7 @@ CASES = {
     "stftc": lambda: case_stft(8, 600, complex_out=True),
     "stftcold": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_POW_OLD", "1"),
     "fir": lambda: case_fir(8, 1 << 24),
+    "firspan": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_REG", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),
@@ -306,7 +323,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw", "lab", "model"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw", "lab", "model", "firlab"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

@@ -6,6 +6,7 @@
 // 16 rows as 16 B/lane stores (garbage values), 32 plain instead of streaming stores.
 #include "../vv-dsp_amd/csrc/hip/tables.hip"
 #include "../vv-dsp_amd/csrc/hip/stft_kernels.hip"
+#include "../vv-dsp_amd/csrc/hip/fir_kernels.hip"
 
 namespace vvh {
 template <int EXP>
@@ -23,7 +24,34 @@ static hipError_t lab_launch(const float* sig, long long n, long long nch, const
                        0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, store_sink());
     return hipGetLastError();
 }
+// config 4's bulk launch (8 ch x 2^24, 257 taps: N 1024, le 256) of k_fir_bulk<1024, true, EXP>
+template <int EXP>
+static hipError_t lab_fir(const float2* H, const float* x, float* y, long long n, long long nch, hipStream_t s) {
+    constexpr int N = 1024;
+    const long long le = 256, lout = N - le, nblk = (n + lout - 1) / lout, ppc = (nblk + 1) / 2;
+    const long long qf = (le + 2 * lout - 1) / (2 * lout);
+    long long ql = n / (2 * lout);
+    if (ql > ppc) ql = ppc;
+    static std::atomic<int> cap;
+    const int capv = cached_grid(cap, (const void*)k_fir_bulk<N, true, EXP>, 256, 0, 1LL << 40);
+    const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
+    const int grid = (int)(need < capv ? need : capv);
+    hipLaunchKernelGGL((k_fir_bulk<N, true, EXP>), dim3(grid), dim3(256), 0, s, le, H, x, y, nch, n, n, cnt, qf,
+                       pass_twiddles(N), store_sink());
+    return hipGetLastError();
+}
 }  // namespace vvh
+
+extern "C" int firlab_run(int exp, const void* H, const float* x, float* y, long long n, long long nch, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const float2* h = (const float2*)H;
+    switch (exp) {
+#define C(E) case E: return (int)vvh::lab_fir<E>(h, x, y, n, nch, s);
+        C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(8) C(10) C(12) C(14)
+#undef C
+        default: return -1;
+    }
+}
 
 extern "C" int stftlab_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
                            void* stream) {

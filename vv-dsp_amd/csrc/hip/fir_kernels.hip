@@ -202,7 +202,10 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
 // registers q with q % RL == 0, so those stores are dropped at compile time
 // (no sink stores: 3/4 of the store instructions of the general variant).
 // ------------------------------------------------------------------------
-template <int N, bool LQ>
+// EXP: timing ablations for scripts/stftlab.hip only (the library instantiates
+// EXP = 0): bit 0 FFTs without their LDS exchanges, bit 1 no FFTs, bit 2 no
+// output stores, bit 3 no span loads.  Results are wrong under any of them.
+template <int N, bool LQ, int EXP = 0>
 __global__ void __launch_bounds__(256, 3)   // 3 waves per SIMD: the LDS allows 3 workgroups per CU
 k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long nch, long long x_stride,
            long long y_stride, long long cnt, long long q0, const float2* gpass, float* sink) {
@@ -210,7 +213,7 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
     static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
     constexpr int F = 4, RL = G::RL;
     constexpr int SPAN = N + (3 * N) / 4;
-    constexpr int NST = LQ ? 2 * (G::P - G::P / RL) : 2 * G::P;   // stores per pair
+    constexpr int NST = (EXP & 4) ? 0 : LQ ? 2 * (G::P - G::P / RL) : 2 * G::P;   // stores per pair
     constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
     constexpr int XW = ri_floats<N>();   // exchange floats per transform (a multiple of 4)
     __shared__ __attribute__((aligned(16))) float xch[F * XW];   // 16 B: pass_exchange_ri's b128 writes
@@ -241,6 +244,7 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
     locate(p, &c, &j);
     float* snk = sink + ((((long long)blockIdx.x * F + slot) * 64) % SINK_FLOATS) + t;
     auto issue_span = [&](long long cc, long long jj) {
+        if constexpr (EXP & 8) return;
         const float* s0 = x + cc * x_stride + jj * lout - le;
         const int len = (int)(N + lout);
 #pragma unroll
@@ -262,7 +266,7 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
         lgkm_wait0();
         if (more) issue_span(cn, jn);
         tw.opaque();
-        fft_regs<N, true, false, true>(v, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, true, false, true, TwLastReg<N>, (EXP & 1) != 0>(v, t, my, tw);
         float2 u[G::P];
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
@@ -271,7 +275,7 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
             else u[m] = cmul(v[q], cconj(lH[N - t - 64 * m]));
         }
         tw.opaque();
-        fft_regs<N, false, false, true>(u, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, false, false, true, TwLastReg<N>, (EXP & 1) != 0>(u, t, my, tw);
         float* ya = y + c * y_stride + j * lout - le;   // + e: block j output (e >= le)
         if constexpr (LQ) {
             // le = N/4, lout = 3N/4: register q (q % RL != 0) holds outputs
@@ -280,10 +284,14 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
             // from a second base 4 KB on, the immediate is 13-bit)
             const unsigned lo = 4u * (unsigned)t;
             const float* yb = ya + 1024;
+            if constexpr (EXP & 4) {
+#pragma unroll
+                for (int q = 0; q < G::P; ++q) asm volatile("" ::"v"(u[q].x), "v"(u[q].y));
+            }
             static_for<0, G::P>([&](auto qc) {
                 constexpr int q = decltype(qc)::value;
                 constexpr int m = q / RL + G::NPT * (q % RL);
-                if constexpr (q % RL != 0) {
+                if constexpr ((EXP & 4) == 0 && q % RL != 0) {
                     st4_nt_sbase<256 * m>(lo, u[q].x, ya);
                     st4_nt_sbase<256 * m + 4 * (3 * N / 4) - 4096>(lo, u[q].y, yb);
                 }
@@ -298,6 +306,98 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
                 st4_counted(ok ? ya + e + lout : snk, u[q].y);
             }
         }
+        }
+        c = cn;
+        j = jn;
+    }
+}
+
+// ------------------------------------------------------------------------
+// k_fir_bulk_reg<N>: k_fir_bulk's LQ case with the pair's two blocks loaded
+// straight into registers (coalesced dword loads, the LE overlap re-read from
+// L1/L2) instead of an LDS span.  Without the 28 KB of spans a workgroup needs
+// 24 KB of LDS, so four workgroups fit per CU (16 waves instead of 12): the
+// kernel is latency-bound on its LDS exchanges (scripts/kbench.py firlab*).
+// The next pair's loads are issued after the inverse FFT, ahead of this
+// pair's stores (issued during the FFT they would need 32 more VGPRs than the
+// four waves per SIMD allow).  All global accesses are compiler-visible.
+// ------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(256, 4)
+k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
+               long long cnt, long long q0, const float2* gpass) {
+    using G = Geo<N>;
+    static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
+    constexpr int F = 4, RL = G::RL;
+    constexpr int LE = N / 4, LOUT = N - LE;   // taps <= N/4 + 1
+    constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
+    constexpr int XW = ri_floats<N>();
+    __shared__ __attribute__((aligned(16))) float xch[F * XW];
+    __shared__ float2 ltab[TWL];
+    __shared__ float2 lH[N / 2 + 1];
+    for (int i = threadIdx.x; i < G::tw_off(G::NPASS - 1); i += 256) ltab[i] = gpass[i];
+    for (int i = threadIdx.x; i <= N / 2; i += 256) lH[i] = Hg[i];
+    const int lt = threadIdx.x, slot = lt >> 6, t = lt & 63;
+    TwLastReg<N> tw;
+    tw.tab = ltab;
+    tw.load(gpass, t);
+    __syncthreads();
+    float2* my = reinterpret_cast<float2*>(xch + slot * XW);
+    long long p, p_end, p_step;
+    xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+    p = uni<64>(p);
+    p_end = uni<64>(p_end);
+    p_step = uni<64>(p_step);
+    if (p >= p_end) return;
+    auto locate = [&](long long it, long long* cc, long long* jj) {
+        *cc = it / cnt;
+        *jj = 2 * (q0 + (it - *cc * cnt));
+    };
+    long long c, j;
+    locate(p, &c, &j);
+    float xa[G::P], xb[G::P];
+    auto load_a = [&](long long cc, long long jj) {
+        const float* a = x + cc * x_stride + jj * LOUT - LE;   // wave-uniform block base
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) xa[r] = __builtin_nontemporal_load(a + t + 64 * r);
+    };
+    auto load_b = [&](long long cc, long long jj) {
+        const float* b = x + cc * x_stride + jj * LOUT - LE + LOUT;
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) xb[r] = b[t + 64 * r];   // overlaps the next pair's block a: cached
+    };
+    load_a(c, j);
+    load_b(c, j);
+    for (; p < p_end; p += p_step) {
+        const bool more = p + p_step < p_end;
+        long long cn = c, jn = j;
+        if (more) locate(p + p_step, &cn, &jn);
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
+        tw.opaque();
+        fft_regs<N, true, false, true, TwLastReg<N>>(v, t, my, tw);
+        float2 u[G::P];
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int m = q / RL + G::NPT * (q % RL);   // out_pos<N>(t, q) = t + 64*m
+            if (m < G::P / 2) u[m] = cmul(v[q], lH[t + 64 * m]);
+            else u[m] = cmul(v[q], cconj(lH[N - t - 64 * m]));
+        }
+        tw.opaque();
+        fft_regs<N, false, false, true, TwLastReg<N>>(u, t, my, tw);
+        if (more) {   // ahead of this pair's stores: in flight across them
+            load_a(cn, jn);
+            load_b(cn, jn);
+        }
+        float* ya = y + c * y_stride + j * LOUT - LE;   // + e: block j output (e >= LE)
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            if (q % RL != 0) {   // e = t + 64 m >= LE exactly for these registers
+                const int m = q / RL + G::NPT * (q % RL);
+                __builtin_nontemporal_store(u[q].x, ya + t + 64 * m);
+                __builtin_nontemporal_store(u[q].y, ya + LOUT + t + 64 * m);
+            }
         }
         c = cn;
         j = jn;
@@ -348,7 +448,18 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     const char* eo = getenv("VVHIP_FIR_OLD");   // A/B switch (scripts/kbench.py), read per call
     const bool old = eo && *eo == '1';
     // le == N/4 holds for every filter fir_block gives N = 1024 (taps <= 257)
-    if (ql > qf && le == N / 4 && !old) {
+    const char* er = getenv("VVHIP_FIR_REG");   // A/B switch (scripts/kbench.py): 0 = LDS-span k_fir_bulk
+    const bool reg = !(er && *er == '0');
+    if (ql > qf && le == N / 4 && !old && reg) {
+        if constexpr (FIR_BULK<N>) {
+            static std::atomic<int> capc_r;
+            const int cap_r = cached_grid(capc_r, (const void*)k_fir_bulk_reg<N>, 256, 0, 1LL << 40);
+            const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
+            const int grid = (int)(need < cap_r ? need : cap_r);
+            hipLaunchKernelGGL((k_fir_bulk_reg<N>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, cnt,
+                               qf, pN);
+        }
+    } else if (ql > qf && le == N / 4 && !old) {
         if constexpr (FIR_BULK<N>) {
             const int cap_v2 = cached_grid(capc_v2, (const void*)k_fir_bulk<N, true>, 256, 0, 1LL << 40);
             const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
