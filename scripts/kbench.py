@@ -194,6 +194,17 @@ def case_firlab(e, nch=8, n=1 << 24):
         (x, y, H, lib)
 
 
+def case_c2clab(e, batch=65536):
+    """k_c2c<1024> forward with parts switched off (scripts/stftlab.hip c2clab_run: 1 no exchanges, 2 no FFT)"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
+    lib.c2clab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
+    x = torch.rand(batch, 1024, dtype=torch.complex64, device="cuda")
+    y = torch.empty_like(x)
+    s = torch.cuda.current_stream().cuda_stream
+    return (lambda: lib.c2clab_run(e, x.data_ptr(), y.data_ptr(), batch, s)), 2 * batch * 1024 * 8, (x, y, lib)
+
+
 def case_rw(w, in_bytes=3686400000, blocks=4096):
     """streaming read 1 : write w (scripts/membench.hip k_rw), 16 B/lane, nt"""
     import ctypes
@@ -297,6 +308,7 @@ CASES = {
     "r2c1024": lambda: case_r2c(1024, 131072),
     "c2r1024": lambda: case_c2r(1024, 131072),
     "stft": lambda: case_stft(32, 600),
+    **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152]},
@@ -323,7 +335,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw", "lab", "model", "firlab"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw", "lab", "model", "firlab", "c2clab"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

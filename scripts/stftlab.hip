@@ -7,6 +7,7 @@
 #include "../vv-dsp_amd/csrc/hip/tables.hip"
 #include "../vv-dsp_amd/csrc/hip/stft_kernels.hip"
 #include "../vv-dsp_amd/csrc/hip/fir_kernels.hip"
+#include "../vv-dsp_amd/csrc/hip/fft_kernels.hip"
 
 namespace vvh {
 template <int EXP>
@@ -40,7 +41,28 @@ static hipError_t lab_fir(const float2* H, const float* x, float* y, long long n
                        pass_twiddles(N), store_sink());
     return hipGetLastError();
 }
+template <int EXP>
+static hipError_t lab_c2c(const float2* in, float2* out, long long batch, hipStream_t s) {
+    constexpr int N = 1024, F = Wg<N>::F;
+    static std::atomic<int> cap;
+    const int grid_cap = cached_grid(cap, (const void*)k_c2c<N, true, EXP>, 256, 0, 1LL << 40);
+    const long long need = (batch + F - 1) / F;
+    const int grid = (int)(need < grid_cap ? need : grid_cap);
+    hipLaunchKernelGGL((k_c2c<N, true, EXP>), dim3(grid), dim3(256), 0, s, in, out, batch, (long long)N, (long long)N,
+                       pass_twiddles(N), twiddle_table(N), 1.0f);
+    return hipGetLastError();
+}
 }  // namespace vvh
+
+extern "C" int c2clab_run(int exp, const void* in, void* out, long long batch, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (exp) {
+        case 0: return (int)vvh::lab_c2c<0>((const float2*)in, (float2*)out, batch, s);
+        case 1: return (int)vvh::lab_c2c<1>((const float2*)in, (float2*)out, batch, s);
+        case 2: return (int)vvh::lab_c2c<2>((const float2*)in, (float2*)out, batch, s);
+        default: return -1;
+    }
+}
 
 extern "C" int firlab_run(int exp, const void* H, const float* x, float* y, long long n, long long nch, void* stream) {
     hipStream_t s = (hipStream_t)stream;

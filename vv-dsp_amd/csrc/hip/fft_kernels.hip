@@ -22,20 +22,27 @@ namespace vvh {
 // ------------------------------------------------------------------------
 // C2C
 // ------------------------------------------------------------------------
-template <int N, bool FWD>
-__global__ void __launch_bounds__(Wg<N>::value)
+// EXP: timing ablations for scripts/stftlab.hip only (the library instantiates
+// EXP = 0): bit 0 FFT without its LDS exchanges, bit 1 no FFT.
+// N = 1024 exchanges through the half-size real/imaginary buffer
+// (pass_exchange_ri): 26 KB of LDS per workgroup instead of 43 KB, so four
+// workgroups (16 waves) fit per CU and keep more transforms' loads in flight.
+template <int N, bool FWD, int EXP = 0>
+__global__ void __launch_bounds__(Wg<N>::value, N == 1024 ? 4 : 1)
 k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
       const float2* gpass, const float2* gtab, float scale) {
     using G = Geo<N>;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
-    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
-    __shared__ float2 lds[LDSN];
+    constexpr bool RI = N == 1024;
+    constexpr int XF = RI ? ri_floats<N>() / 2 : G::LDS;   // float2 per transform
+    constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
+    __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
     stage_twiddles<N, WG>(ltab, gpass, gtab);
     __syncthreads();
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
-    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
     const long long stride = (long long)gridDim.x * F;
     long long f = uni<G::T>((long long)blockIdx.x * F + slot);
     float2 nx[G::P];
@@ -52,7 +59,7 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
 #pragma unroll
             for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(in + fn * in_dist + t + r * G::T);
         }
-        fft_regs<N, FWD>(v, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, FWD, false, RI, TwTab<N>, (EXP & 1) != 0>(v, t, my, tw);
         float2* dst = out + f * out_dist;
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
