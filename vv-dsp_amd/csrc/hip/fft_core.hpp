@@ -582,7 +582,7 @@ __device__ __forceinline__ void glds16(const float* gsrc, float* lds_dst) {
                  : "v"(gsrc), "s"(l)
                  : "memory");
 }
-// the same with a cache-policy suffix (timing ablations: "nt", "sc1", "sc0 sc1 nt")
+// the same with a cache-policy suffix: loads POL 1 "nt", 2 "sc1"; stores POL 1 "sc1", 2 "sc0 sc1 nt"
 template <int POL>
 __device__ __forceinline__ void glds16_pol(const float* gsrc, float* lds_dst) {
     const unsigned l = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_dst);
