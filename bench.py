@@ -22,6 +22,7 @@ on this host's cores on a bounded sample.
 import argparse
 import concurrent.futures as cf
 import ctypes as C
+import glob
 import json
 import os
 import sys
@@ -44,7 +45,9 @@ CH_PER_GPU = 32
 SAMPLES = 10 * 60 * FS        # 10 min per channel
 PUBLISHED_CPU_FPS = 24903.0   # BASELINE.md §1 STFT_size_1024 (CPU, 1 thread) -- informational only:
                               # BASELINE.json "published" is empty, so vs_baseline is null
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_bench_pmc.json")
+# the newest round's committed PMC summary of this command (profiles/rNN_bench_pmc.json)
+TRAFFIC_JSON = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_pmc.json"))) or
+                [os.path.join(ROOT, "profiles", "r01_bench_pmc.json")])[-1]
 METRIC = "STFT frames/sec (1024-pt, hop 256) at 1/2/4/8 GPU; achieved HBM GB/s vs peak"
 
 
@@ -52,11 +55,21 @@ def frames_of(n):
     return 1 if n < NFFT else 1 + (n - NFFT + HOP) // HOP
 
 
-def timed_launches(fn, reps, warm=3):
+def timed_launches(fn, reps, warm=3, warm_s=0.25):
     """Average device time of fn() (one kernel launch each) with HIP events
-    recorded on torch's current stream -- the stream the library launches on."""
+    recorded on torch's current stream -- the stream the library launches on.
+    Warm-up: at least `warm` launches AND `warm_s` seconds of back-to-back
+    launches, so the GPU clock has left its idle state (a 0.2 ms kernel timed
+    after ten warm-up launches reads up to 30 % slow: the clock ramp is tens of
+    ms, measured on the FIR leg)."""
     for _ in range(warm):
         fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        for _ in range(8):
+            fn()
+        torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in ev:
@@ -68,7 +81,7 @@ def timed_launches(fn, reps, warm=3):
     return float(np.mean(ms)), float(np.min(ms))
 
 
-def fft_c2c_roofline(reps=20):
+def fft_c2c_roofline(reps=50):
     """Config 2: 65536 x 1024-pt c2c f32 forward, device resident."""
     B, N = 65536, 1024
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -119,7 +132,7 @@ def stft_config3(reps=50, burst=100):
                                       "frac": round(byts / (per * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
 
-def fir_roofline(reps=10):
+def fir_roofline(reps=50):
     """Config 4: 257-tap lowpass (Hann, fc 0.25) overlap-save, 8 ch x 2^24 f32."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     nch, n = 8, 1 << 24
