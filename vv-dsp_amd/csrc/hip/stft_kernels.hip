@@ -936,33 +936,58 @@ k_istft(const float2* __restrict__ spec, long long count, int hop, int K, const 
             *acc_o = acc;
             *nacc_o = nacc;
         };
-        for (int idx = tid; idx < 8 * hop; idx += 256) {   // phase A: blocks [g, g+8) become final
-            const int bb = idx >> lh, j = idx & (hop - 1);   // idx = bb * hop + j
-            if (bb < bb_fa || bb >= bb_bend || bb >= bb_tot) continue;
-            const bool fresh = g == g0 || bb >= K - 1;
-            const float a0 = fresh ? out_add[gh + idx] : carry[idx];
-            const float n0 = norm_add ? (fresh ? norm_add[gh + idx] : ncarry[idx]) : 0.0f;
-            float acc, nacc;
-            combine(bb, j, a0, n0, &acc, &nacc);
-            out_add[gh + idx] = acc;
-            if (norm_add) norm_add[gh + idx] = nacc;
+        // Both phases read their out_add / norm_add words for eight samples per
+        // thread before combining any (one memory latency per chunk instead of
+        // one per sample: the loop body's load -> add -> store chain otherwise
+        // serialises them).
+        constexpr int CH = 8;
+        for (int base = 0; base < 8 * hop; base += 256 * CH) {   // phase A: blocks [g, g+8) become final
+            float a0[CH], n0[CH];
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                const int idx = base + tid + 256 * s, bb = idx >> lh;
+                const bool ok = idx < 8 * hop && bb >= bb_fa && bb < bb_bend && bb < bb_tot;
+                const bool fresh = g == g0 || bb >= K - 1;
+                a0[s] = ok ? (fresh ? out_add[gh + idx] : carry[idx]) : 0.0f;
+                n0[s] = ok && norm_add ? (fresh ? norm_add[gh + idx] : ncarry[idx]) : 0.0f;
+            }
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                const int idx = base + tid + 256 * s, bb = idx >> lh, j = idx & (hop - 1);   // idx = bb * hop + j
+                if (idx >= 8 * hop || bb < bb_fa || bb >= bb_bend || bb >= bb_tot) continue;
+                float acc, nacc;
+                combine(bb, j, a0[s], n0[s], &acc, &nacc);
+                out_add[gh + idx] = acc;
+                if (norm_add) norm_add[gh + idx] = nacc;
+            }
         }
         __syncthreads();   // phase A's carry reads before phase B's carry writes
         const bool last = g + 8 >= fb;
         const long long gh8 = gh + 8LL * hop;
-        for (int idx = tid; idx < (K - 1) * hop; idx += 256) {   // phase B: blocks [g+8, g+8+K-1), fresh
-            const int bb = 8 + (idx >> lh), j = idx & (hop - 1);
-            if (bb >= bb_tot) continue;
-            float acc, nacc;
-            combine(bb, j, out_add[gh8 + idx], norm_add ? norm_add[gh8 + idx] : 0.0f, &acc, &nacc);
-            if (last) {
-                if (bb >= bb_fa && bb < bb_bend) {
-                    out_add[gh8 + idx] = acc;
-                    if (norm_add) norm_add[gh8 + idx] = nacc;
+        for (int base = 0; base < (K - 1) * hop; base += 256 * CH) {   // phase B: blocks [g+8, g+8+K-1), fresh
+            float a0[CH], n0[CH];
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                const int idx = base + tid + 256 * s, bb = 8 + (idx >> lh);
+                const bool ok = idx < (K - 1) * hop && bb < bb_tot;
+                a0[s] = ok ? out_add[gh8 + idx] : 0.0f;
+                n0[s] = ok && norm_add ? norm_add[gh8 + idx] : 0.0f;
+            }
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                const int idx = base + tid + 256 * s, bb = 8 + (idx >> lh), j = idx & (hop - 1);
+                if (idx >= (K - 1) * hop || bb >= bb_tot) continue;
+                float acc, nacc;
+                combine(bb, j, a0[s], n0[s], &acc, &nacc);
+                if (last) {
+                    if (bb >= bb_fa && bb < bb_bend) {
+                        out_add[gh8 + idx] = acc;
+                        if (norm_add) norm_add[gh8 + idx] = nacc;
+                    }
+                } else {
+                    carry[idx] = acc;   // = (b - (g+8)) * hop + j: next step's base
+                    ncarry[idx] = nacc;
                 }
-            } else {
-                carry[idx] = acc;   // = (b - (g+8)) * hop + j: next step's base
-                ncarry[idx] = nacc;
             }
         }
         __syncthreads();   // stage and carry are reused by the next step
