@@ -326,7 +326,14 @@ CASES = {
     **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
-                                                                         128, 256, 512, 1024, 640, 1152]},
+                                                                         128, 256, 512, 1024, 640, 1152,
+                                                                         2048, 2050, 2052, 2056]},
+    "stftspan": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RING", "0"),
+    "stftpowspan": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RING", "0"),
+    "stftcspan": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_RING", "0"),
+    "stft60span": with_env(lambda: case_stft(1, 60), "VVHIP_STFT_RING", "0"),
+    **{f"stftrun{r}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RUN", str(r)) for r in (1, 2, 4, 8, 16)},
+    **{f"stftpowrun{r}": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RUN", str(r)) for r in (1, 2, 4, 8, 16)},
     "stft60": lambda: case_stft(1, 60),
     "stftpow": lambda: case_stft_power(32, 600),
     "stftpowold": with_env(lambda: case_stft_power(32, 600), "VVHIP_POW_OLD", "1"),

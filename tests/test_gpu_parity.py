@@ -375,6 +375,31 @@ def test_stft_multichannel_equals_single(vdev):
     torch.testing.assert_close(spec.abs(), multi, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("nch,n", [(1, 48000 + 333), (3, 20000), (5, 1280), (4, 700), (7, 480000),
+                                   (50, 480000 + 333), (2, 9 * 48000 + 4)])
+def test_stft_ring_equals_span(vdev, monkeypatch, nch, n):
+    """hop % 256 == 0 on the LDS-DMA path runs the ring-span kernel (VAR 3: each
+    wave walks a contiguous run of pairs and DMAs only the 2*hop new samples of
+    each span).  Rows must be bit-identical to the whole-span kernel (VAR 0,
+    VVHIP_STFT_RING=0) in all three output kinds: runs cross channel boundaries
+    (50 ch: 16-pair runs over 938-pair channels), start at tail pairs, and end
+    on odd frame counts."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(nch * 7 + n)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
+    for hop in (256, 512):
+        st = vdev.Stft(1024, hop)
+        kinds = (lambda: st.spectrogram(sig), lambda: st.spectrogram(sig, complex_out=True), lambda: st.power(sig))
+        for kind, f in enumerate(kinds):
+            monkeypatch.setenv("VVHIP_STFT_RING", "1")
+            ring = f()
+            monkeypatch.setenv("VVHIP_STFT_RING", "0")
+            span = f()
+            torch.cuda.synchronize()
+            assert torch.equal(ring, span), (hop, kind)
+            del ring, span
+
+
 # ---------------------------------------------------------------- FIR
 def test_golden_fir_direct_bitexact(amd, golden):
     g = golden("fir_257_n16384")

@@ -60,10 +60,28 @@ __device__ __forceinline__ vf2_t pk(float2 a) { return vf2_t{a.x, a.y}; }
 __device__ __forceinline__ float2 upk(vf2_t v) { return make_float2(v.x, v.y); }
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return upk(pk(a) + pk(b)); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return upk(pk(a) - pk(b)); }
-// a*w = a.xx * w + a.yy * (-w.y, w.x)
+// a*w = a.xx * w + a.yy * (-w.y, w.x): t = a.yy * (-w.y, w.x) as one v_pk_mul_f32
+// with op_sel swizzles and a neg modifier, then one v_pk_fma_f32 -- two
+// instructions (left to itself the compiler spends a third, multiplying w by
+// (-1, 1) first).  Same roundings: (fma(a.x, w.x, -a.y w.y), fma(a.x, w.y, a.y w.x)).
 __device__ __forceinline__ float2 cmul(float2 a, float2 w) {
     const vf2_t A = pk(a), W = pk(w);
-    return upk(A.xx * W + A.yy * (W.yx * vf2_t{-1.0f, 1.0f}));
+    vf2_t t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(t) : "v"(A), "v"(W));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(A), "v"(W), "v"(t));
+    return upk(r);
+}
+// e + i*o (PLUS_I) or e - i*o as one v_pk_add_f32 with swizzle and negation
+// modifiers: the quarter-turn rotations of the radix-4/8/16 butterflies cost no
+// multiply (exact, as the multiply by +-1 it replaces)
+template <bool PLUS_I>
+__device__ __forceinline__ float2 cadd_i(float2 e, float2 o) {
+    vf2_t r;
+    if constexpr (PLUS_I)   // (e.x - o.y, e.y + o.x)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pk(e)), "v"(pk(o)));
+    else                    // (e.x + o.y, e.y - o.x)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pk(e)), "v"(pk(o)));
+    return upk(r);
 }
 __device__ __forceinline__ float2 cconj(float2 a) { return upk(pk(a) * vf2_t{1.0f, -1.0f}); }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return upk(pk(a) * s); }
@@ -121,9 +139,16 @@ struct Dft {
         Dft<R / 2, FWD>::run(o);
 #pragma unroll
         for (int k = 0; k < R / 2; ++k) {
-            const float2 t = twc<R, FWD>(o[k], k);
-            v[k] = cadd(e[k], t);
-            v[k + R / 2] = csub(e[k], t);
+            const int m = (k * (16 / R)) & 15;
+            if (m == 4 || m == 12) {   // o * (-+i): folded into the adds
+                const bool plus_i = (m == 12) == FWD;
+                v[k] = plus_i ? cadd_i<true>(e[k], o[k]) : cadd_i<false>(e[k], o[k]);
+                v[k + R / 2] = plus_i ? cadd_i<false>(e[k], o[k]) : cadd_i<true>(e[k], o[k]);
+            } else {
+                const float2 t = twc<R, FWD>(o[k], k);
+                v[k] = cadd(e[k], t);
+                v[k + R / 2] = csub(e[k], t);
+            }
         }
     }
 };
@@ -144,12 +169,11 @@ struct Dft<4, FWD> {
     __device__ __forceinline__ static void run(float2* v) {
         const float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
         const float2 s13 = cadd(v[1], v[3]), d13 = csub(v[1], v[3]);
-        // d13 * W_4^1: forward -i, backward +i
-        const float2 r = FWD ? cmul_mi(d13) : cmul_pi(d13);
+        // d13 * W_4^1: forward -i, backward +i (folded into the adds)
         v[0] = cadd(s02, s13);
         v[2] = csub(s02, s13);
-        v[1] = cadd(d02, r);
-        v[3] = csub(d02, r);
+        v[1] = FWD ? cadd_i<false>(d02, d13) : cadd_i<true>(d02, d13);
+        v[3] = FWD ? cadd_i<true>(d02, d13) : cadd_i<false>(d02, d13);
     }
 };
 
@@ -267,6 +291,17 @@ struct TwTab {
         } else {
             return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
         }
+    }
+};
+
+// Timing probe only (wrong twiddles): TwTab's LDS reads from a 128-entry table.
+template <int N>
+struct TwMask {
+    const float2* tab;
+    template <int p>
+    __device__ __forceinline__ float2 at(int j, int r, int /*i*/ = 0) const {
+        using G = Geo<N>;
+        return tab[(G::tw_off(p) + (r - 1) * G::ns(p) + j) & 127];
     }
 };
 

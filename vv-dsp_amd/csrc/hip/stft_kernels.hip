@@ -32,6 +32,7 @@
 #include "vvhip_internal.hpp"
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace vvh {
 
@@ -278,14 +279,18 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
 // with nt / sc1, bits 9/10 row stores with sc1 / nt (default sc0 sc1 nt).  Results are
 // wrong under bits 0-4 and 6.
 template <int N, int MODE, int VAR, int EXP = 0>
-__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && VAR == 0) ? 3 : 1)
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3)) ? ((EXP & 2048) ? 4 : 3) : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink) {
     using G = Geo<N>;
     using Mi = Mirror<N>;
     constexpr bool TAIL = VAR == 2;
-    constexpr bool BULK = VAR == 0;
+    constexpr bool BULK = VAR == 0 || VAR == 3;
+    // VAR 3: VAR 0 with each wave walking a contiguous run of pairs and its
+    // span kept as a ring of 256-float chunks (hop % 256 == 0): a pair DMAs only
+    // its 2*hop new samples instead of the whole N + hop span
+    constexpr bool RING = VAR == 3;
     constexpr bool STAGE = BULK && MODE == 0 && G::NPASS > 1 && G::T > 1;
     // power rows (N = 1024): the DIRECT stores below, keeping only the
     // 64-bin blocks under N/2 plus one lane for bin N/2
@@ -293,11 +298,12 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // complex rows (N = 1024): DIRECT with 8 B/lane stores, conj() for the mirror blocks
     constexpr bool CPXD = BULK && MODE == 1 && G::T == 64 && G::NPASS > 1;
     constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
-    constexpr int SPAN = GLDS ? N + N / 2 : 1;   // floats per transform: hop <= N/2
+    constexpr int SPAN = GLDS ? ((EXP & 2048) ? N + 256 : N + N / 2) : 1;   // floats per transform: hop <= N/2
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
     // written as 16 B/lane stores
     constexpr bool DIRECT = GLDS && G::T == 64;
+    static_assert(!RING || DIRECT, "ring spans: one wave per transform on the LDS-DMA path");
     // stores per pair (both rows): power rows keep half the blocks + bin N/2
     constexpr int NST = (EXP & 4) ? 0 : (EXP & 16) ? 8 : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
@@ -307,9 +313,13 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr int XF = RI ? (ri_floats<N>() + 3) / 4 * 2 : G::LDS;   // float2 per transform (16 B multiple)
     constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
     __shared__ __attribute__((aligned(16))) float2 lds[LDSN];   // 16 B: pass_exchange_ri's b128 writes
-    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    // EXP bit 11 (occupancy probe, wrong results): a 128-entry twiddle table and
+    // N + 256 float spans, so 4 workgroups fit per CU
+    constexpr int TWE = (EXP & 2048) ? 128 : TwLayout<N>::ENTRIES;
+    __shared__ float2 ltab[TWE];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
-    const TwTab<N> tw{ltab};
+    using TWT = std::conditional_t<(EXP & 2048) != 0, TwMask<N>, TwTab<N>>;
+    const TWT tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
     // window values 0.5 w[t + r T], packed two per VGPR pair (pk_mul_bcast)
@@ -366,7 +376,19 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     };
     const long long pairs = nch * ppc;
     long long p, p_end, p_step;
-    work_walk(pairs, F, slot, chunk, &p, &p_end, &p_step);
+    // RING: block b owns items [b*chunk, (b+1)*chunk) (chunk = the low 40 bits),
+    // cut into groups of F runs of `rl` consecutive pairs (rl = the high bits);
+    // slot s walks run s of every group
+    const long long rl = RING ? (chunk >> 40) : 1;
+    long long kk = 0;   // items this slot has done
+    if constexpr (RING) {
+        const long long ch = chunk & ((1LL << 40) - 1);
+        p = (long long)blockIdx.x * ch + slot * rl;
+        p_end = (long long)(blockIdx.x + 1) * ch < pairs ? (long long)(blockIdx.x + 1) * ch : pairs;
+        p_step = 1;
+    } else {
+        work_walk(pairs, F, slot, chunk, &p, &p_end, &p_step);
+    }
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
     p_step = uni<G::T>(p_step);
@@ -409,7 +431,23 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             }
         }
     };
+    // ring (VAR 3): chunk k of the current pair's span [fa*hop, fa*hop + N + hop)
+    // sits in ring slot (rs + k) mod rc; the next pair of the same channel
+    // reuses chunks h2.. and DMAs its last h2 into the slots of chunks 0..h2-1,
+    // which this pair has read (into registers) before the DMA is issued
+    const int rc = RING ? (int)((N + hop) >> 8) : 1, h2 = RING ? (int)((2 * hop) >> 8) : 0,
+              hb = RING ? (int)(hop >> 8) : 0;
+    int rs = 0, rsn = 0;
+    auto issue_new = [&](long long cc, long long ff) {
+        const float* s0 = sig + cc * ch_stride + ff * hop;
+        rsn = rs + h2 >= rc ? rs + h2 - rc : rs + h2;
+        for (int k = rc - h2; k < rc; ++k) {
+            const int sl = rsn + k >= rc ? rsn + k - rc : rsn + k;
+            glds16(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
+        }
+    };
     auto load_pair = [&](long long cc, long long ff) {
+        if constexpr (RING) rsn = 0;   // whole span, chunk k in slot k
         if constexpr (EXP & 8) {
         } else if constexpr (GLDS) {
             issue_span(cc, ff);
@@ -429,15 +467,53 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     };
     // the first span's DMA is in flight while the block stages its twiddles
     if (any) load_pair(c, fa);
-    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    if constexpr ((EXP & 2048) != 0) {
+        for (int i = threadIdx.x; i < TWE; i += WG) ltab[i] = gpass[i];
+    } else {
+        stage_twiddles<N, WG>(ltab, gpass, gtab);
+    }
     __syncthreads();
     if (!any) return;
     if constexpr (GLDS) vm_wait<0>();
+    if constexpr (RING) rs = rsn;
     for (; p < p_end; p += p_step) {
+        if constexpr (RING) p_step = ((kk + 1) % rl) ? 1 : (long long)F * rl - rl + 1;
         const bool more = p + p_step < p_end;
         long long cn = c, fn = fa;
-        if (more) locate(p + p_step, &cn, &fn);
-        if constexpr (GLDS) {
+        if constexpr (RING) {   // within a run: the next pair, or frame 2*pair0 of the next channel
+            if (p_step == 1) {
+                fn = fa + 2;
+                if (fn >= 2 * (pair0 + ppc)) {
+                    cn = c + 1;
+                    fn = 2 * pair0;
+                }
+            } else if (more) {
+                locate(p + p_step, &cn, &fn);
+            }
+        } else {
+            if (more) locate(p + p_step, &cn, &fn);
+        }
+        if constexpr (RING) {
+            vm_wait<NST>();
+            // chunk slots of frame a (chunks 0..3) and frame b (chunks hb..hb+3)
+            int ca[4], cbk[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int a = rs + k, b = rs + k + hb;
+                ca[k] = __builtin_amdgcn_readfirstlane(a >= rc ? a - rc : a) * 256;
+                cbk[k] = __builtin_amdgcn_readfirstlane(b >= rc ? b - rc : b) * 256;
+            }
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = span[ca[r / 4] + t + 64 * (r % 4)];
+                xb[r] = span[cbk[r / 4] + t + 64 * (r % 4)];
+            }
+            lgkm_wait0();   // span read before it is refilled
+            if (more) {
+                if (p_step == 1 && cn == c && fn * hop + (N + hop) <= n) issue_new(cn, fn);
+                else load_pair(cn, fn);
+            }
+        } else if constexpr (GLDS) {
             // younger than this span's DMA: only the previous pair's NST stores
             vm_wait<NST>();
             if constexpr (G::T > 64) lds_barrier();   // the other waves' pieces
@@ -462,7 +538,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
-        if constexpr (!(EXP & 2)) fft_regs<N, true, true, RI, TwTab<N>, (EXP & 1) != 0>(v, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, true, true, RI, TWT, (EXP & 1) != 0>(v, t, my, tw);
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
         char* rowb = rowa + ROW * ES;
         const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
@@ -514,6 +590,10 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         }
         c = cn;
         fa = fn;
+        if constexpr (RING) {
+            rs = rsn;
+            ++kk;
+        }
     }
 }
 
@@ -642,7 +722,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         long long mpc = (nfull < frames ? nfull : frames) / 2;
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
-        static std::atomic<int> capc[3];   // zero-initialised (static storage)
+        static std::atomic<int> capc[4];   // zero-initialised (static storage)
         // The bulk launch is NOT persistent: one workgroup per `cps` pairs per
         // transform slot, so the hardware dispatcher balances the CUs and the
         // launch has no straggler tail (measured 8-13 % faster than the
@@ -661,9 +741,16 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             const long long need = (nch * cnt + F - 1) / F;
             long long grid = need < capv ? need : capv;
             long long chunk = 0;
-            if (var == 0) {
+            if (var == 0 || var == 3) {
                 chunk = cps * F;
                 grid = (nch * cnt + chunk - 1) / chunk;
+            }
+            if (var == 3) {   // run length (pairs), a divisor of cps; VVHIP_STFT_RUN overrides (A/B)
+                long long rl = cps;
+                const char* eru = getenv("VVHIP_STFT_RUN");
+                if (eru && *eru) rl = atoll(eru);
+                if (rl < 1 || cps % rl) rl = cps;
+                chunk |= rl << 40;
             }
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0,
                                cnt, win, out, out_ch_stride, pN, tN, chunk, sink);
@@ -684,7 +771,16 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // the VAR 0 kernels that read spans by LDS-DMA run the tail pairs too:
         // one launch for the whole job
         constexpr bool FUSE_TAIL = (MODE == 0 || Geo<N>::T == 64) && Geo<N>::NPASS > 1 && Geo<N>::T >= 64;
-        if (aligned && FUSE_TAIL) {
+        // ring spans (VAR 3) when the span is whole 256-float chunks: power rows only
+        // (2.74 vs 2.84 ms for 32 ch x 10 min; magnitude and complex rows measured
+        // 1-2 % slower than with VAR 0's interleaved walk, profiles/r02_kbench_ring.jsonl).
+        // VVHIP_STFT_RING = 0 / 1 forces VAR 0 / VAR 3 (A/B switch, read per call)
+        const char* er = getenv("VVHIP_STFT_RING");
+        const bool ring = Geo<N>::T == 64 && hop % 256 == 0 &&
+                          (er && *er ? *er == '1' : MODE == 2);
+        if (aligned && FUSE_TAIL && ring) {
+            if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 3>, 3, 0LL, ppc);
+        } else if (aligned && FUSE_TAIL) {
             launch(k_stft_pair<N, MODE, 0>, 0, 0LL, ppc);
         } else {
             if (mpc > 0) {
