@@ -192,12 +192,19 @@ def case_lab(e, nch=32, seconds=600, fn="stftlab_run"):
         byts, (sig, win, out, lib)
 
 
-def case_firlab(e, nch=8, n=1 << 24):
+def case_firreglab(e, nch=8, n=1 << 24):
+    """the product's k_fir_bulk_reg with parts switched off (scripts/stftlab.hip firreglab_run:
+    2 no FFTs, 4 no stores, 8 no loads)"""
+    return case_firlab(e, nch, n, fn="firreglab_run")
+
+
+def case_firlab(e, nch=8, n=1 << 24, fn="firlab_run"):
     """k_fir_bulk (config 4's bulk pairs) with parts switched off (scripts/stftlab.hip firlab_run,
     EXP bits: 1 no FFT exchanges, 2 no FFTs, 4 no stores, 8 no span loads); H = a unit impulse's spectrum"""
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
-    lib.firlab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+    run = getattr(lib, fn)
+    run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                ctypes.c_longlong, ctypes.c_void_p]
     x = torch.rand(nch, n, device="cuda") * 2 - 1
     y = torch.empty_like(x)
@@ -205,7 +212,7 @@ def case_firlab(e, nch=8, n=1 << 24):
     hp[:257] = lowpass(257)
     H = (torch.fft.fft(hp.double()) / 1024).to(torch.complex64).cuda()   # config 4's spectrum
     s = torch.cuda.current_stream().cuda_stream
-    return (lambda: lib.firlab_run(e, H.data_ptr(), x.data_ptr(), y.data_ptr(), n, nch, s)), 2 * nch * n * 4, \
+    return (lambda: run(e, H.data_ptr(), x.data_ptr(), y.data_ptr(), n, nch, s)), 2 * nch * n * 4, \
         (x, y, H, lib)
 
 
@@ -325,9 +332,10 @@ CASES = {
     "stft": lambda: case_stft(32, 600),
     **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
+    **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152,
-                                                                         2048, 2050, 2052, 2056]},
+                                                                         2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194]},
     "stftspan": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RING", "0"),
     "stftpowspan": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RING", "0"),
     "stftcspan": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_RING", "0"),

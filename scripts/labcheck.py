@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Check that a timing-lab STFT variant (scripts/stftlab.hip, EXP bits that keep
+the results exact) writes the same rows as the lab's EXP 0 (the library's kernel).
+    python scripts/labcheck.py 8192 [nch] [seconds]"""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "vv-dsp_amd"))
+import vvdsp_amd as vv  # noqa: E402
+
+e = int(sys.argv[1])
+nch = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+sec = int(sys.argv[3]) if len(sys.argv) > 3 else 60
+lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
+lib.stftlab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
+                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+n = sec * 48000
+sig = torch.rand(nch, n, device="cuda") * 2 - 1
+win = torch.hann_window(1024, periodic=False, device="cuda")
+frames = (n - 1024 + 256) // 256 + 1
+ref = torch.full((nch, frames, 1024), -2.0, device="cuda")
+assert lib.stftlab_run(0, sig.data_ptr(), n, nch, win.data_ptr(), ref.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream) == 0
+out = torch.full_like(ref, -1.0)
+for rep in range(3):   # the counters must reset between launches
+    out.fill_(-1.0)
+    assert lib.stftlab_run(e, sig.data_ptr(), n, nch, win.data_ptr(), out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    bad = (out != ref).sum().item()
+    print(f"lab{e} launch {rep}: {bad} of {out.numel()} values differ")
+    assert bad == 0

@@ -20,9 +20,19 @@ static hipError_t lab_launch(const float* sig, long long n, long long nch, const
     const long long pairs = nch * ppc;
     long long cps = (pairs + (long long)F * cap0 - 1) / ((long long)F * cap0);
     cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
-    const long long chunk = cps * F, grid = (pairs + chunk - 1) / chunk;
+    const long long chunk = cps * F;
+    const long long grid = (EXP & (4096 | 8192)) ? (cap0 / 8) * 8 : (pairs + chunk - 1) / chunk;
+    float* sink = store_sink();
+    if constexpr ((EXP & 8192) != 0) {   // XCD counters (zero once; the kernel's last waves reset them)
+        static unsigned* ctr = nullptr;
+        if (!ctr) {
+            if (hipMalloc(&ctr, 32 * 32 * sizeof(unsigned)) != hipSuccess) return hipErrorOutOfMemory;
+            (void)hipMemset(ctr, 0, 32 * 32 * sizeof(unsigned));
+        }
+        sink = reinterpret_cast<float*>(ctr);
+    }
     hipLaunchKernelGGL((k_stft_pair<N, 0, 0, EXP>), dim3((unsigned)grid), dim3(256), 0, s, sig, n, nch, n, frames, hop,
-                       0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, store_sink());
+                       0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, sink);
     return hipGetLastError();
 }
 // config 4's bulk launch (8 ch x 2^24, 257 taps: N 1024, le 256) of k_fir_bulk<1024, true, EXP>
@@ -39,6 +49,22 @@ static hipError_t lab_fir(const float2* H, const float* x, float* y, long long n
     const int grid = (int)(need < capv ? need : capv);
     hipLaunchKernelGGL((k_fir_bulk<N, true, EXP>), dim3(grid), dim3(256), 0, s, le, H, x, y, nch, n, n, cnt, qf,
                        pass_twiddles(N), store_sink());
+    return hipGetLastError();
+}
+// the same bulk pairs through the product's register-load kernel k_fir_bulk_reg<1024, EXP>
+template <int EXP>
+static hipError_t lab_firreg(const float2* H, const float* x, float* y, long long n, long long nch, hipStream_t s) {
+    constexpr int N = 1024;
+    const long long le = 256, lout = N - le, nblk = (n + lout - 1) / lout, ppc = (nblk + 1) / 2;
+    const long long qf = (le + 2 * lout - 1) / (2 * lout);
+    long long ql = n / (2 * lout);
+    if (ql > ppc) ql = ppc;
+    static std::atomic<int> cap;
+    const int capv = cached_grid(cap, (const void*)k_fir_bulk_reg<N, EXP>, 256, 0, 1LL << 40);
+    const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
+    const int grid = (EXP & 64) ? (int)((nch * cnt + 31) / 32) : (EXP & 128) ? capv / 8 * 8 : (int)(need < capv ? need : capv);
+    hipLaunchKernelGGL((k_fir_bulk_reg<N, EXP>), dim3(grid), dim3(256), 0, s, H, x, y, nch, n, n, cnt, qf,
+                       pass_twiddles(N));
     return hipGetLastError();
 }
 template <int EXP>
@@ -75,6 +101,18 @@ extern "C" int firlab_run(int exp, const void* H, const float* x, float* y, long
     }
 }
 
+extern "C" int firreglab_run(int exp, const void* H, const float* x, float* y, long long n, long long nch,
+                             void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const float2* h = (const float2*)H;
+    switch (exp) {
+#define C(E) case E: return (int)vvh::lab_firreg<E>(h, x, y, n, nch, s);
+        C(0) C(2) C(4) C(6) C(8) C(10) C(12) C(14) C(16) C(32) C(64) C(80) C(18) C(34) C(66) C(82) C(128) C(144) C(130)
+#undef C
+        default: return -1;
+    }
+}
+
 extern "C" int stftlab_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
                            void* stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -82,7 +120,7 @@ extern "C" int stftlab_run(int exp, const float* sig, long long n, long long nch
 #define C(E) case E: return (int)vvh::lab_launch<E>(sig, n, nch, win, out, s);
         C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
         C(16) C(18) C(24) C(26) C(32) C(34) C(40) C(42) C(64) C(66) C(68) C(80) C(82)
-        C(128) C(256) C(512) C(1024) C(640) C(1152) C(2048) C(2050) C(2052) C(2056)
+        C(128) C(256) C(512) C(1024) C(640) C(1152) C(2048) C(2050) C(2052) C(2056) C(4096) C(4098) C(8192) C(8194)
 #undef C
         default: return -1;
     }

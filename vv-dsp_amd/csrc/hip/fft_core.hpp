@@ -433,9 +433,19 @@ template <int N>
 __host__ __device__ constexpr int ri_floats() {
     return N == 1024 ? 1148 : Geo<N>::LDS;
 }
+// VVH_RI_B128 (default): pass-0 writes as four ds_write_b128 per half (pad 4
+// per 32 floats).  VVH_RI_B128=0: ds_write2_b32 pairs straight from the complex
+// registers (pad 1 per 32 floats: lane b's 16 floats start at 16b + (b >> 1), on
+// 32 distinct banks), which saves the 16 v_mov per half that gather four real
+// (or imaginary) parts into a 16 B register quad -- but measured no faster
+// (c2c 1024 +3.9 %, FIR +1.4 %, STFT even; profiles/r02_ab_ri_write2.jsonl):
+// the LDS instruction count, not VALU, is what these kernels wait on.
+#ifndef VVH_RI_B128
+#define VVH_RI_B128 1
+#endif
 template <int N, int p>
 __host__ __device__ constexpr int ri_pad(int e) {
-    if constexpr (N == 1024 && p == 0) return e + 4 * (e >> 5);
+    if constexpr (N == 1024 && p == 0) return VVH_RI_B128 ? e + 4 * (e >> 5) : e + (e >> 5);
     else if constexpr (N == 1024 && p == 1) return e + 4 * (e >> 7) + 8 * (e >> 8);
     else return Geo<N>::pad(e);
 }
@@ -451,27 +461,27 @@ __host__ __device__ constexpr int ri_pad(int e) {
 //   p 1 reads   b + 256r  (b < 256) -> (b + 4(b>>7)) + 272r
 struct Ri1024 {
     template <int p>
-    __device__ __forceinline__ static int wbase(int b) {
-        return p == 0 ? 16 * b + 4 * (b >> 1) : 272 * (b >> 4) + (b & 15);
+    __host__ __device__ static constexpr int wbase(int b) {
+        return p == 0 ? (VVH_RI_B128 ? 16 * b + 4 * (b >> 1) : 16 * b + (b >> 1)) : 272 * (b >> 4) + (b & 15);
     }
     template <int p>
     __host__ __device__ static constexpr int woff(int r) {
         return p == 0 ? r : 16 * r + (r >= 8 ? 4 : 0);
     }
     template <int p>
-    __device__ __forceinline__ static int rbase(int b) {
-        return p == 0 ? b + 4 * (b >> 5) : b + 4 * (b >> 7);
+    __host__ __device__ static constexpr int rbase(int b) {
+        return p == 0 ? (VVH_RI_B128 ? b + 4 * (b >> 5) : b + (b >> 5)) : b + 4 * (b >> 7);
     }
     template <int p>
     __host__ __device__ static constexpr int roff(int r) {
-        return p == 0 ? 72 * r : 272 * r;
+        return p == 0 ? (VVH_RI_B128 ? 72 * r : 66 * r) : 272 * r;
     }
 };
 __host__ __device__ constexpr bool ri1024_check() {
     for (int b = 0; b < 64; ++b)
         for (int r = 0; r < 16; ++r) {
-            if (ri_pad<1024, 0>(16 * b + r) != 16 * b + 4 * (b >> 1) + Ri1024::woff<0>(r)) return false;
-            if (ri_pad<1024, 0>(b + 64 * r) != b + 4 * (b >> 5) + Ri1024::roff<0>(r)) return false;
+            if (ri_pad<1024, 0>(16 * b + r) != Ri1024::wbase<0>(b) + Ri1024::woff<0>(r)) return false;
+            if (ri_pad<1024, 0>(b + 64 * r) != Ri1024::rbase<0>(b) + Ri1024::roff<0>(r)) return false;
             const int e = 256 * (b >> 4) + (b & 15) + 16 * r;
             if (ri_pad<1024, 1>(e) != 272 * (b >> 4) + (b & 15) + Ri1024::woff<1>(r)) return false;
         }
@@ -496,7 +506,7 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
         int rb[G::P / R2];
 #pragma unroll
         for (int i = 0; i < G::P / R2; ++i) rb[i] = Ri1024::rbase<p>(bfly<N, p + 1, PAIRED>(t, i));
-        if constexpr (p == 0) {   // 16 contiguous floats: four 16 B stores
+        if constexpr (p == 0 && VVH_RI_B128) {   // 16 contiguous floats: four 16 B stores
 #pragma unroll
             for (int u = 0; u < R / 4; ++u)
                 *reinterpret_cast<vf4_t*>(lds + wb + 4 * u) =
@@ -511,7 +521,7 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
 #pragma unroll
             for (int r = 0; r < R2; ++r) nx[i * R2 + r] = lds[rb[i] + Ri1024::roff<p>(r)];
         xsync<G::T>();
-        if constexpr (p == 0) {
+        if constexpr (p == 0 && VVH_RI_B128) {
 #pragma unroll
             for (int u = 0; u < R / 4; ++u)
                 *reinterpret_cast<vf4_t*>(lds + wb + 4 * u) =
@@ -711,6 +721,18 @@ __device__ __forceinline__ void xcd_walk(long long total, int F, int slot, long 
     *first = lo + (b / ng) * F + slot;
     *end = hi;
     *step = nbg * F;
+}
+
+// Band walk (persistent, grid a multiple of 8): each step the whole grid covers
+// S = gridDim.x * F consecutive items, cut into 8 contiguous sub-bands, one per
+// XCD (block b runs on XCD b % 8), so at any time the chip reads and writes one
+// moving band of the data and neighbouring items share their XCD's L2.
+__device__ __forceinline__ void band_walk(long long total, int F, int slot, long long* first, long long* end,
+                                          long long* step) {
+    const long long nb = gridDim.x, b = blockIdx.x;
+    *first = (b % 8) * (nb / 8) * F + (b / 8) * F + slot;
+    *step = nb * F;
+    *end = total;
 }
 
 // Work sequence of transform slot `slot` (of F per block): with chunk > 0 the

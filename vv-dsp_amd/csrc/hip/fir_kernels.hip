@@ -322,7 +322,11 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
 // pair's stores (issued during the FFT they would need 32 more VGPRs than the
 // four waves per SIMD allow).  All global accesses are compiler-visible.
 // ------------------------------------------------------------------------
-template <int N>
+// EXP: timing ablations for scripts/stftlab.hip only (library: EXP = 0): bit 1 no
+// FFTs, bit 2 no output stores, bit 3 no input loads (results are wrong); bit 4
+// stores as sc0 sc1 nt, bit 5 plain stores, bit 6 non-persistent walk (8 pairs per
+// wave, the launcher sizes the grid).
+template <int N, int EXP = 0>
 __global__ void __launch_bounds__(256, 4)
 k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
                long long cnt, long long q0, const float2* gpass) {
@@ -344,7 +348,9 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
     __syncthreads();
     float2* my = reinterpret_cast<float2*>(xch + slot * XW);
     long long p, p_end, p_step;
-    xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+    if constexpr (EXP & 64) work_walk(nch * cnt, F, slot, 8 * F, &p, &p_end, &p_step);
+    else if constexpr (EXP & 128) band_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+    else xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
     p = uni<64>(p);
     p_end = uni<64>(p_end);
     p_step = uni<64>(p_step);
@@ -357,15 +363,21 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
     locate(p, &c, &j);
     float xa[G::P], xb[G::P];
     auto load_a = [&](long long cc, long long jj) {
+        if constexpr (EXP & 8) return;
         const float* a = x + cc * x_stride + jj * LOUT - LE;   // wave-uniform block base
 #pragma unroll
         for (int r = 0; r < G::P; ++r) xa[r] = __builtin_nontemporal_load(a + t + 64 * r);
     };
     auto load_b = [&](long long cc, long long jj) {
+        if constexpr (EXP & 8) return;
         const float* b = x + cc * x_stride + jj * LOUT - LE + LOUT;
 #pragma unroll
         for (int r = 0; r < G::P; ++r) xb[r] = b[t + 64 * r];   // overlaps the next pair's block a: cached
     };
+    if constexpr (EXP & 8) {
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) xa[r] = xb[r] = (float)(t + r);
+    }
     load_a(c, j);
     load_b(c, j);
     for (; p < p_end; p += p_step) {
@@ -376,7 +388,7 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
         tw.opaque();
-        fft_regs<N, true, false, true, TwLastReg<N>>(v, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, true, false, true, TwLastReg<N>>(v, t, my, tw);
         float2 u[G::P];
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
@@ -385,7 +397,7 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
             else u[m] = cmul(v[q], cconj(lH[N - t - 64 * m]));
         }
         tw.opaque();
-        fft_regs<N, false, false, true, TwLastReg<N>>(u, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, false, false, true, TwLastReg<N>>(u, t, my, tw);
         if (more) {   // ahead of this pair's stores: in flight across them
             load_a(cn, jn);
             load_b(cn, jn);
@@ -393,11 +405,30 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
         float* ya = y + c * y_stride + j * LOUT - LE;   // + e: block j output (e >= LE)
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
-            if (q % RL != 0) {   // e = t + 64 m >= LE exactly for these registers
+            if constexpr (EXP & 4) {
+                asm volatile("" ::"v"(u[q].x), "v"(u[q].y));
+            } else if constexpr (EXP & 48) {
+            } else if (q % RL != 0) {   // e = t + 64 m >= LE exactly for these registers
                 const int m = q / RL + G::NPT * (q % RL);
                 __builtin_nontemporal_store(u[q].x, ya + t + 64 * m);
                 __builtin_nontemporal_store(u[q].y, ya + LOUT + t + 64 * m);
             }
+        }
+        if constexpr ((EXP & 48) != 0 && (EXP & 4) == 0) {
+            const unsigned lo = 4u * (unsigned)t;
+            static_for<0, G::P>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                constexpr int m = q / RL + G::NPT * (q % RL);
+                if constexpr (q % RL != 0) {
+                    if constexpr (EXP & 16) {
+                        st4_pol_sbase<256 * m, 2>(lo, u[q].x, ya);
+                        st4_pol_sbase<256 * m, 2>(lo, u[q].y, ya + LOUT);
+                    } else {
+                        st4_sbase<256 * m>(lo, u[q].x, ya);
+                        st4_sbase<256 * m>(lo, u[q].y, ya + LOUT);
+                    }
+                }
+            });
         }
         c = cn;
         j = jn;

@@ -291,6 +291,12 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // span kept as a ring of 256-float chunks (hop % 256 == 0): a pair DMAs only
     // its 2*hop new samples instead of the whole N + hop span
     constexpr bool RING = VAR == 3;
+    // EXP bit 13 (probe): dynamic band walk -- each wave takes its next pair from
+    // its XCD's counter (ctr, passed as `sink`): counter value k is pair
+    // (k / DB) * 8 DB + xcd * DB + k % DB, so the chip works on one moving band and
+    // neighbouring pairs share an L2, while waves balance dynamically.  The
+    // counter atomics are hand-counted VMEM ops like the spans and stores.
+    constexpr bool DYN = (EXP & 8192) != 0;
     constexpr bool STAGE = BULK && MODE == 0 && G::NPASS > 1 && G::T > 1;
     // power rows (N = 1024): the DIRECT stores below, keeping only the
     // 64-bin blocks under N/2 plus one lane for bin N/2
@@ -386,12 +392,41 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         p = (long long)blockIdx.x * ch + slot * rl;
         p_end = (long long)(blockIdx.x + 1) * ch < pairs ? (long long)(blockIdx.x + 1) * ch : pairs;
         p_step = 1;
+    } else if constexpr ((EXP & 4096) != 0) {   // probe: persistent band walk (lab launches cap0 blocks)
+        band_walk(pairs, F, slot, &p, &p_end, &p_step);
+    } else if constexpr (DYN) {
+        p = 0;   // set below from the XCD's counter
+        p_end = pairs;
+        p_step = 1;
     } else {
         work_walk(pairs, F, slot, chunk, &p, &p_end, &p_step);
     }
     p = uni<G::T>(p);
     p_end = uni<G::T>(p_end);
     p_step = uni<G::T>(p_step);
+    // one counter per (XCD, slot): 32 streams, so no address takes more than one
+    // atomic per workgroup of its XCD per pair
+    const int stream = __builtin_amdgcn_readfirstlane((int)(blockIdx.x & 7) * F + slot);
+    unsigned* const ctr = DYN ? reinterpret_cast<unsigned*>(sink) + 32 * stream : nullptr;
+    constexpr long long DB = 64;
+    auto band_pair = [&](unsigned k) -> long long {
+        return (long long)(k / DB) * (8 * F * DB) + (long long)stream * DB + (long long)(k % DB);
+    };
+    unsigned rr = 0;   // lane 0: an issued counter atomic's result (valid after a vmcnt wait)
+    auto grab = [&]() {
+        if (t == 0) asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(rr) : "v"(ctr), "v"(1u) : "memory");
+    };
+    long long pn = 0;   // DYN: the pair after p
+    if constexpr (DYN) {
+        unsigned r0 = 0;
+        if (t == 0)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)" : "=v"(r0) : "v"(ctr), "v"(1u) : "memory");
+        grab();
+        unsigned k1;
+        asm volatile("s_waitcnt vmcnt(0)\n\tv_readfirstlane_b32 %0, %1" : "=s"(k1) : "v"(rr) : "memory");
+        p = band_pair(__builtin_amdgcn_readfirstlane(r0));
+        pn = band_pair(k1);
+    }
     const bool any = p < p_end;   // uniform per transform
     // (channel, first frame) of a pair; this launch covers frames
     // [2*pair0, 2*(pair0 + ppc)) of every channel
@@ -467,17 +502,21 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     };
     // the first span's DMA is in flight while the block stages its twiddles
     if (any) load_pair(c, fa);
+    if constexpr (DYN) {
+        if (any && pn < pairs) grab();   // -> the pair after pn
+    }
     if constexpr ((EXP & 2048) != 0) {
         for (int i = threadIdx.x; i < TWE; i += WG) ltab[i] = gpass[i];
     } else {
         stage_twiddles<N, WG>(ltab, gpass, gtab);
     }
     __syncthreads();
-    if (!any) return;
+    if (!any && !DYN) return;
     if constexpr (GLDS) vm_wait<0>();
     if constexpr (RING) rs = rsn;
     for (; p < p_end; p += p_step) {
         if constexpr (RING) p_step = ((kk + 1) % rl) ? 1 : (long long)F * rl - rl + 1;
+        if constexpr (DYN) p_step = pn - p;
         const bool more = p + p_step < p_end;
         long long cn = c, fn = fa;
         if constexpr (RING) {   // within a run: the next pair, or frame 2*pair0 of the next channel
@@ -513,6 +552,23 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 if (p_step == 1 && cn == c && fn * hop + (N + hop) <= n) issue_new(cn, fn);
                 else load_pair(cn, fn);
             }
+        } else if constexpr (DYN) {
+            // this span's DMA and the counter atomic issued after it are older
+            // than the previous pair's NST stores
+            unsigned knn;
+            asm volatile("s_waitcnt vmcnt(%1)\n\tv_readfirstlane_b32 %0, %2" : "=s"(knn) : "n"(NST), "v"(rr) : "memory");
+            const long long pnn = more ? band_pair(knn) : pairs;
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = span[t + r * G::T];
+                xb[r] = span[hop + t + r * G::T];
+            }
+            lgkm_wait0();   // span read before it is refilled
+            if (more) {
+                load_pair(cn, fn);
+                if (pnn < pairs) grab();
+            }
+            pn = pnn;
         } else if constexpr (GLDS) {
             // younger than this span's DMA: only the previous pair's NST stores
             vm_wait<NST>();
@@ -593,6 +649,16 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         if constexpr (RING) {
             rs = rsn;
             ++kk;
+        }
+    }
+    if constexpr (DYN) {   // the XCD's last wave out resets its counters for the next launch
+        vm_wait<0>();
+        if (t == 0) {
+            const unsigned nw = (unsigned)((gridDim.x - (blockIdx.x & 7) + 7) / 8);
+            if (atomicAdd(ctr + 16, 1u) == nw - 1) {
+                atomicExch(ctr, 0u);
+                atomicExch(ctr + 16, 0u);
+            }
         }
     }
 }
