@@ -12,6 +12,9 @@
 #include "vv_dsp/spectral/dct.h"
 #include "vv_dsp/filter/fir.h"
 #include "vv_dsp/features/mel.h"
+#include "vv_dsp/spectral/czt.h"
+#include "vv_dsp/envelope/cepstrum.h"
+#include "vv_dsp/envelope/minphase.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -108,6 +111,24 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_mfcc_process_device(const vv_dsp_mfcc_plan
                                                           size_t num_frames, vv_dsp_real* d_out_mfcc, void* stream);
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_log_mel_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
                                                      size_t num_frames, vv_dsp_real* d_out_log_mel, void* stream);
+
+/* Chirp-z plan (vv_dsp_czt_exec_cpx / _real semantics, czt.c:44-178): chirps and
+ * the chirp's spectrum resident on the device; `batch` contiguous rows
+ * complex[batch][N] (real_input 0) or real[batch][N] (real_input 1) ->
+ * complex[batch][M].  N + M - 1 <= 2^24. */
+typedef struct vv_dsp_czt_plan vv_dsp_czt_plan;
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_czt_plan_create(size_t N, size_t M, vv_dsp_real W_real, vv_dsp_real W_imag,
+                                                      vv_dsp_real A_real, vv_dsp_real A_imag, vv_dsp_czt_plan** out);
+vv_dsp_status vv_dsp_czt_plan_destroy(vv_dsp_czt_plan* p);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_czt_execute_device(const vv_dsp_czt_plan* p, const void* d_in, int real_input,
+                                                         size_t batch, vv_dsp_cpx* d_out, void* stream);
+/* Cepstrum family on `batch` contiguous rows of n (cepstrum.c:7-78, minphase.c:7-31) */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_cepstrum_real_device(const vv_dsp_real* d_x, size_t n, size_t batch,
+                                                           vv_dsp_real* d_cep, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_icepstrum_minphase_device(const vv_dsp_real* d_c, size_t n, size_t batch,
+                                                                vv_dsp_real* d_x, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_minphase_from_cepstrum_device(const vv_dsp_real* d_c, size_t n, size_t batch,
+                                                                    vv_dsp_cpx* d_spec, void* stream);
 
 #ifdef __cplusplus
 }

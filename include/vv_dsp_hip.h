@@ -23,6 +23,9 @@
  *   vvhip_fir_*  : src/filter/fir.c:75-196 (apply_fft, apply)
  *   vvhip_hilbert_*: src/spectral/hilbert.c:14-75
  *   vvhip_dct_*  : src/spectral/dct.c:86-136
+ *   vvhip_czt_*  : src/spectral/czt.c:44-178 (exec_cpx, exec_real)
+ *   vvhip_cepstrum_* / _icepstrum_minphase_* / _minphase_from_cepstrum_*:
+ *                  src/envelope/cepstrum.c:7-78, src/envelope/minphase.c:7-31
  */
 #ifndef VV_DSP_HIP_H
 #define VV_DSP_HIP_H
@@ -38,6 +41,7 @@ typedef struct vvhip_fft vvhip_fft;
 typedef struct vvhip_stft vvhip_stft;
 typedef struct vvhip_fir vvhip_fir;
 typedef struct vvhip_mel vvhip_mel;
+typedef struct vvhip_czt vvhip_czt;
 
 /* Number of usable HIP devices (0 when none: every other call then fails). */
 int vvhip_available(void);
@@ -147,6 +151,29 @@ int vvhip_inst_phase_host(const float* z, size_t n, float* phase);
 int vvhip_inst_phase_device(const float* d_z, size_t n, size_t batch, float* d_phase, void* stream);
 int vvhip_inst_freq_host(const float* phase, size_t n, double fs, float* freq);
 int vvhip_inst_freq_device(const float* d_phase, size_t n, size_t batch, double fs, float* d_freq, void* stream);
+
+/* ---- Chirp-z transform (src/spectral/czt.c:58-178) ----
+ * X[k] = sum_{n<N} x[n] A^-n W^(nk), k < M (scipy.signal.czt convention).  A plan
+ * holds the chirps and the chirp's spectrum for P = next_pow2(N + M - 1) <= 2^24.
+ * Device: `batch` contiguous rows, x complex[batch][N] (real_in 0) or
+ * real[batch][N] (real_in 1) -> X complex[batch][M]. */
+int vvhip_czt_create(size_t n, size_t m, float w_re, float w_im, float a_re, float a_im, vvhip_czt** out);
+void vvhip_czt_destroy(vvhip_czt* h);
+int vvhip_czt_exec_device(const vvhip_czt* h, const void* d_x, int real_in, size_t batch, void* d_X,
+                          void* stream);
+int vvhip_czt_exec_host(const void* x, int real_in, size_t n, size_t m, float w_re, float w_im, float a_re,
+                        float a_im, void* X);
+
+/* ---- Cepstrum / minimum phase (src/envelope/cepstrum.c:7-78, minphase.c:7-31) ----
+ * `batch` contiguous rows of n: real cepstrum Re IFFT(log(|FFT x| + 1e-12));
+ * Re IFFT(exp(Re FFT(fold c))) and the spectrum exp(Re FFT(fold c)) (complex,
+ * imaginary parts 0), fold c = (c0, 2 c1 .. 2 c(n/2-1), 0 ..). */
+int vvhip_cepstrum_device(const float* d_x, size_t n, size_t batch, float* d_c, void* stream);
+int vvhip_icepstrum_minphase_device(const float* d_c, size_t n, size_t batch, float* d_x, void* stream);
+int vvhip_minphase_from_cepstrum_device(const float* d_c, size_t n, size_t batch, float* d_spec, void* stream);
+int vvhip_cepstrum_host(const float* x, size_t n, float* c);
+int vvhip_icepstrum_minphase_host(const float* c, size_t n, float* x);
+int vvhip_minphase_from_cepstrum_host(const float* c, size_t n, float* spec);
 
 /* ---- DCT (dct.c:86-136); nan_policy as core/nan_policy.h (0..3) ---- */
 int vvhip_dct_host(const float* in, float* out, size_t n, int type, int dir, int nan_policy);

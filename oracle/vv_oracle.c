@@ -563,3 +563,151 @@ int orc_overlap_add(const float* frame, float* out, size_t out_len, size_t frame
         if (s0 + i < out_len) out[s0 + i] += frame[i];
     return 0;
 }
+
+/* ---- CZT (src/spectral/czt.c) ------------------------------------------ */
+/* czt.c:10-12 -- product without FMA contraction (the file is built -ffp-contract=off) */
+static ocpx orc_cmul(ocpx a, ocpx b) {
+    ocpx r;
+    r.re = a.re * b.re - a.im * b.im;
+    r.im = a.re * b.im + a.im * b.re;
+    return r;
+}
+
+/* czt.c:22-42 */
+int orc_czt_params(float f_start, float f_end, size_t M, float fs, float* w, float* a) {
+    if (!w || !a) return 1;
+    if (M == 0 || fs <= 0.0f) return 2;
+    const float delta = (f_end - f_start) / (float)M;
+    const float theta = (float)(-2.0 * ORC_PI_D * (double)delta / (double)fs);
+    w[0] = cosf(theta);
+    w[1] = sinf(theta);
+    const float phi0 = (float)(-2.0 * ORC_PI_D * (double)f_start / (double)fs);
+    a[0] = cosf(phi0);
+    a[1] = sinf(phi0);
+    return 0;
+}
+
+/* W^{+-e}: czt.c:96-101 / 147-153 (e, ang, mag rounded to float, powf/cosf/sinf) */
+static ocpx czt_chirp(float e, float argW, float magW, int sign) {
+    const float ang = sign > 0 ? e * argW : -e * argW;
+    const float mag = powf(magW, sign > 0 ? e : -e);
+    ocpx z;
+    z.re = mag * cosf(ang);
+    z.im = mag * sinf(ang);
+    return z;
+}
+
+/* czt.c:58-178: Bluestein with P = next_pow2(N + M - 1), Kiss FFTs (orc_fft_c2c) */
+int orc_czt_cpx(const float* x, size_t N, size_t M, float w_re, float w_im, float a_re, float a_im, float* X) {
+    if (!x || !X) return 1;
+    if (N == 0 || M == 0) return 2;
+    const ocpx* xc = (const ocpx*)x;
+    ocpx A = {a_re, a_im};
+    ocpx A_inv = {A.re, -A.im};
+    const float denom = A.re * A.re + A.im * A.im;
+    if (denom != 0.0f) { A_inv.re = A.re / denom; A_inv.im = -A.im / denom; }
+    const float argW = (float)atan2f((float)(double)w_im, (float)(double)w_re);
+    const float magW = (float)hypot((double)w_re, (double)w_im);
+    size_t L = N + M - 1, P = 1;
+    while (P < L) P <<= 1;
+    ocpx* a = (ocpx*)calloc(P, sizeof(ocpx));
+    ocpx* b = (ocpx*)calloc(P, sizeof(ocpx));
+    ocpx* Af = (ocpx*)malloc(P * sizeof(ocpx));
+    ocpx* Bf = (ocpx*)malloc(P * sizeof(ocpx));
+    if (!a || !b || !Af || !Bf) { free(a); free(b); free(Af); free(Bf); return 4; }
+    ocpx A_inv_pow = {1.0f, 0.0f};
+    for (size_t n = 0; n < N; ++n) {   /* :90-108, g[n] = A^-n W^(n^2/2) by recurrence */
+        const float e = 0.5f * (float)((double)n * (double)n);
+        const ocpx Wn2 = czt_chirp(e, argW, magW, +1);
+        if (n == 0) { A_inv_pow.re = 1.0f; A_inv_pow.im = 0.0f; }
+        else A_inv_pow = orc_cmul(A_inv_pow, A_inv);
+        a[n] = orc_cmul(xc[n], orc_cmul(A_inv_pow, Wn2));   /* :140 */
+    }
+    for (size_t i = 0; i < L; ++i) {   /* :142-150 b[i] = W^(-(i-(N-1))^2/2) */
+        const long m = (long)i - (long)(N - 1);
+        const float dm = (float)m;
+        b[i] = czt_chirp(0.5f * dm * dm, argW, magW, -1);
+    }
+    orc_fft_c2c((const float*)a, (float*)Af, P, 1);
+    orc_fft_c2c((const float*)b, (float*)Bf, P, 1);
+    for (size_t i = 0; i < P; ++i) Af[i] = orc_cmul(Af[i], Bf[i]);   /* :161-163 */
+    orc_fft_c2c((const float*)Af, (float*)a, P, -1);                  /* :166, x 1/P */
+    ocpx* Xc = (ocpx*)X;
+    for (size_t k = 0; k < M; ++k) {   /* :169-178 */
+        const float e = 0.5f * (float)(k * (double)k);
+        Xc[k] = orc_cmul(a[(N - 1) + k], czt_chirp(e, argW, magW, +1));
+    }
+    free(a); free(b); free(Af); free(Bf);
+    return 0;
+}
+
+/* czt.c:44-56: real input promoted to complex */
+int orc_czt_real(const float* x, size_t N, size_t M, float w_re, float w_im, float a_re, float a_im, float* X) {
+    if (!x || !X) return 1;
+    float* xc = (float*)calloc(2 * (N ? N : 1), sizeof(float));
+    if (!xc) return 4;
+    for (size_t n = 0; n < N; ++n) xc[2 * n] = x[n];
+    const int st = orc_czt_cpx(xc, N, M, w_re, w_im, a_re, a_im, X);
+    free(xc);
+    return st;
+}
+
+/* ---- cepstrum / minimum phase (src/envelope/cepstrum.c, minphase.c) ---- */
+/* cepstrum.c:7-41: Re(IFFT(log(|FFT(x)| + 1e-12))) with C2C transforms */
+int orc_cepstrum_real(const float* x, size_t n, float* c) {
+    if (!x || !c) return 1;
+    ocpx* t = (ocpx*)calloc(3 * (n ? n : 1), sizeof(ocpx));
+    if (!t) return 4;
+    ocpx *xin = t, *X = t + n, *Y = t + 2 * n;
+    for (size_t i = 0; i < n; ++i) { xin[i].re = x[i]; xin[i].im = 0.0f; }
+    orc_fft_c2c((const float*)xin, (float*)X, n, 1);
+    for (size_t k = 0; k < n; ++k) {
+        const float mag = sqrtf(X[k].re * X[k].re + X[k].im * X[k].im);
+        Y[k].re = logf(mag + 1e-12f);
+        Y[k].im = 0.0f;
+    }
+    orc_fft_c2c((const float*)Y, (float*)xin, n, -1);
+    for (size_t i = 0; i < n; ++i) c[i] = xin[i].re;
+    free(t);
+    return 0;
+}
+
+/* cepstrum.c:48-57 / minphase.c:15-19: the causal fold of a cepstrum */
+static void ceps_fold(const float* c, size_t n, ocpx* C) {
+    const size_t nh = n / 2;
+    for (size_t i = 0; i < n; ++i) { C[i].re = 0.0f; C[i].im = 0.0f; }
+    if (n > 0) C[0].re = c[0];
+    for (size_t i = 1; i < nh; ++i) C[i].re = 2 * c[i];
+    if (n % 2 == 0 && nh < n) C[nh].re = 0.0f;
+}
+
+/* cepstrum.c:43-78: Re(IFFT(expf(Re FFT(fold(c))))) */
+int orc_icepstrum_minphase(const float* c, size_t n, float* x) {
+    if (!c || !x) return 1;
+    ocpx* t = (ocpx*)calloc(3 * (n ? n : 1), sizeof(ocpx));
+    if (!t) return 4;
+    ocpx *C = t, *H = t + n, *h = t + 2 * n;
+    ceps_fold(c, n, C);
+    orc_fft_c2c((const float*)C, (float*)H, n, 1);
+    for (size_t k = 0; k < n; ++k) { H[k].re = expf(H[k].re); H[k].im = 0.0f; }
+    orc_fft_c2c((const float*)H, (float*)h, n, -1);
+    for (size_t i = 0; i < n; ++i) x[i] = h[i].re;
+    free(t);
+    return 0;
+}
+
+/* minphase.c:7-31: spec[k] = ((float)exp((double)Re FFT(fold(c))[k]), 0) */
+int orc_minphase_from_cepstrum(const float* c, size_t n, float* spec) {
+    if (!c || !spec) return 1;
+    ocpx* t = (ocpx*)calloc(2 * (n ? n : 1), sizeof(ocpx));
+    if (!t) return 4;
+    ocpx *C = t, *H = t + n;
+    ceps_fold(c, n, C);
+    orc_fft_c2c((const float*)C, (float*)H, n, 1);
+    for (size_t k = 0; k < n; ++k) {
+        spec[2 * k] = (float)exp((double)H[k].re);
+        spec[2 * k + 1] = 0.0f;
+    }
+    free(t);
+    return 0;
+}

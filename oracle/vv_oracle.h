@@ -73,6 +73,18 @@ int orc_log_mel(const float* power, size_t frames, size_t nb, const float* fb, s
 int orc_mfcc(const float* log_mel, size_t frames, size_t n_mels, size_t n_coeffs, float lifter,
              float* out);                                                 /* :249-309 */
 
+/* ---- CZT (src/spectral/czt.c) ---- w, a: {re, im} of W and A; X complex[M] */
+int orc_czt_params(float f_start, float f_end, size_t M, float fs, float* w, float* a);  /* :22-42 */
+int orc_czt_cpx(const float* x, size_t N, size_t M, float w_re, float w_im, float a_re, float a_im,
+                float* X);                                                /* :58-178 */
+int orc_czt_real(const float* x, size_t N, size_t M, float w_re, float w_im, float a_re, float a_im,
+                 float* X);                                               /* :44-56 */
+
+/* ---- cepstrum / minimum phase (src/envelope/cepstrum.c, minphase.c) ---- */
+int orc_cepstrum_real(const float* x, size_t n, float* c);               /* cepstrum.c:7-41 */
+int orc_icepstrum_minphase(const float* c, size_t n, float* x);          /* cepstrum.c:43-78 */
+int orc_minphase_from_cepstrum(const float* c, size_t n, float* spec);   /* minphase.c:7-31 */
+
 #ifdef __cplusplus
 }
 #endif

@@ -139,6 +139,21 @@ def case_dct(n, batch):
     return (lambda: vv.dct(x)), batch * n * 8, (x,)
 
 
+def case_czt(n, m, batch):
+    """batched chirp-z (czt.c:44-178) at a zoom arc; bytes = rows in + outputs"""
+    import numpy as np
+    x = torch.complex(torch.rand(batch, n, device="cuda") - 0.5, torch.rand(batch, n, device="cuda") - 0.5)
+    p = vv.CztPlan(n, m, np.exp(-2j * np.pi * 0.05 / m), np.exp(0.3j))
+    y = torch.empty(batch, m, dtype=torch.complex64, device="cuda")
+    return (lambda: p(x, out=y)), batch * 8 * (n + m), (x, y, p)
+
+
+def case_cepstrum(n, batch, kind=0):
+    x = torch.rand(batch, n, device="cuda") * 2 - 1
+    f = (vv.cepstrum, vv.icepstrum_minphase)[kind]
+    return (lambda: f(x)), batch * n * 8, (x,)
+
+
 def case_copy(nbytes):
     a = torch.empty(nbytes // 4, device="cuda")
     b = torch.empty_like(a)
@@ -357,6 +372,10 @@ CASES = {
     "ola": lambda: case_ola(),
     "olaold": with_env(lambda: case_ola(), "VVHIP_ISTFT_OLD", "1"),
     "dct1024": lambda: case_dct(1024, 131072),
+    "czt1000": lambda: case_czt(1000, 1000, 16384),
+    "czt48000": lambda: case_czt(48000, 4096, 256),
+    "ceps1024": lambda: case_cepstrum(1024, 65536),
+    "iceps1024": lambda: case_cepstrum(1024, 65536, 1),
 }
 # A/B switches for launcher experiments: CASES["stftX"] = with_env(CASES["stft"], "VVHIP_EXP_...", "1")
 

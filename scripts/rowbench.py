@@ -227,6 +227,33 @@ def main():
                    note="compute-bound: 257 multiply-adds per sample in the reference's order, no FMA"))
     del xf, yf, fp
 
+    # ---- f4 (CZT, czt.c:44-178) and the cepstrum family (8b callers) ---------------------
+    for n, m, B, label in ((1000, 1000, 16384, "czt_1000x1000_zoom"), (48000, 4096, 256, "czt_48000x4096_zoom")):
+        w, aa = np.exp(-2j * np.pi * 0.05 / m), np.exp(0.3j)
+        xz = torch.complex(torch.rand(B, n, device="cuda") - 0.5, torch.rand(B, n, device="cuda") - 0.5)
+        cz = vv.CztPlan(n, m, w, aa)
+        yz = torch.empty(B, m, dtype=torch.complex64, device="cuda")
+        ms = gpu_time(lambda: cz(xz, out=yz), a.reps)
+        P = 1 << (n + m - 2).bit_length()
+        xzh = (rng.random(n) + 1j * rng.random(n)).astype(np.complex64)
+        out.append(row(label, f"f4 vv_dsp_czt_exec_cpx, N = {n}, M = {m} (P = {P})", (f"{B} rows", B), ms,
+                       B * 8 * (n + m), "transforms", cpu(lambda: ref.czt(xzh, m, complex(w), complex(aa)), 1),
+                       note="algorithmic bytes = rows in + outputs; the chain moves ~4 x 16 P per row (pre-multiply, "
+                            "two P-point FFTs, product, post-multiply)"))
+        del xz, yz, cz
+    B = 65536
+    xc = torch.rand(B, 1024, device="cuda") * 2 - 1
+    ms = gpu_time(lambda: vv.cepstrum(xc), a.reps)
+    xch = rng.standard_normal(1024).astype(np.float32)
+    out.append(row("cepstrum_1024", "8b vv_dsp_cepstrum_real (R2C, log|X|, C2R)", (f"{B} x 1024", B), ms,
+                   8 * 1024 * B, "transforms", cpu(lambda: ref.cepstrum(xch), 1),
+                   note="the reference runs two C2C FFTs (Kiss radix-2 at n = 1024)"))
+    ms = gpu_time(lambda: vv.icepstrum_minphase(xc), a.reps)
+    out.append(row("icepstrum_minphase_1024", "8b vv_dsp_icepstrum_minphase", (f"{B} x 1024", B), ms,
+                   8 * 1024 * B, "transforms", cpu(lambda: ref.icepstrum_minphase(0.05 * xch), 1)))
+    del xc
+    torch.cuda.empty_cache()
+
     # ---- host-buffer (PCIe-inclusive) rate of the reference's own host-pointer API ------
     # vv_dsp_stft_spectrogram / vv_dsp_fft_execute take host pointers: the library copies
     # H2D, runs the kernel and copies D2H on the handle's stream (two-lane pipeline).

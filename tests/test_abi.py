@@ -11,7 +11,7 @@ import re
 import pytest
 
 from conftest import ROOT
-from vvapi import (VvDsp, StftParams, FirState, OK, ERR_NULL, ERR_SIZE, ERR_RANGE, ERR_UNSUPPORTED,
+from vvapi import (VvDsp, StftParams, FirState, OK, ERR_NULL, ERR_SIZE, ERR_RANGE, ERR_INTERNAL, ERR_UNSUPPORTED,
                    C2C, R2C, FWD, BWD, KISS, HIP)
 
 DECL = re.compile(r"\b((?:vv_dsp|vvhip)_\w+)\s*\(")
@@ -91,6 +91,22 @@ def test_argument_validation_matches_reference(cpu_lib, ref):
         assert L.vv_dsp_instantaneous_phase(hp, 0, hp) == ERR_SIZE
         assert L.vv_dsp_instantaneous_frequency(hp, 4, 1000.0, None) == ERR_NULL
         assert L.vv_dsp_instantaneous_frequency(hp, 0, 1000.0, hp) == ERR_SIZE
+        # czt.c:22-63, cepstrum.c:7-11 / 43-48, minphase.c:7-10 (n = 0: the FFT plan fails -> INTERNAL)
+        lib.czt_params(0.0, 1.0, 4, 1000.0)   # binds argtypes
+        f = C.c_float()
+        fpp = C.cast(C.byref(f), C.POINTER(C.c_float))
+        assert L.vv_dsp_czt_params_for_freq_range(0.0, 1.0, 4, 1000.0, None, fpp, fpp, fpp) == ERR_NULL
+        assert L.vv_dsp_czt_params_for_freq_range(0.0, 1.0, 0, 1000.0, fpp, fpp, fpp, fpp) == ERR_SIZE
+        assert L.vv_dsp_czt_params_for_freq_range(0.0, 1.0, 4, 0.0, fpp, fpp, fpp, fpp) == ERR_SIZE
+        for fn in (L.vv_dsp_czt_exec_cpx, L.vv_dsp_czt_exec_real):
+            assert fn(None, 4, 4, 1.0, 0.0, 1.0, 0.0, hp) == ERR_NULL
+            assert fn(hp, 4, 4, 1.0, 0.0, 1.0, 0.0, None) == ERR_NULL
+            assert fn(hp, 0, 4, 1.0, 0.0, 1.0, 0.0, hp) == ERR_SIZE
+            assert fn(hp, 4, 0, 1.0, 0.0, 1.0, 0.0, hp) == ERR_SIZE
+        for fn in (L.vv_dsp_cepstrum_real, L.vv_dsp_icepstrum_minphase, L.vv_dsp_minphase_from_cepstrum):
+            assert fn(None, 4, hp) == ERR_NULL
+            assert fn(hp, 4, None) == ERR_NULL
+            assert fn(hp, 0, hp) == ERR_INTERNAL
 
 
 def test_fir_design_bitexact_host_setup(cpu_lib, orc):
@@ -100,6 +116,14 @@ def test_fir_design_bitexact_host_setup(cpu_lib, orc):
             import numpy as np
             assert np.array_equal(cpu_lib.fir_design_lowpass(taps, 0.3, wk), orc.fir_design_lowpass(taps, 0.3, wk),
                                   equal_nan=True)
+
+
+def test_czt_params_bitexact_host_setup(cpu_lib, ref):
+    """vv_dsp_czt_params_for_freq_range is scalar host setup with the reference's
+    float arithmetic (czt.c:22-42): bit-identical."""
+    for args in ((800.0, 1200.0, 64, 48000.0), (0.0, 24000.0, 1024, 48000.0), (-100.0, 100.0, 3, 1000.0),
+                 (5.0, 5.0, 7, 44100.0)):
+        assert cpu_lib.czt_params(*args) == ref.czt_params(*args)
 
 
 def test_mel_filterbank_bitexact_host_setup(cpu_lib, orc, ref):
@@ -160,6 +184,12 @@ def test_no_gpu_fails_loudly(cpu_lib):
     assert L.vv_dsp_fir_apply(C.byref(st), fp(x), fp(x), fp(z), 64) == ERR_UNSUPPORTED
     assert L.vv_dsp_fir_apply_fft(C.byref(st), fp(x), fp(x), fp(z), 64) == ERR_UNSUPPORTED
     L.vv_dsp_fir_state_free(C.byref(st))
+    cpu_lib.czt_params(0.0, 1.0, 4, 1000.0)   # binds argtypes
+    assert L.vv_dsp_czt_exec_cpx(fp(z), 32, 32, 1.0, 0.0, 1.0, 0.0, fp(z)) == ERR_UNSUPPORTED
+    assert L.vv_dsp_czt_exec_real(fp(x), 32, 32, 1.0, 0.0, 1.0, 0.0, fp(z)) == ERR_UNSUPPORTED
+    assert L.vv_dsp_cepstrum_real(fp(x), 64, fp(x)) == ERR_UNSUPPORTED
+    assert L.vv_dsp_icepstrum_minphase(fp(x), 64, fp(x)) == ERR_UNSUPPORTED
+    assert L.vv_dsp_minphase_from_cepstrum(fp(x), 64, fp(z)) == ERR_UNSUPPORTED
     assert b"no HIP device" in L.vvhip_last_error()
 
 

@@ -155,3 +155,72 @@ def test_golden_kiss_accuracy_profile(golden):
     for n in (1024, 255):
         g = golden(f"hilbert_n{n}")
         assert np.max(np.abs(g["kiss"] - g["np64"])) < 1e-4
+
+
+# ---- CZT and cepstrum family (src/spectral/czt.c, src/envelope/cepstrum.c, minphase.c) ----
+CZT_CASES = [(8, 8), (32, 32), (100, 64), (257, 300), (1000, 17), (1, 5), (5, 1)]
+
+
+def test_oracle_czt_bitexact_vs_reference(orc, ref):
+    """czt.c:22-178 restated (float chirps, Kiss FFTs of P = next_pow2(N+M-1)):
+    bit-identical to the compiled reference for complex and real input, DFT and
+    zoom parameters."""
+    rng = np.random.default_rng(31)
+    for n, m in CZT_CASES:
+        x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+        for w, a in ((np.exp(-2j * np.pi / n), 1.0 + 0j), (np.exp(-2j * np.pi * 0.37 / m), np.exp(0.3j)),
+                     (1.001 * np.exp(-0.05j), 0.999 * np.exp(0.2j))):
+            assert np.array_equal(orc.czt(x, m, w, a), ref.czt(x, m, w, a), equal_nan=True), (n, m, w, a)
+            xr = x.real.astype(np.float32)
+            assert np.array_equal(orc.czt(xr, m, w, a), ref.czt(xr, m, w, a), equal_nan=True), (n, m)
+    for args in ((800.0, 1200.0, 64, 48000.0), (0.0, 24000.0, 1024, 48000.0), (-100.0, 100.0, 3, 1000.0)):
+        assert orc.czt_params(*args) == ref.czt_params(*args)
+    assert ref.czt_params(0.0, 1.0, 0, 1000.0)[0] == orc.czt_params(0.0, 1.0, 0, 1000.0)[0] == 2
+    assert ref.czt_params(0.0, 1.0, 4, 0.0)[0] == orc.czt_params(0.0, 1.0, 4, 0.0)[0] == 2
+
+
+def test_reference_czt_known_answers(ref):
+    """czt_tests.c:10-39 (impulse -> ones at DFT parameters, 1e-3) and the
+    reference's python/test_czt.py cases against scipy.signal.czt at its
+    rtol = atol = 2e-4 (N = M = 32 and the 800-1200 Hz zoom of a 1 kHz tone)."""
+    from scipy.signal import czt
+    n = 8
+    x = np.zeros(n, np.complex64)
+    x[0] = 1
+    X = ref.czt(x, n, np.exp(-2j * np.pi / n), 1.0 + 0j)
+    assert np.allclose(X, 1.0, atol=1e-3)
+    rng = np.random.default_rng(0)
+    x = (rng.standard_normal(32) + 1j * rng.standard_normal(32)).astype(np.complex64)
+    w = complex(np.complex64(np.exp(-2j * np.pi / 32)))
+    np.testing.assert_allclose(ref.czt(x, 32, w, 1.0 + 0j), czt(x.astype(np.complex128), m=32, w=w, a=1.0),
+                               rtol=2e-4, atol=2e-4)
+    fs, f0 = 48000.0, 1000.0
+    xr = np.cos(2 * np.pi * f0 * np.arange(32) / fs).astype(np.float32)
+    W = np.exp(-1j * 2 * np.pi * ((1200.0 - 800.0) / 64) / fs)
+    A = np.exp(-1j * 2 * np.pi * 800.0 / fs)
+    Wf, Af = complex(np.complex64(W)), complex(np.complex64(A))
+    np.testing.assert_allclose(ref.czt(xr, 64, Wf, Af), czt(xr.astype(np.float64), m=64, w=Wf, a=Af),
+                               rtol=2e-4, atol=2e-4)
+
+
+def test_oracle_cepstrum_family_bitexact_vs_reference(orc, ref):
+    """cepstrum.c:7-78 and minphase.c:7-31 restated: bit-identical (NaN/inf where
+    the reference's expf overflows compare equal too)."""
+    rng = np.random.default_rng(32)
+    for n in (1, 2, 3, 16, 17, 64, 100, 1024):
+        x = rng.standard_normal(n).astype(np.float32)
+        assert np.array_equal(orc.cepstrum(x), ref.cepstrum(x), equal_nan=True), n
+        for c in (x, (0.05 * x).astype(np.float32)):
+            assert np.array_equal(orc.icepstrum_minphase(c), ref.icepstrum_minphase(c), equal_nan=True), n
+            assert np.array_equal(orc.minphase_from_cepstrum(c), ref.minphase_from_cepstrum(c), equal_nan=True), n
+
+
+def test_reference_envelope_known_answers(ref):
+    """envelope_tests.c:9-23: an impulse's cepstrum is ~0 (c0 1e-3, others 1e-2)
+    and its minimum-phase inverse starts at ~1."""
+    x = np.zeros(16, np.float32)
+    x[0] = 1
+    c = ref.cepstrum(x)
+    assert abs(c[0]) < 1e-3 and np.all(np.abs(c[1:]) < 1e-2)
+    assert abs(ref.icepstrum_minphase(c)[0] - 1.0) < 1e-2
+    assert np.all(np.isfinite(ref.minphase_from_cepstrum(c).view(np.float32)))

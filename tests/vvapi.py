@@ -46,7 +46,89 @@ def _cplx_view(a):
     return a.view(np.float32)
 
 
-class VvDsp:
+# ---- CZT and cepstrum (src/spectral/czt.c, src/envelope/{cepstrum,minphase}.c) ----
+# The same methods on both wrappers: VvDsp binds the public vv_dsp_* names
+# (reference or MI355X library), Oracle the orc_* restatement.
+def _czt_names(lib, prefix):
+    if prefix == "vv_dsp_":
+        return (lib.vv_dsp_czt_params_for_freq_range, lib.vv_dsp_czt_exec_cpx, lib.vv_dsp_czt_exec_real,
+                lib.vv_dsp_cepstrum_real, lib.vv_dsp_icepstrum_minphase, lib.vv_dsp_minphase_from_cepstrum)
+    return (lib.orc_czt_params, lib.orc_czt_cpx, lib.orc_czt_real, lib.orc_cepstrum_real,
+            lib.orc_icepstrum_minphase, lib.orc_minphase_from_cepstrum)
+
+
+class _CztMixin:
+    _prefix = "vv_dsp_"
+
+    def _czt_setup(self):
+        if getattr(self, "_czt_ok", False):
+            return self._czt_fns
+        fns = _czt_names(self.lib, self._prefix)
+        par, cpx, real, ceps, iceps, minph = fns
+        if self._prefix == "vv_dsp_":
+            par.argtypes = [C.c_float, C.c_float, C.c_size_t, C.c_float] + [_f32p] * 4
+        else:
+            par.argtypes = [C.c_float, C.c_float, C.c_size_t, C.c_float, _f32p, _f32p]
+        for f in (cpx, real):
+            f.argtypes = [_f32p, C.c_size_t, C.c_size_t] + [C.c_float] * 4 + [_f32p]
+        for f in (ceps, iceps, minph):
+            f.argtypes = [_f32p, C.c_size_t, _f32p]
+        self._czt_fns, self._czt_ok = fns, True
+        return fns
+
+    def czt_params(self, f_start, f_end, m, fs):
+        """-> (status, W, A) as complex (vv_dsp_czt_params_for_freq_range, czt.c:22-42)"""
+        par = self._czt_setup()[0]
+        if self._prefix == "vv_dsp_":
+            v = [C.c_float() for _ in range(4)]
+            st = par(f_start, f_end, m, fs, *[C.cast(C.byref(x), _f32p) for x in v])
+            return st, complex(v[0].value, v[1].value), complex(v[2].value, v[3].value)
+        w, a = np.zeros(2, np.float32), np.zeros(2, np.float32)
+        st = par(f_start, f_end, m, fs, _fp(w), _fp(a))
+        return st, complex(w[0], w[1]), complex(a[0], a[1])
+
+    def czt_status(self, x, m, w, a):
+        """-> (status, X complex64[m]); x complex -> czt_exec_cpx, real -> czt_exec_real"""
+        _, cpx, real = self._czt_setup()[:3]
+        X = np.zeros(2 * max(m, 1), np.float32)
+        if np.iscomplexobj(x):
+            xf = _cplx_view(x)
+            st = cpx(_fp(xf), len(x), m, w.real, w.imag, a.real, a.imag, _fp(X))
+        else:
+            xf = np.ascontiguousarray(x, np.float32)
+            st = real(_fp(xf), len(x), m, w.real, w.imag, a.real, a.imag, _fp(X))
+        return st, X.view(np.complex64)[:m]
+
+    def czt(self, x, m, w, a):
+        st, X = self.czt_status(x, m, w, a)
+        if st != OK:
+            raise RuntimeError(f"czt status {st}{self._err() if hasattr(self, '_err') else ''}")
+        return X
+
+    def _ceps_call(self, i, x, out_len):
+        f = self._czt_setup()[i]
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.zeros(max(out_len, 1), np.float32)
+        st = f(_fp(x), len(x), _fp(out))
+        if st != OK:
+            raise RuntimeError(f"cepstrum-family status {st}")
+        return out[:out_len]
+
+    def cepstrum(self, x):
+        """vv_dsp_cepstrum_real (cepstrum.c:7-41)"""
+        return self._ceps_call(3, x, len(x))
+
+    def icepstrum_minphase(self, c):
+        """vv_dsp_icepstrum_minphase (cepstrum.c:43-78)"""
+        return self._ceps_call(4, c, len(c))
+
+    def minphase_from_cepstrum(self, c):
+        """vv_dsp_minphase_from_cepstrum (minphase.c:7-31) -> complex64[n]"""
+        return self._ceps_call(5, c, 2 * len(c)).view(np.complex64)
+
+
+
+class VvDsp(_CztMixin):
     """Thin wrapper around a library exporting the vv_dsp_* API."""
 
     def __init__(self, path):
@@ -334,8 +416,9 @@ class VvDsp:
         return out
 
 
-class Oracle:
+class Oracle(_CztMixin):
     """Binding of oracle/liboracle.so (our C restatement; test infrastructure)."""
+    _prefix = "orc_"
 
     def __init__(self, path):
         self.lib = L = C.CDLL(path)
@@ -486,3 +569,4 @@ class Oracle:
             assert self.lib.orc_fir_apply(_fp(h), len(h), _fp(hist), C.byref(idx), _fp(x),
                                           _fp(y), len(x)) == 0
         return y
+

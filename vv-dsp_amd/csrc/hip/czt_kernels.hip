@@ -1,0 +1,126 @@
+// czt_kernels.hip -- element-wise stages of the chirp-z transform and of the
+// real cepstrum / minimum-phase family for gfx950.  The transforms between them
+// are the library's own FFT launches (fft_run in shim.hip).
+//
+// CZT (src/spectral/czt.c:58-178), X[k] = sum_n x[n] A^-n W^(nk), k < M, as
+// Bluestein's convolution with P = next_pow2(N + M - 1):
+//   a[i] = x[i] g[i] (i < N, else 0),  g[n] = A^-n W^(n^2/2)      k_czt_pre
+//   a <- IFFT(FFT(a) * B),  B = FFT(b), b[i] = W^(-(i-N+1)^2/2)    k_cmul_rows
+//   X[k] = a[N-1+k] W^(k^2/2)                                      k_czt_post
+// The chirps g, W^(k^2/2) and b are tabulated once per plan on the host in
+// extended precision (the reference rounds n^2/2 and its angle to float, which
+// loses the phase for N beyond a few hundred).
+//
+// Cepstrum (src/envelope/cepstrum.c:7-41): c = Re IFFT(log(|FFT(x)| + 1e-12)),
+// computed as R2C -> log-magnitude of the n/2+1 bins -> C2R (the log-magnitude
+// spectrum of a real signal is real and even, so C2R gives its real inverse).
+// Minimum phase (cepstrum.c:43-78, minphase.c:7-31): the causal fold of a
+// cepstrum (c0, 2c1 .. 2c(n/2-1), 0 ..), a C2C FFT, then exp of the real part.
+#include "fft_core.hpp"
+#include "vvhip_internal.hpp"
+
+namespace vvh {
+
+static inline unsigned czt_blocks(long long count) {
+    long long b = (count + 255) / 256;
+    if (b > 65536) b = 65536;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+#define CZT_GRID_STRIDE(i, count) \
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (count); i += (long long)gridDim.x * blockDim.x)
+
+// a[r][i] = x[r][i] * g[i] for i < n, 0 for n <= i < p; real_in: x is float[r][n]
+__global__ void k_czt_pre(const void* __restrict__ x, int real_in, long long n, long long p, long long rows,
+                          long long in_dist, const float2* __restrict__ g, float2* __restrict__ a) {
+    CZT_GRID_STRIDE(i, p * rows) {
+        const long long r = i / p, j = i - r * p;
+        float2 v = make_float2(0.0f, 0.0f);
+        if (j < n) {
+            const float2 xv = real_in ? make_float2(static_cast<const float*>(x)[r * in_dist + j], 0.0f)
+                                      : static_cast<const float2*>(x)[r * in_dist + j];
+            v = cmul(xv, g[j]);
+        }
+        a[i] = v;
+    }
+}
+
+hipError_t launch_czt_pre(const void* x, int real_in, long long n, long long p, long long rows, long long in_dist,
+                          const float2* g, float2* a, hipStream_t s) {
+    hipLaunchKernelGGL(k_czt_pre, dim3(czt_blocks(p * rows)), dim3(256), 0, s, x, real_in, n, p, rows, in_dist, g, a);
+    return hipGetLastError();
+}
+
+// a[r][i] *= B[i] (the chirp's spectrum, shared by every row)
+__global__ void k_cmul_rows(float2* __restrict__ a, const float2* __restrict__ B, long long p, long long rows) {
+    CZT_GRID_STRIDE(i, p * rows) {
+        const long long j = i % p;
+        a[i] = cmul(a[i], B[j]);
+    }
+}
+
+hipError_t launch_cmul_rows(float2* a, const float2* B, long long p, long long rows, hipStream_t s) {
+    hipLaunchKernelGGL(k_cmul_rows, dim3(czt_blocks(p * rows)), dim3(256), 0, s, a, B, p, rows);
+    return hipGetLastError();
+}
+
+// X[r][k] = a[r][n - 1 + k] * post[k], k < m
+__global__ void k_czt_post(const float2* __restrict__ a, long long n, long long p, long long m, long long rows,
+                           const float2* __restrict__ post, float2* __restrict__ X, long long out_dist) {
+    CZT_GRID_STRIDE(i, m * rows) {
+        const long long r = i / m, k = i - r * m;
+        X[r * out_dist + k] = cmul(a[r * p + (n - 1) + k], post[k]);
+    }
+}
+
+hipError_t launch_czt_post(const float2* a, long long n, long long p, long long m, long long rows, const float2* post,
+                           float2* X, long long out_dist, hipStream_t s) {
+    hipLaunchKernelGGL(k_czt_post, dim3(czt_blocks(m * rows)), dim3(256), 0, s, a, n, p, m, rows, post, X, out_dist);
+    return hipGetLastError();
+}
+
+// Y[i] = (logf(sqrtf(re^2 + im^2) + 1e-12f), 0)  (cepstrum.c:26-32, float build)
+__global__ void k_log_magnitude(float2* Y, long long count) {
+    CZT_GRID_STRIDE(i, count) {
+        const float2 v = Y[i];
+        Y[i] = make_float2(logf(sqrtf(v.x * v.x + v.y * v.y) + 1e-12f), 0.0f);
+    }
+}
+
+hipError_t launch_log_magnitude(float2* Y, long long count, hipStream_t s) {
+    hipLaunchKernelGGL(k_log_magnitude, dim3(czt_blocks(count)), dim3(256), 0, s, Y, count);
+    return hipGetLastError();
+}
+
+// C[r][i] = (c0, 0), (2 c[i], 0) for 1 <= i < n/2, else 0  (cepstrum.c:50-55, minphase.c:15-19)
+__global__ void k_cepstrum_fold(const float* __restrict__ c, long long n, long long rows, float2* __restrict__ C) {
+    const long long nh = n / 2;
+    CZT_GRID_STRIDE(i, n * rows) {
+        const long long j = i % n;
+        float v = 0.0f;
+        if (j == 0) v = c[i];
+        else if (j < nh) v = 2.0f * c[i];
+        C[i] = make_float2(v, 0.0f);
+    }
+}
+
+hipError_t launch_cepstrum_fold(const float* c, long long n, long long rows, float2* C, hipStream_t s) {
+    hipLaunchKernelGGL(k_cepstrum_fold, dim3(czt_blocks(n * rows)), dim3(256), 0, s, c, n, rows, C);
+    return hipGetLastError();
+}
+
+// H[i] = (exp(Re H[i]), 0): dbl = 0 expf (cepstrum.c:64-69), 1 (float)exp((double)..) (minphase.c:24)
+__global__ void k_exp_real(float2* H, long long count, int dbl) {
+    CZT_GRID_STRIDE(i, count) {
+        const float re = H[i].x;
+        H[i] = make_float2(dbl ? (float)exp((double)re) : expf(re), 0.0f);
+    }
+}
+
+hipError_t launch_exp_real(float2* H, long long count, int dbl, hipStream_t s) {
+    hipLaunchKernelGGL(k_exp_real, dim3(czt_blocks(count)), dim3(256), 0, s, H, count, dbl);
+    return hipGetLastError();
+}
+
+}  // namespace vvh

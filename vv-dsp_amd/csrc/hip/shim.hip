@@ -1287,3 +1287,228 @@ int vvhip_mel_host(vvhip_mel* m, const float* in, size_t frames, float* out, int
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Chirp-z transform (src/spectral/czt.c:58-178) and the cepstrum family
+// (src/envelope/cepstrum.c:7-78, minphase.c:7-31): element-wise kernels of
+// czt_kernels.hip around the library's own FFTs (fft_run).
+// ---------------------------------------------------------------------------
+struct vvhip_czt {
+    size_t n = 0, m = 0, p = 0;
+    float2* g = nullptr;      // [n] A^-n W^(n^2/2)
+    float2* post = nullptr;   // [m] W^(k^2/2)
+    float2* B = nullptr;      // [p] FFT_p of b[i] = W^(-(i-n+1)^2/2), zero past n+m-1
+};
+
+namespace {
+
+// z^e for z = exp(lm + i th) (lm = log|z|, th = arg z) in extended precision:
+// e = k^2/2 is exact, the angle is reduced mod 2 pi before cos/sin.  |z| enters
+// rounded to float, as the reference's magW = (float)hypot(W) (czt.c:81-82): the
+// float components of exp(-2 pi i / N) then give an exact unit-circle arc (their
+// |W| = 1 +- 1e-8 would otherwise grow a spiral factor of e^(k^2 * 1e-8 / 2)).
+struct Chirp {
+    long double lm, th;
+    Chirp(float re, float im)
+        : lm(logl((long double)(float)hypot((double)re, (double)im))), th(atan2l((long double)im, (long double)re)) {}
+};
+float2 chirp_value(long double log_mag, long double angle) {
+    const long double two_pi = 6.283185307179586476925286766559005768L;
+    const long double a = fmodl(angle, two_pi);
+    const long double mag = expl(log_mag);
+    return make_float2((float)(mag * cosl(a)), (float)(mag * sinl(a)));
+}
+
+int czt_run(const vvhip_czt* h, const void* x, int real_in, size_t batch, float2* X, hipStream_t s) {
+    if (batch == 0) return ST_OK;
+    const size_t p = h->p, esz = real_in ? sizeof(float) : sizeof(float2);
+    size_t rows = ((size_t)256 << 20) / (8 * p);   // scratch <= 256 MiB per chunk
+    if (rows < 1) rows = 1;
+    if (rows > batch) rows = batch;
+    Scratch a(s);
+    HIPCHK(a.alloc(8 * p * rows), ST_INTERNAL);
+    float2* ap = (float2*)a.p;
+    for (size_t r0 = 0; r0 < batch; r0 += rows) {
+        const size_t rc = batch - r0 < rows ? batch - r0 : rows;
+        HIPCHK(launch_czt_pre((const char*)x + esz * h->n * r0, real_in, (long long)h->n, (long long)p,
+                              (long long)rc, (long long)h->n, h->g, ap, s),
+               ST_INTERNAL);
+        int st = fft_run(p, 0, 1, ap, ap, rc, s);
+        if (st) return st;
+        HIPCHK(launch_cmul_rows(ap, h->B, (long long)p, (long long)rc, s), ST_INTERNAL);
+        if ((st = fft_run(p, 0, -1, ap, ap, rc, s))) return st;
+        HIPCHK(launch_czt_post(ap, (long long)h->n, (long long)p, (long long)h->m, (long long)rc, h->post,
+                               X + h->m * r0, (long long)h->m, s),
+               ST_INTERNAL);
+    }
+    return ST_OK;
+}
+
+// One call through the device: in_bytes up, run(din, dout, stream), out_bytes down.
+template <class F>
+int host_io(const void* in, size_t in_bytes, void* out, size_t out_bytes, const char* what, F&& run) {
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), ST_INTERNAL);
+    int st = ST_OK;
+    {
+        Scratch din(s), dout(s);
+        if (din.alloc(in_bytes) != hipSuccess || dout.alloc(out_bytes) != hipSuccess ||
+            hipMemcpyAsync(din.p, in, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess) {
+            st = fail(ST_INTERNAL, what);
+        } else if ((st = run(din.p, dout.p, s)) == ST_OK &&
+                   (hipMemcpyAsync(out, dout.p, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess)) {
+            st = fail(ST_INTERNAL, what);
+        }
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vvhip_czt_create(size_t n, size_t m, float w_re, float w_im, float a_re, float a_im, vvhip_czt** out) {
+    if (!out) return ST_NULL;
+    *out = nullptr;
+    if (n == 0 || m == 0) return ST_SIZE;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    const size_t L = n + m - 1;
+    size_t p = 1;
+    while (p < L) p <<= 1;
+    if (p > ((size_t)1 << 24)) return fail(ST_UNSUP, "CZT: N + M - 1 above 2^24");
+    const Chirp W(w_re, w_im), A(a_re, a_im);
+    std::vector<float2> g(n), post(m), b(p, make_float2(0.0f, 0.0f));
+    for (size_t k = 0; k < n; ++k) {   // A^-k W^(k^2/2)
+        const long double e = 0.5L * (long double)k * (long double)k, kk = (long double)k;
+        g[k] = chirp_value(e * W.lm - kk * A.lm, e * W.th - kk * A.th);
+    }
+    for (size_t k = 0; k < m; ++k) {
+        const long double e = 0.5L * (long double)k * (long double)k;
+        post[k] = chirp_value(e * W.lm, e * W.th);
+    }
+    for (size_t i = 0; i < L; ++i) {   // W^(-j^2/2), j = i - (n - 1)
+        const long double j = (long double)i - (long double)(n - 1), e = 0.5L * j * j;
+        b[i] = chirp_value(-e * W.lm, -e * W.th);
+    }
+    vvhip_czt* h = new (std::nothrow) vvhip_czt;
+    if (!h) return fail(ST_INTERNAL, "czt alloc");
+    h->n = n;
+    h->m = m;
+    h->p = p;
+    int st = ST_OK;
+    if (hipMalloc(&h->g, 8 * n) != hipSuccess || hipMalloc(&h->post, 8 * m) != hipSuccess ||
+        hipMalloc(&h->B, 8 * p) != hipSuccess || hipMemcpy(h->g, g.data(), 8 * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->post, post.data(), 8 * m, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->B, b.data(), 8 * p, hipMemcpyHostToDevice) != hipSuccess) {
+        st = fail(ST_INTERNAL, "czt tables");
+    } else if ((st = fft_run(p, 0, 1, h->B, h->B, 1, nullptr)) == ST_OK && hipDeviceSynchronize() != hipSuccess) {
+        st = fail(ST_INTERNAL, "czt chirp spectrum");
+    }
+    if (st != ST_OK) {
+        vvhip_czt_destroy(h);
+        return st;
+    }
+    *out = h;
+    return ST_OK;
+}
+
+void vvhip_czt_destroy(vvhip_czt* h) {
+    if (!h) return;
+    if (h->g) (void)hipFree(h->g);
+    if (h->post) (void)hipFree(h->post);
+    if (h->B) (void)hipFree(h->B);
+    delete h;
+}
+
+int vvhip_czt_exec_device(const vvhip_czt* h, const void* d_x, int real_in, size_t batch, void* d_X,
+                          void* stream) {
+    if (!h || !d_x || !d_X) return ST_NULL;
+    return czt_run(h, d_x, real_in, batch, (float2*)d_X, (hipStream_t)stream);
+}
+
+int vvhip_czt_exec_host(const void* x, int real_in, size_t n, size_t m, float w_re, float w_im, float a_re,
+                        float a_im, void* X) {
+    if (!x || !X) return ST_NULL;
+    vvhip_czt* h = nullptr;
+    int st = vvhip_czt_create(n, m, w_re, w_im, a_re, a_im, &h);
+    if (st) return st;
+    st = host_io(x, (real_in ? 4 : 8) * n, X, 8 * m, "czt", [&](void* dx, void* dX, hipStream_t s) {
+        return czt_run(h, dx, real_in, 1, (float2*)dX, s);
+    });
+    vvhip_czt_destroy(h);
+    return st;
+}
+
+int vvhip_cepstrum_device(const float* d_x, size_t n, size_t batch, float* d_c, void* stream) {
+    if (!d_x || !d_c) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (batch == 0) return ST_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t nh = n / 2 + 1;
+    Scratch half(s);
+    HIPCHK(half.alloc(8 * nh * batch), ST_INTERNAL);
+    int st = fft_run(n, 1, 1, d_x, half.p, batch, s);
+    if (st) return st;
+    HIPCHK(launch_log_magnitude((float2*)half.p, (long long)(nh * batch), s), ST_INTERNAL);
+    return fft_run(n, 2, -1, half.p, d_c, batch, s);
+}
+
+int vvhip_icepstrum_minphase_device(const float* d_c, size_t n, size_t batch, float* d_x, void* stream) {
+    if (!d_c || !d_x) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (batch == 0) return ST_OK;
+    hipStream_t s = (hipStream_t)stream;
+    Scratch C(s);
+    HIPCHK(C.alloc(8 * n * batch), ST_INTERNAL);
+    float2* cp = (float2*)C.p;
+    HIPCHK(launch_cepstrum_fold(d_c, (long long)n, (long long)batch, cp, s), ST_INTERNAL);
+    int st = fft_run(n, 0, 1, cp, cp, batch, s);
+    if (st) return st;
+    HIPCHK(launch_exp_real(cp, (long long)(n * batch), 0, s), ST_INTERNAL);
+    if ((st = fft_run(n, 0, -1, cp, cp, batch, s))) return st;
+    HIPCHK(launch_take_real(cp, d_x, (long long)(n * batch), s), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_minphase_from_cepstrum_device(const float* d_c, size_t n, size_t batch, float* d_spec, void* stream) {
+    if (!d_c || !d_spec) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (batch == 0) return ST_OK;
+    hipStream_t s = (hipStream_t)stream;
+    float2* sp = (float2*)d_spec;
+    HIPCHK(launch_cepstrum_fold(d_c, (long long)n, (long long)batch, sp, s), ST_INTERNAL);
+    int st = fft_run(n, 0, 1, sp, sp, batch, s);
+    if (st) return st;
+    HIPCHK(launch_exp_real(sp, (long long)(n * batch), 1, s), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_cepstrum_host(const float* x, size_t n, float* c) {
+    if (!x || !c) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    return host_io(x, 4 * n, c, 4 * n, "cepstrum", [&](void* dx, void* dc, hipStream_t s) {
+        return vvhip_cepstrum_device((const float*)dx, n, 1, (float*)dc, s);
+    });
+}
+
+int vvhip_icepstrum_minphase_host(const float* c, size_t n, float* x) {
+    if (!c || !x) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    return host_io(c, 4 * n, x, 4 * n, "icepstrum", [&](void* dc, void* dx, hipStream_t s) {
+        return vvhip_icepstrum_minphase_device((const float*)dc, n, 1, (float*)dx, s);
+    });
+}
+
+int vvhip_minphase_from_cepstrum_host(const float* c, size_t n, float* spec) {
+    if (!c || !spec) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    return host_io(c, 4 * n, spec, 8 * n, "minphase", [&](void* dc, void* ds, hipStream_t s) {
+        return vvhip_minphase_from_cepstrum_device((const float*)dc, n, 1, (float*)ds, s);
+    });
+}
+
+}  // extern "C"

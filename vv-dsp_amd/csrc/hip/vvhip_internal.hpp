@@ -162,5 +162,14 @@ hipError_t launch_dct3_post(long long n, const float* v, float* x, long long bat
 hipError_t launch_dct_naive(long long n, int type, int dir, const float* in, float* out,
                             long long batch, hipStream_t s);
 hipError_t launch_nan_policy(float* p, long long count, int policy, int* flag, hipStream_t s);
+// czt_kernels.hip: chirp-z stages (czt.c:58-178) and the cepstrum family (cepstrum.c, minphase.c)
+hipError_t launch_czt_pre(const void* x, int real_in, long long n, long long p, long long rows, long long in_dist,
+                          const float2* g, float2* a, hipStream_t s);
+hipError_t launch_cmul_rows(float2* a, const float2* B, long long p, long long rows, hipStream_t s);
+hipError_t launch_czt_post(const float2* a, long long n, long long p, long long m, long long rows, const float2* post,
+                           float2* X, long long out_dist, hipStream_t s);
+hipError_t launch_log_magnitude(float2* Y, long long count, hipStream_t s);
+hipError_t launch_cepstrum_fold(const float* c, long long n, long long rows, float2* C, hipStream_t s);
+hipError_t launch_exp_real(float2* H, long long count, int dbl, hipStream_t s);
 
 }  // namespace vvh

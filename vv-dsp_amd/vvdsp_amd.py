@@ -71,6 +71,11 @@ def lib():
     L.vv_dsp_mfcc_destroy.argtypes = [_vp]
     L.vv_dsp_mfcc_process_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.vv_dsp_log_mel_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.vv_dsp_czt_plan_create.argtypes = [_sz, _sz, C.c_float, C.c_float, C.c_float, C.c_float, C.POINTER(_vp)]
+    L.vv_dsp_czt_plan_destroy.argtypes = [_vp]
+    L.vv_dsp_czt_execute_device.argtypes = [_vp, _vp, C.c_int, _sz, _vp, _vp]
+    for f in ("cepstrum_real", "icepstrum_minphase", "minphase_from_cepstrum"):
+        getattr(L, f"vv_dsp_{f}_device").argtypes = [_vp, _sz, _sz, _vp, _vp]
     L.vvhip_fir_block_size.argtypes = [_vp, _sz]
     L.vvhip_fir_block_size.restype = _sz
     _lib = L
@@ -326,3 +331,59 @@ def dct(x, dct_type=2, inverse=False, stream=None):
     finally:
         lib().vv_dsp_dct_destroy(p)
     return y if x.dim() == 2 else y[0]
+
+
+class CztPlan:
+    """Chirp-z transform of `batch` rows (vv_dsp_czt_exec_cpx / _real semantics,
+    czt.c:44-178): X[k] = sum_n x[n] A^-n W^(nk), k < m.  x: (batch, n) or (n,)
+    complex64 or float32 device tensor -> complex64 (batch, m)."""
+
+    def __init__(self, n, m, w, a=1.0 + 0j):
+        self.n, self.m = n, m
+        self.h = _vp()
+        w, a = complex(w), complex(a)
+        _check(lib().vv_dsp_czt_plan_create(n, m, w.real, w.imag, a.real, a.imag, C.byref(self.h)),
+               "czt_plan_create")
+
+    def __call__(self, x, out=None, stream=None):
+        x2 = x if x.dim() == 2 else x.unsqueeze(0)
+        b = x2.shape[0]
+        real = not x2.is_complex()
+        _expect(x2, torch.float32 if real else torch.complex64, b * self.n, "czt input")
+        if x2.shape[1] != self.n:
+            raise VvError(f"czt input: rows of {x2.shape[1]}, the plan's N is {self.n}")
+        if out is None:
+            out = torch.empty((b, self.m), dtype=torch.complex64, device=x.device)
+        _expect(out, torch.complex64, b * self.m, "czt output")
+        _check(lib().vv_dsp_czt_execute_device(self.h, _ptr(x2), 1 if real else 0, b, _ptr(out), _stream(stream)),
+               "czt_execute_device")
+        return out if x.dim() == 2 else out.view(-1)[:self.m]
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.vv_dsp_czt_plan_destroy(self.h)
+            self.h = None
+
+
+def _ceps_rows(fn, x, out_dtype, what, stream):
+    x2 = x if x.dim() == 2 else x.unsqueeze(0)
+    b, n = x2.shape
+    _expect(x2, torch.float32, b * n, what + " input")
+    y = torch.empty((b, n), dtype=out_dtype, device=x.device)
+    _check(getattr(lib(), fn)(_ptr(x2), n, b, _ptr(y), _stream(stream)), fn)
+    return y if x.dim() == 2 else y[0]
+
+
+def cepstrum(x, stream=None):
+    """real cepstrum of float32 rows (cepstrum.c:7-41): Re IFFT(log(|FFT x| + 1e-12))"""
+    return _ceps_rows("vv_dsp_cepstrum_real_device", x, torch.float32, "cepstrum", stream)
+
+
+def icepstrum_minphase(c, stream=None):
+    """minimum-phase signal from cepstrum rows (cepstrum.c:43-78)"""
+    return _ceps_rows("vv_dsp_icepstrum_minphase_device", c, torch.float32, "icepstrum_minphase", stream)
+
+
+def minphase_from_cepstrum(c, stream=None):
+    """minimum-phase spectrum (complex64, imaginary parts 0) from cepstrum rows (minphase.c:7-31)"""
+    return _ceps_rows("vv_dsp_minphase_from_cepstrum_device", c, torch.complex64, "minphase_from_cepstrum", stream)
