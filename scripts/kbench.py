@@ -373,6 +373,7 @@ CASES = {
     "olaold": with_env(lambda: case_ola(), "VVHIP_ISTFT_OLD", "1"),
     "dct1024": lambda: case_dct(1024, 131072),
     "czt1000": lambda: case_czt(1000, 1000, 16384),
+    "czt1000unf": with_env(lambda: case_czt(1000, 1000, 16384), "VVHIP_CZT_UNFUSED", "1"),
     "czt48000": lambda: case_czt(48000, 4096, 256),
     "ceps1024": lambda: case_cepstrum(1024, 65536),
     "iceps1024": lambda: case_cepstrum(1024, 65536, 1),

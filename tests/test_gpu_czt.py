@@ -189,3 +189,22 @@ def test_cepstrum_batched_device(vdev, amd):
         np.testing.assert_array_equal(xm[7].cpu().numpy(), amd.icepstrum_minphase(cc[7].cpu().numpy()))
         sp = vdev.minphase_from_cepstrum(cc)
         np.testing.assert_array_equal(sp[12].cpu().numpy(), amd.minphase_from_cepstrum(cc[12].cpu().numpy()))
+
+
+@pytest.mark.parametrize("n,m", [(8, 8), (100, 64), (257, 300), (1000, 17), (1500, 2000), (2049, 2048), (1, 1)])
+def test_czt_fused_equals_unfused(vdev, monkeypatch, n, m):
+    """P = next_pow2(N + M - 1) <= 4096 runs the one-pass kernel (k_czt_fused);
+    VVHIP_CZT_UNFUSED=1 the chain of element-wise kernels and library FFTs.  The
+    arithmetic is the same (the 1/P of the inverse folded into B is a power of
+    two), so the rows must be bit-identical, complex and real input."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(n + 3 * m)
+    plan = vdev.CztPlan(n, m, _c64(np.exp(-2j * np.pi * 0.13 / m)), _c64(np.exp(0.2j)))
+    xc = torch.complex(torch.randn(41, n, device="cuda", generator=g), torch.randn(41, n, device="cuda", generator=g))
+    for x in (xc, xc.real.contiguous()):
+        monkeypatch.setenv("VVHIP_CZT_UNFUSED", "0")
+        a = plan(x)
+        monkeypatch.setenv("VVHIP_CZT_UNFUSED", "1")
+        b = plan(x)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)

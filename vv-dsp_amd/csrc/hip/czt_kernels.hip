@@ -124,3 +124,109 @@ hipError_t launch_exp_real(float2* H, long long count, int dbl, hipStream_t s) {
 }
 
 }  // namespace vvh
+
+namespace vvh {
+
+// ------------------------------------------------------------------------
+// k_czt_fused<P>: the whole chirp-z chain for P = next_pow2(N + M - 1) <= 4096
+// in one pass per row: x * g on load, the P-point forward FFT in registers,
+// the product with B / P re-indexed in registers (after the forward Stockham
+// passes register q holds bin t + T*m, exactly the inverse transform's input
+// set, as in the FIR overlap-save kernel), the inverse FFT, and W^(k^2/2) on
+// the M outputs at positions N-1+k.  HBM traffic: the row in and the M outputs
+// (plus the L2-resident g, B, post tables) instead of ~4 x 16 P bytes.
+// Rows are walked grid-stride by a persistent grid, the next row's samples
+// prefetched into registers during the current row's transforms.
+// ------------------------------------------------------------------------
+template <int P, bool REAL>
+__global__ void __launch_bounds__(Wg<P>::value)
+k_czt_fused(const void* __restrict__ x, long long n, long long m, long long rows, const float2* __restrict__ g,
+            const float2* __restrict__ Bs, const float2* __restrict__ post, float2* __restrict__ X,
+            const float2* gpass, const float2* gtab) {
+    using G = Geo<P>;
+    constexpr int WG = Wg<P>::value, F = Wg<P>::F;
+    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
+    __shared__ float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<P>::ENTRIES];
+    stage_twiddles<P, WG>(ltab, gpass, gtab);
+    __syncthreads();
+    const TwTab<P> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    const long long stride = (long long)gridDim.x * F;
+    long long f = uni<G::T>((long long)blockIdx.x * F + slot);
+    float2 nx[G::P];
+    auto load = [&](long long row) {
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            const long long e = t + r * G::T;
+            float2 v = make_float2(0.0f, 0.0f);
+            if (e < n) {
+                if constexpr (REAL) v = make_float2(static_cast<const float*>(x)[row * n + e], 0.0f);
+                else v = static_cast<const float2*>(x)[row * n + e];
+            }
+            nx[r] = v;
+        }
+    };
+    if (f < rows) load(f);
+    for (; f < rows; f += stride) {
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            const long long e = t + r * G::T;
+            v[r] = e < n ? cmul(nx[r], g[e]) : make_float2(0.0f, 0.0f);
+        }
+        if (f + stride < rows) load(f + stride);
+        fft_regs<P, true>(v, t, my, tw);
+        float2 u[G::P];
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int mm = q / G::RL + G::NPT * (q % G::RL);   // out_pos<P>(t, q) = t + T*mm
+            u[mm] = cmul(v[q], Bs[t + G::T * mm]);
+        }
+        fft_regs<P, false>(u, t, my, tw);
+        float2* dst = X + f * m;
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const long long k = (long long)out_pos<P>(t, q) - (n - 1);
+            if (k >= 0 && k < m) dst[k] = cmul(u[q], post[k]);
+        }
+    }
+}
+
+template <int P>
+static hipError_t run_czt_fused(const void* x, int real_in, long long n, long long m, long long rows,
+                                const float2* g, const float2* Bs, const float2* post, float2* X, hipStream_t s) {
+    const float2* tab = twiddle_table(P);
+    const float2* pas = pass_twiddles(P);
+    if (!tab || !pas) return hipErrorOutOfMemory;
+    constexpr int WG = Wg<P>::value, F = Wg<P>::F;
+    static std::atomic<int> capc[2];
+    auto go = [&](auto kern, int ri) {
+        const int cap = cached_grid(capc[ri], (const void*)kern, WG, 0, 1LL << 40);
+        const long long need = (rows + F - 1) / F;
+        const int grid = (int)(need < cap ? need : cap);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(WG), 0, s, x, n, m, rows, g, Bs, post, X, pas, tab);
+    };
+    if (real_in) go(k_czt_fused<P, true>, 1);
+    else go(k_czt_fused<P, false>, 0);
+    return hipGetLastError();
+}
+
+bool czt_fused_supported(long long p) { return p >= 2 && p <= 4096 && (p & (p - 1)) == 0; }
+
+// Bs = B / P (the inverse transform's scale folded into the chirp spectrum)
+hipError_t launch_czt_fused(long long p, const void* x, int real_in, long long n, long long m, long long rows,
+                            const float2* g, const float2* Bs, const float2* post, float2* X, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+#define VVH_CZT(PP) \
+    case PP: return run_czt_fused<PP>(x, real_in, n, m, rows, g, Bs, post, X, s);
+    switch (p) {
+        VVH_CZT(2) VVH_CZT(4) VVH_CZT(8) VVH_CZT(16) VVH_CZT(32) VVH_CZT(64) VVH_CZT(128) VVH_CZT(256)
+        VVH_CZT(512) VVH_CZT(1024) VVH_CZT(2048) VVH_CZT(4096)
+        default: return hipErrorInvalidValue;
+    }
+#undef VVH_CZT
+}
+
+}  // namespace vvh

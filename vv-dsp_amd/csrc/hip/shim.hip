@@ -1298,6 +1298,7 @@ struct vvhip_czt {
     float2* g = nullptr;      // [n] A^-n W^(n^2/2)
     float2* post = nullptr;   // [m] W^(k^2/2)
     float2* B = nullptr;      // [p] FFT_p of b[i] = W^(-(i-n+1)^2/2), zero past n+m-1
+    float2* Bs = nullptr;     // [p] B / p (the fused kernel's inverse-transform scale folded in)
 };
 
 namespace {
@@ -1321,6 +1322,13 @@ float2 chirp_value(long double log_mag, long double angle) {
 
 int czt_run(const vvhip_czt* h, const void* x, int real_in, size_t batch, float2* X, hipStream_t s) {
     if (batch == 0) return ST_OK;
+    const char* eu = getenv("VVHIP_CZT_UNFUSED");   // A/B switch (tests, kbench): the multi-kernel chain
+    if (h->Bs && !(eu && *eu == '1')) {
+        HIPCHK(launch_czt_fused((long long)h->p, x, real_in, (long long)h->n, (long long)h->m, (long long)batch, h->g,
+                                h->Bs, h->post, X, s),
+               ST_INTERNAL);
+        return ST_OK;
+    }
     const size_t p = h->p, esz = real_in ? sizeof(float) : sizeof(float2);
     size_t rows = ((size_t)256 << 20) / (8 * p);   // scratch <= 256 MiB per chunk
     if (rows < 1) rows = 1;
@@ -1407,6 +1415,12 @@ int vvhip_czt_create(size_t n, size_t m, float w_re, float w_im, float a_re, flo
         st = fail(ST_INTERNAL, "czt tables");
     } else if ((st = fft_run(p, 0, 1, h->B, h->B, 1, nullptr)) == ST_OK && hipDeviceSynchronize() != hipSuccess) {
         st = fail(ST_INTERNAL, "czt chirp spectrum");
+    } else if (st == ST_OK && czt_fused_supported((long long)p)) {   // B / p for the one-pass kernel
+        if (hipMalloc(&h->Bs, 8 * p) != hipSuccess ||
+            hipMemcpy(h->Bs, h->B, 8 * p, hipMemcpyDeviceToDevice) != hipSuccess ||
+            launch_scale_cpx(h->Bs, (long long)p, 1.0f / (float)p, nullptr) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess)
+            st = fail(ST_INTERNAL, "czt scaled chirp spectrum");
     }
     if (st != ST_OK) {
         vvhip_czt_destroy(h);
@@ -1421,6 +1435,7 @@ void vvhip_czt_destroy(vvhip_czt* h) {
     if (h->g) (void)hipFree(h->g);
     if (h->post) (void)hipFree(h->post);
     if (h->B) (void)hipFree(h->B);
+    if (h->Bs) (void)hipFree(h->Bs);
     delete h;
 }
 

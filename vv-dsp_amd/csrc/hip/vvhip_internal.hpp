@@ -171,5 +171,9 @@ hipError_t launch_czt_post(const float2* a, long long n, long long p, long long 
 hipError_t launch_log_magnitude(float2* Y, long long count, hipStream_t s);
 hipError_t launch_cepstrum_fold(const float* c, long long n, long long rows, float2* C, hipStream_t s);
 hipError_t launch_exp_real(float2* H, long long count, int dbl, hipStream_t s);
+// the whole chirp-z chain in one kernel for P <= 4096 (Bs = FFT_P(b) / P)
+bool czt_fused_supported(long long p);
+hipError_t launch_czt_fused(long long p, const void* x, int real_in, long long n, long long m, long long rows,
+                            const float2* g, const float2* Bs, const float2* post, float2* X, hipStream_t s);
 
 }  // namespace vvh
