@@ -377,6 +377,8 @@ CASES = {
     "czt48000": lambda: case_czt(48000, 4096, 256),
     "ceps1024": lambda: case_cepstrum(1024, 65536),
     "iceps1024": lambda: case_cepstrum(1024, 65536, 1),
+    "ceps1024unf": with_env(lambda: case_cepstrum(1024, 65536), "VVHIP_CEPS_UNFUSED", "1"),
+    "iceps1024unf": with_env(lambda: case_cepstrum(1024, 65536, 1), "VVHIP_CEPS_UNFUSED", "1"),
 }
 # A/B switches for launcher experiments: CASES["stftX"] = with_env(CASES["stft"], "VVHIP_EXP_...", "1")
 

@@ -208,3 +208,23 @@ def test_czt_fused_equals_unfused(vdev, monkeypatch, n, m):
         b = plan(x)
         torch.cuda.synchronize()
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [2, 16, 256, 1024, 4096])
+def test_cepstrum_fused_vs_chain(vdev, monkeypatch, n):
+    """Power-of-two n <= 4096 runs the one-pass kernels (k_ceps_fused);
+    VVHIP_CEPS_UNFUSED=1 the element-wise chains around the library FFTs (the
+    chain's cepstrum goes through R2C/C2R instead of the reference's C2C pair).
+    Both are f32 computations of the same definitions: normwise within 2e-6 (the
+    one-pass kernel is compiled separately, so its FMA contractions may differ)."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randn(23, n, device="cuda", generator=g)
+    c = (0.1 * torch.randn(23, n, device="cuda", generator=g)).contiguous()
+    monkeypatch.setenv("VVHIP_CEPS_UNFUSED", "0")
+    a = (vdev.cepstrum(x), vdev.icepstrum_minphase(c), vdev.minphase_from_cepstrum(c))
+    monkeypatch.setenv("VVHIP_CEPS_UNFUSED", "1")
+    b = (vdev.cepstrum(x), vdev.icepstrum_minphase(c), vdev.minphase_from_cepstrum(c))
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert _normwise(u.cpu().numpy(), v.cpu().numpy()) <= 2e-6

@@ -230,3 +230,108 @@ hipError_t launch_czt_fused(long long p, const void* x, int real_in, long long n
 }
 
 }  // namespace vvh
+
+namespace vvh {
+
+// ------------------------------------------------------------------------
+// k_ceps_fused<N, KIND>: one row of the cepstrum family per N-point complex
+// transform pair, N <= 4096, the row read once and written once:
+//   KIND 0  cepstrum       x -> FFT(x + 0i) -> (log(|X| + 1e-12), 0) -> IFFT -> Re
+//   KIND 1  icepstrum      c -> fold -> FFT -> (expf(Re H), 0)        -> IFFT -> Re
+//   KIND 2  minphase spec  c -> fold -> FFT -> ((float)exp((double)Re H), 0)   (no inverse)
+// (cepstrum.c:7-78, minphase.c:7-31, the reference's own C2C formulation).
+// The element-wise step is done in the forward transform's output layout, which
+// is the inverse transform's input layout after the register re-index (as in
+// the FIR and CZT kernels); the 1/N of the inverse is applied at the store.
+// ------------------------------------------------------------------------
+template <int N, int KIND>
+__global__ void __launch_bounds__(Wg<N>::value)
+k_ceps_fused(const float* __restrict__ x, long long rows, float* __restrict__ y, const float2* gpass,
+             const float2* gtab) {
+    using G = Geo<N>;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    constexpr int LDSN = G::NPASS > 1 ? F * G::LDS : 1;
+    __shared__ float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    const long long stride = (long long)gridDim.x * F;
+    long long f = uni<G::T>((long long)blockIdx.x * F + slot);
+    float nx[G::P];
+    auto load = [&](long long row) {
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) nx[r] = x[row * N + t + r * G::T];
+    };
+    if (f < rows) load(f);
+    for (; f < rows; f += stride) {
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            float a = nx[r];
+            if constexpr (KIND != 0) {   // causal fold: c0, 2 c[i] for 1 <= i < N/2, 0 beyond
+                const int e = t + r * G::T;
+                a = e == 0 ? a : (e < N / 2 ? 2.0f * a : 0.0f);
+            }
+            v[r] = make_float2(a, 0.0f);
+        }
+        if (f + stride < rows) load(f + stride);
+        fft_regs<N, true>(v, t, my, tw);
+        if constexpr (KIND == 2) {
+            float2* dst = reinterpret_cast<float2*>(y) + f * N;
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) dst[out_pos<N>(t, q)] = make_float2((float)exp((double)v[q].x), 0.0f);
+        } else {
+            float2 u[G::P];
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                const int mm = q / G::RL + G::NPT * (q % G::RL);   // out_pos<N>(t, q) = t + T*mm
+                const float2 z = v[q];
+                const float e = KIND == 0 ? logf(sqrtf(z.x * z.x + z.y * z.y) + 1e-12f) : expf(z.x);
+                u[mm] = make_float2(e, 0.0f);
+            }
+            fft_regs<N, false>(u, t, my, tw);
+            float* dst = y + f * N;
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) dst[out_pos<N>(t, q)] = u[q].x * (1.0f / (float)N);
+        }
+    }
+}
+
+bool ceps_fused_supported(long long n) { return n >= 2 && n <= 4096 && (n & (n - 1)) == 0; }
+
+template <int N>
+static hipError_t run_ceps_fused(int kind, const float* x, long long rows, float* y, hipStream_t s) {
+    const float2* tab = twiddle_table(N);
+    const float2* pas = pass_twiddles(N);
+    if (!tab || !pas) return hipErrorOutOfMemory;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    static std::atomic<int> capc[3];
+    auto go = [&](auto kern, int k) {
+        const int cap = cached_grid(capc[k], (const void*)kern, WG, 0, 1LL << 40);
+        const long long need = (rows + F - 1) / F;
+        const int grid = (int)(need < cap ? need : cap);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(WG), 0, s, x, rows, y, pas, tab);
+    };
+    if (kind == 0) go(k_ceps_fused<N, 0>, 0);
+    else if (kind == 1) go(k_ceps_fused<N, 1>, 1);
+    else go(k_ceps_fused<N, 2>, 2);
+    return hipGetLastError();
+}
+
+// kind 0 cepstrum, 1 icepstrum_minphase, 2 minphase_from_cepstrum (y complex[rows][n])
+hipError_t launch_ceps_fused(int kind, long long n, const float* x, long long rows, float* y, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+#define VVH_CEPS(NN) \
+    case NN: return run_ceps_fused<NN>(kind, x, rows, y, s);
+    switch (n) {
+        VVH_CEPS(2) VVH_CEPS(4) VVH_CEPS(8) VVH_CEPS(16) VVH_CEPS(32) VVH_CEPS(64) VVH_CEPS(128) VVH_CEPS(256)
+        VVH_CEPS(512) VVH_CEPS(1024) VVH_CEPS(2048) VVH_CEPS(4096)
+        default: return hipErrorInvalidValue;
+    }
+#undef VVH_CEPS
+}
+
+}  // namespace vvh

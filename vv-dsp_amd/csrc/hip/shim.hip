@@ -1458,11 +1458,21 @@ int vvhip_czt_exec_host(const void* x, int real_in, size_t n, size_t m, float w_
     return st;
 }
 
+// one-pass kernels for pow2 n <= 4096; VVHIP_CEPS_UNFUSED=1 selects the chains (A/B, tests)
+static bool ceps_fused(size_t n) {
+    const char* e = getenv("VVHIP_CEPS_UNFUSED");
+    return ceps_fused_supported((long long)n) && !(e && *e == '1');
+}
+
 int vvhip_cepstrum_device(const float* d_x, size_t n, size_t batch, float* d_c, void* stream) {
     if (!d_x || !d_c) return ST_NULL;
     if (n == 0) return ST_SIZE;
     if (batch == 0) return ST_OK;
     hipStream_t s = (hipStream_t)stream;
+    if (ceps_fused(n)) {
+        HIPCHK(launch_ceps_fused(0, (long long)n, d_x, (long long)batch, d_c, s), ST_INTERNAL);
+        return ST_OK;
+    }
     const size_t nh = n / 2 + 1;
     Scratch half(s);
     HIPCHK(half.alloc(8 * nh * batch), ST_INTERNAL);
@@ -1477,6 +1487,10 @@ int vvhip_icepstrum_minphase_device(const float* d_c, size_t n, size_t batch, fl
     if (n == 0) return ST_SIZE;
     if (batch == 0) return ST_OK;
     hipStream_t s = (hipStream_t)stream;
+    if (ceps_fused(n)) {
+        HIPCHK(launch_ceps_fused(1, (long long)n, d_c, (long long)batch, d_x, s), ST_INTERNAL);
+        return ST_OK;
+    }
     Scratch C(s);
     HIPCHK(C.alloc(8 * n * batch), ST_INTERNAL);
     float2* cp = (float2*)C.p;
@@ -1494,6 +1508,10 @@ int vvhip_minphase_from_cepstrum_device(const float* d_c, size_t n, size_t batch
     if (n == 0) return ST_SIZE;
     if (batch == 0) return ST_OK;
     hipStream_t s = (hipStream_t)stream;
+    if (ceps_fused(n)) {
+        HIPCHK(launch_ceps_fused(2, (long long)n, d_c, (long long)batch, d_spec, s), ST_INTERNAL);
+        return ST_OK;
+    }
     float2* sp = (float2*)d_spec;
     HIPCHK(launch_cepstrum_fold(d_c, (long long)n, (long long)batch, sp, s), ST_INTERNAL);
     int st = fft_run(n, 0, 1, sp, sp, batch, s);

@@ -173,6 +173,10 @@ hipError_t launch_cepstrum_fold(const float* c, long long n, long long rows, flo
 hipError_t launch_exp_real(float2* H, long long count, int dbl, hipStream_t s);
 // the whole chirp-z chain in one kernel for P <= 4096 (Bs = FFT_P(b) / P)
 bool czt_fused_supported(long long p);
+// the cepstrum family in one pass per row for pow2 n <= 4096 (kind 0 cepstrum,
+// 1 icepstrum_minphase, 2 minphase_from_cepstrum with complex output rows)
+bool ceps_fused_supported(long long n);
+hipError_t launch_ceps_fused(int kind, long long n, const float* x, long long rows, float* y, hipStream_t s);
 hipError_t launch_czt_fused(long long p, const void* x, int real_in, long long n, long long m, long long rows,
                             const float2* g, const float2* Bs, const float2* post, float2* X, hipStream_t s);
 
