@@ -129,6 +129,15 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_icepstrum_minphase_device(const vv_dsp_rea
                                                                 vv_dsp_real* d_x, void* stream);
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_minphase_from_cepstrum_device(const vv_dsp_real* d_c, size_t n, size_t batch,
                                                                     vv_dsp_cpx* d_spec, void* stream);
+/* Spectral utilities on `batch` contiguous rows of n (utils.c:5-73): fftshift
+ * (inverse 0) / ifftshift (inverse 1) of float or complex rows (in place
+ * allowed); phase wrap of `count` floats; phase unwrap of each row. */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_fftshift_device(const void* d_in, void* d_out, size_t n, size_t batch,
+                                                      int is_complex, int inverse, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_phase_wrap_device(const vv_dsp_real* d_in, vv_dsp_real* d_out, size_t count,
+                                                        void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_phase_unwrap_device(const vv_dsp_real* d_in, vv_dsp_real* d_out, size_t n,
+                                                          size_t batch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,7 @@
  *   vvhip_hilbert_*: src/spectral/hilbert.c:14-75
  *   vvhip_dct_*  : src/spectral/dct.c:86-136
  *   vvhip_czt_*  : src/spectral/czt.c:44-178 (exec_cpx, exec_real)
+ *   vvhip_fftshift_* / _phase_wrap_* / _phase_unwrap_*: src/spectral/utils.c:5-73
  *   vvhip_cepstrum_* / _icepstrum_minphase_* / _minphase_from_cepstrum_*:
  *                  src/envelope/cepstrum.c:7-78, src/envelope/minphase.c:7-31
  */
@@ -174,6 +175,18 @@ int vvhip_minphase_from_cepstrum_device(const float* d_c, size_t n, size_t batch
 int vvhip_cepstrum_host(const float* x, size_t n, float* c);
 int vvhip_icepstrum_minphase_host(const float* c, size_t n, float* x);
 int vvhip_minphase_from_cepstrum_host(const float* c, size_t n, float* spec);
+
+/* ---- Spectral utilities (src/spectral/utils.c:5-73) ----
+ * `batch` contiguous rows of n: fftshift (inverse 0) / ifftshift (inverse 1) of
+ * float (cpx 0) or complex (cpx 1) rows, a permutation (in place allowed);
+ * phase wrap of `count` floats into (-pi, pi]; phase unwrap of each row. */
+int vvhip_fftshift_device(const void* d_in, void* d_out, size_t n, size_t batch, int cpx, int inverse,
+                          void* stream);
+int vvhip_phase_wrap_device(const float* d_in, float* d_out, size_t count, void* stream);
+int vvhip_phase_unwrap_device(const float* d_in, float* d_out, size_t n, size_t batch, void* stream);
+int vvhip_fftshift_host(const void* in, void* out, size_t n, int cpx, int inverse);
+int vvhip_phase_wrap_host(const float* in, float* out, size_t n);
+int vvhip_phase_unwrap_host(const float* in, float* out, size_t n);
 
 /* ---- DCT (dct.c:86-136); nan_policy as core/nan_policy.h (0..3) ---- */
 int vvhip_dct_host(const float* in, float* out, size_t n, int type, int dir, int nan_policy);

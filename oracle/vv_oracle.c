@@ -711,3 +711,41 @@ int orc_minphase_from_cepstrum(const float* c, size_t n, float* spec) {
     free(t);
     return 0;
 }
+
+/* ---- spectral utilities (src/spectral/utils.c) ------------------------- */
+/* :5-49 -- k = n/2; fftshift out = in[k..n) ++ in[0..k), ifftshift out = in[n-k..n) ++ in[0..n-k) */
+int orc_fftshift(const float* in, float* out, size_t n, int cpx, int inverse) {
+    if (!in || !out) return 1;
+    if (n == 0) return 2;
+    const size_t k = n / 2, w = cpx ? 2 : 1;
+    const size_t first = inverse ? n - k : k;   /* index of in[] that lands at out[0] */
+    memcpy(out, in + w * first, sizeof(float) * w * (n - first));
+    memcpy(out + w * (n - first), in, sizeof(float) * w * first);
+    return 0;
+}
+
+/* :51-61 */
+int orc_phase_wrap(const float* in, float* out, size_t n) {
+    if (!in || !out) return 1;
+    for (size_t i = 0; i < n; ++i) {
+        float x = in[i];
+        while (x <= -kPi) x += kTwoPi;
+        while (x > kPi) x -= kTwoPi;
+        out[i] = x;
+    }
+    return 0;
+}
+
+/* :63-73 -- float accumulation left to right */
+int orc_phase_unwrap(const float* in, float* out, size_t n) {
+    if (!in || !out) return 1;
+    if (n == 0) return 2;
+    out[0] = in[0];
+    for (size_t i = 1; i < n; ++i) {
+        float delta = in[i] - in[i - 1];
+        if (delta > kPi) delta -= kTwoPi;
+        else if (delta < -kPi) delta += kTwoPi;
+        out[i] = out[i - 1] + delta;
+    }
+    return 0;
+}

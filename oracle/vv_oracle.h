@@ -85,6 +85,11 @@ int orc_cepstrum_real(const float* x, size_t n, float* c);               /* ceps
 int orc_icepstrum_minphase(const float* c, size_t n, float* x);          /* cepstrum.c:43-78 */
 int orc_minphase_from_cepstrum(const float* c, size_t n, float* spec);   /* minphase.c:7-31 */
 
+/* ---- spectral utilities (src/spectral/utils.c) ---- cpx: complex rows of n */
+int orc_fftshift(const float* in, float* out, size_t n, int cpx, int inverse);  /* :5-49 */
+int orc_phase_wrap(const float* in, float* out, size_t n);                   /* :51-61 */
+int orc_phase_unwrap(const float* in, float* out, size_t n);                 /* :63-73 */
+
 #ifdef __cplusplus
 }
 #endif

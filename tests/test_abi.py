@@ -107,6 +107,13 @@ def test_argument_validation_matches_reference(cpu_lib, ref):
             assert fn(None, 4, hp) == ERR_NULL
             assert fn(hp, 4, None) == ERR_NULL
             assert fn(hp, 0, hp) == ERR_INTERNAL
+        # utils.c:5-73: shifts and unwrap reject n = 0, wrap accepts it
+        z0 = np.zeros(0, np.float32)
+        for f in ("fftshift", "ifftshift", "phase_unwrap"):
+            assert lib._util(f, z0)[0] == ERR_SIZE
+        assert lib._util("phase_wrap", z0)[0] == OK
+        for f in (L.vv_dsp_fftshift_real, L.vv_dsp_ifftshift_cpx, L.vv_dsp_phase_wrap, L.vv_dsp_phase_unwrap):
+            assert f(None, hp, 4) == ERR_NULL
 
 
 def test_fir_design_bitexact_host_setup(cpu_lib, orc):
@@ -190,6 +197,9 @@ def test_no_gpu_fails_loudly(cpu_lib):
     assert L.vv_dsp_cepstrum_real(fp(x), 64, fp(x)) == ERR_UNSUPPORTED
     assert L.vv_dsp_icepstrum_minphase(fp(x), 64, fp(x)) == ERR_UNSUPPORTED
     assert L.vv_dsp_minphase_from_cepstrum(fp(x), 64, fp(z)) == ERR_UNSUPPORTED
+    for f in ("fftshift", "ifftshift", "phase_wrap", "phase_unwrap"):
+        assert cpu_lib._util(f, x)[0] == ERR_UNSUPPORTED
+    assert L.vv_dsp_spectral_dummy() == 42
     assert b"no HIP device" in L.vvhip_last_error()
 
 

@@ -224,3 +224,30 @@ def test_reference_envelope_known_answers(ref):
     assert abs(c[0]) < 1e-3 and np.all(np.abs(c[1:]) < 1e-2)
     assert abs(ref.icepstrum_minphase(c)[0] - 1.0) < 1e-2
     assert np.all(np.isfinite(ref.minphase_from_cepstrum(c).view(np.float32)))
+
+
+def test_oracle_spectral_utils_bitexact_vs_reference(orc, ref):
+    """utils.c:5-73 restated: shifts (real and complex, even and odd n), phase wrap
+    and unwrap (float accumulation) bit-identical; spectral_tests.c:71-81's
+    fftshift/ifftshift round trip; n = 0 codes.  For odd n the reference rotates
+    by n/2 rounded down in the fftshift direction (utils.c:8-12), i.e. NumPy's
+    ifftshift: kept as the reference has it."""
+    rng = np.random.default_rng(41)
+    for n in (1, 2, 5, 8, 9, 1024, 1001):
+        x = rng.standard_normal(n).astype(np.float32)
+        z = (x + 1j * rng.standard_normal(n)).astype(np.complex64)
+        for f in ("fftshift", "ifftshift"):
+            assert np.array_equal(getattr(orc, f)(x), getattr(ref, f)(x)), (f, n)
+            assert np.array_equal(getattr(orc, f)(z), getattr(ref, f)(z)), (f, n)
+            if n % 2 == 0:   # odd n: the reference's fftshift is NumPy's ifftshift and vice versa
+                assert np.array_equal(getattr(orc, f)(x), getattr(np.fft, f)(x)), (f, n)
+        ph = (rng.standard_normal(n) * 20).astype(np.float32)
+        assert np.array_equal(orc.phase_wrap(ph), ref.phase_wrap(ph)), n
+        steps = np.cumsum(rng.uniform(-3, 3, n)).astype(np.float32)
+        w = ref.phase_wrap(steps)
+        assert np.array_equal(orc.phase_unwrap(w), ref.phase_unwrap(w)), n
+    a = np.arange(5, dtype=np.float32)
+    assert np.array_equal(ref.ifftshift(ref.fftshift(a)), a)
+    assert ref._util("fftshift", np.zeros(0, np.float32))[0] == 2
+    assert ref._util("phase_unwrap", np.zeros(0, np.float32))[0] == 2
+    assert ref._util("phase_wrap", np.zeros(0, np.float32))[0] == 0

@@ -126,6 +126,42 @@ class _CztMixin:
         """vv_dsp_minphase_from_cepstrum (minphase.c:7-31) -> complex64[n]"""
         return self._ceps_call(5, c, 2 * len(c)).view(np.complex64)
 
+    # ---- spectral utilities (src/spectral/utils.c:5-73) ------------------
+    def _util(self, name, x, out_like=None):
+        """-> (status, out) of one utils.c call; x float32 or complex64 (the shifts)"""
+        L = self.lib
+        cpx = np.iscomplexobj(x)
+        xf = _cplx_view(x) if cpx else np.ascontiguousarray(x, np.float32)
+        out = np.zeros_like(xf)
+        n = len(x)
+        if self._prefix == "orc_":
+            if name in ("fftshift", "ifftshift"):
+                f = L.orc_fftshift
+                f.argtypes = [_f32p, _f32p, C.c_size_t, C.c_int, C.c_int]
+                st = f(_fp(xf) if n else None, _fp(out) if n else None, n, int(cpx), int(name == "ifftshift"))
+            else:
+                f = getattr(L, "orc_" + name)
+                f.argtypes = [_f32p, _f32p, C.c_size_t]
+                st = f(_fp(xf), _fp(out), n)
+        else:
+            sym = {"fftshift": "vv_dsp_fftshift_", "ifftshift": "vv_dsp_ifftshift_"}.get(name)
+            f = getattr(L, sym + ("cpx" if cpx else "real")) if sym else getattr(L, "vv_dsp_" + name)
+            f.argtypes = [_f32p, _f32p, C.c_size_t]
+            st = f(_fp(xf), _fp(out), n)
+        return st, (out.view(np.complex64) if cpx else out)
+
+    def fftshift(self, x):
+        return self._util("fftshift", x)[1]
+
+    def ifftshift(self, x):
+        return self._util("ifftshift", x)[1]
+
+    def phase_wrap(self, x):
+        return self._util("phase_wrap", x)[1]
+
+    def phase_unwrap(self, x):
+        return self._util("phase_unwrap", x)[1]
+
 
 
 class VvDsp(_CztMixin):

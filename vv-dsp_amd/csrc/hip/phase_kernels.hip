@@ -29,6 +29,21 @@ __device__ __forceinline__ double phase_inc(const float2* z, long long i) {
     return atan2(im, re);
 }
 
+// vv_dsp_phase_unwrap (src/spectral/utils.c:63-73): out[0] = in[0], then the
+// float difference of neighbours wrapped once by +-2 pi (float VV_DSP_PI /
+// VV_DSP_TWO_PI), accumulated.  The increments are the reference's float
+// values exactly; their sum runs in f64 (the reference sums in float left to
+// right, so the two differ by that loop's own rounding, ~sqrt(n) ulp).
+__device__ __forceinline__ double phase_inc(const float* p, long long i) {
+    if (i == 0) return (double)p[0];
+    const float kPi = (float)3.141592653589793238462643383279502884;
+    const float kTwoPi = (float)(2.0 * 3.141592653589793238462643383279502884);
+    float d = p[i] - p[i - 1];
+    if (d > kPi) d -= kTwoPi;
+    else if (d < -kPi) d += kTwoPi;
+    return (double)d;
+}
+
 // block-inclusive scan of per-thread totals (256 doubles) in LDS; returns this
 // thread's exclusive offset, *total the block's sum
 __device__ __forceinline__ double block_excl_scan(double v, double* sh, double* total) {
@@ -48,10 +63,11 @@ __device__ __forceinline__ double block_excl_scan(double v, double* sh, double* 
 }
 
 // pass 1: block totals, part[row][blk]
-__global__ void __launch_bounds__(PH_T) k_phase_part(const float2* z, long long n, long long nblk, double* part) {
+template <class In>
+__global__ void __launch_bounds__(PH_T) k_phase_part(const In* z, long long n, long long nblk, double* part) {
     __shared__ double sh[PH_T];
     const long long row = blockIdx.y, blk = blockIdx.x;
-    const float2* zr = z + row * n;
+    const In* zr = z + row * n;
     const long long i0 = blk * PH_CHUNK + (long long)threadIdx.x * PH_PER;
     double s = 0.0;
 #pragma unroll 4
@@ -63,11 +79,12 @@ __global__ void __launch_bounds__(PH_T) k_phase_part(const float2* z, long long 
 }
 
 // pass 2: outputs = offset of the preceding blocks + block-exclusive + thread-serial sums
-__global__ void __launch_bounds__(PH_T) k_phase_out(const float2* z, long long n, long long nblk, const double* part,
+template <class In>
+__global__ void __launch_bounds__(PH_T) k_phase_out(const In* z, long long n, long long nblk, const double* part,
                                                     float* phase) {
     __shared__ double sh[PH_T];
     const long long row = blockIdx.y, blk = blockIdx.x;
-    const float2* zr = z + row * n;
+    const In* zr = z + row * n;
     // offset: sum of the preceding blocks' totals, in block order
     double off = 0.0;
     {
@@ -108,7 +125,8 @@ __global__ void k_inst_freq(const float* p, long long n, long long total, double
     }
 }
 
-hipError_t launch_inst_phase(const float2* z, long long n, long long batch, float* phase, hipStream_t s) {
+template <class In>
+static hipError_t phase_scan(const In* z, long long n, long long batch, float* phase, hipStream_t s) {
     if (n <= 0 || batch <= 0) return hipSuccess;
     const long long nblk = (n + PH_CHUNK - 1) / PH_CHUNK;
     if (nblk > 0x7fffffffLL || batch > 65535) return hipErrorInvalidValue;
@@ -116,11 +134,19 @@ hipError_t launch_inst_phase(const float2* z, long long n, long long batch, floa
     hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * (size_t)(nblk * batch), s);
     if (e != hipSuccess) return e;
     const dim3 grid((unsigned)nblk, (unsigned)batch);
-    hipLaunchKernelGGL(k_phase_part, grid, dim3(PH_T), 0, s, z, n, nblk, part);
-    hipLaunchKernelGGL(k_phase_out, grid, dim3(PH_T), 0, s, z, n, nblk, part, phase);
+    hipLaunchKernelGGL((k_phase_part<In>), grid, dim3(PH_T), 0, s, z, n, nblk, part);
+    hipLaunchKernelGGL((k_phase_out<In>), grid, dim3(PH_T), 0, s, z, n, nblk, part, phase);
     e = hipGetLastError();
     (void)hipFreeAsync(part, s);
     return e;
+}
+
+hipError_t launch_inst_phase(const float2* z, long long n, long long batch, float* phase, hipStream_t s) {
+    return phase_scan(z, n, batch, phase, s);
+}
+
+hipError_t launch_phase_unwrap(const float* p, long long n, long long batch, float* out, hipStream_t s) {
+    return phase_scan(p, n, batch, out, s);
 }
 
 hipError_t launch_inst_freq(const float* phase, long long n, long long batch, double scale, float* freq,

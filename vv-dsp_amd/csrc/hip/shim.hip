@@ -1545,3 +1545,76 @@ int vvhip_minphase_from_cepstrum_host(const float* c, size_t n, float* spec) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Spectral utilities (src/spectral/utils.c:5-73): fftshift / ifftshift,
+// phase wrap and unwrap on `batch` contiguous rows of n.
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int vvhip_fftshift_device(const void* d_in, void* d_out, size_t n, size_t batch, int cpx, int inverse,
+                          void* stream) {
+    if (!d_in || !d_out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t bytes = (cpx ? 8 : 4) * n * batch;
+    const void* src = d_in;
+    Scratch tmp(s);
+    if (d_in == d_out && batch) {   // a permutation in place: read from a copy
+        HIPCHK(tmp.alloc(bytes), ST_INTERNAL);
+        HIPCHK(hipMemcpyAsync(tmp.p, d_in, bytes, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+        src = tmp.p;
+    }
+    HIPCHK(launch_fftshift(src, d_out, (long long)n, (long long)batch, cpx, inverse, s), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_phase_wrap_device(const float* d_in, float* d_out, size_t count, void* stream) {
+    if (!d_in || !d_out) return ST_NULL;
+    HIPCHK(launch_phase_wrap(d_in, d_out, (long long)count, (hipStream_t)stream), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_phase_unwrap_device(const float* d_in, float* d_out, size_t n, size_t batch, void* stream) {
+    if (!d_in || !d_out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (batch == 0) return ST_OK;
+    if (batch > 65535) return fail(ST_RANGE, "phase unwrap: more than 65535 rows per call");
+    hipStream_t s = (hipStream_t)stream;
+    const float* src = d_in;
+    Scratch tmp(s);
+    if (d_in == d_out) {   // the scan reads neighbours: read from a copy
+        HIPCHK(tmp.alloc(4 * n * batch), ST_INTERNAL);
+        HIPCHK(hipMemcpyAsync(tmp.p, d_in, 4 * n * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+        src = (const float*)tmp.p;
+    }
+    HIPCHK(launch_phase_unwrap(src, (long long)n, (long long)batch, d_out, s), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_fftshift_host(const void* in, void* out, size_t n, int cpx, int inverse) {
+    if (!in || !out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    const size_t bytes = (cpx ? 8 : 4) * n;
+    return host_io(in, bytes, out, bytes, "fftshift", [&](void* di, void* dout, hipStream_t s) {
+        return vvhip_fftshift_device(di, dout, n, 1, cpx, inverse, s);
+    });
+}
+
+int vvhip_phase_wrap_host(const float* in, float* out, size_t n) {
+    if (!in || !out) return ST_NULL;
+    if (n == 0) return ST_OK;   // utils.c:51-61 loops zero times
+    return host_io(in, 4 * n, out, 4 * n, "phase wrap", [&](void* di, void* dout, hipStream_t s) {
+        return vvhip_phase_wrap_device((const float*)di, (float*)dout, n, s);
+    });
+}
+
+int vvhip_phase_unwrap_host(const float* in, float* out, size_t n) {
+    if (!in || !out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    return host_io(in, 4 * n, out, 4 * n, "phase unwrap", [&](void* di, void* dout, hipStream_t s) {
+        return vvhip_phase_unwrap_device((const float*)di, (float*)dout, n, 1, s);
+    });
+}
+
+}  // extern "C"

@@ -146,6 +146,11 @@ bool hilbert_fused_supported(long long n);
 hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long long batch, hipStream_t s);
 // instantaneous phase / frequency rows (phase_kernels.hip, hilbert.c:77-113)
 hipError_t launch_inst_phase(const float2* z, long long n, long long batch, float* phase, hipStream_t s);
+hipError_t launch_phase_unwrap(const float* p, long long n, long long batch, float* out, hipStream_t s);
+// spectral_utils_kernels.hip (src/spectral/utils.c)
+hipError_t launch_fftshift(const void* in, void* out, long long n, long long batch, int cpx, int inverse,
+                           hipStream_t s);
+hipError_t launch_phase_wrap(const float* in, float* out, long long count, hipStream_t s);
 hipError_t launch_inst_freq(const float* phase, long long n, long long batch, double scale, float* freq,
                             hipStream_t s);
 bool dct2_fused_supported(long long n);
