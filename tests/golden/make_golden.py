@@ -113,6 +113,38 @@ def main():
          fb=fb, power=power, log_mel_kiss=lm, mfcc_kiss=ref.mfcc(lm, 13, 22.0),
          log_mel_np64=np.log(power.astype(np.float64) @ fb.astype(np.float64).T + 1e-10))
 
+    # 8. CZT (python/test_czt.py cases) and the cepstrum family (envelope_tests.c style)
+    from scipy.signal import czt as sp_czt
+
+    def eff(z):   # W / A as the transform sees them: float pair, |z| rounded to float (czt.c:81-82)
+        z = complex(np.complex64(z))
+        return float(np.float32(abs(z))) * np.exp(1j * np.angle(z))
+
+    rng = np.random.default_rng(0)
+    x = (rng.standard_normal(32) + 1j * rng.standard_normal(32)).astype(np.complex64)
+    w = np.array([np.exp(-2j * np.pi / 32)], np.complex64)
+    save("czt_testpy_n32", man, "python/test_czt.py: 32 complex N(0,1) seed 0, M = 32, DFT parameters",
+         x=x, w=w, kiss=ref.czt(x, 32, complex(w[0]), 1.0 + 0j),
+         np64=sp_czt(x.astype(np.complex128), m=32, w=eff(w[0]), a=1.0))
+    st, W, A = ref.czt_params(800.0, 1200.0, 64, 48000.0)
+    assert st == 0
+    xr = np.cos(2 * np.pi * 1000.0 * np.arange(32) / 48000.0).astype(np.float32)
+    save("czt_zoom_n32_m64", man, "python/test_czt.py zoom: 1 kHz tone, 32 samples @ 48 kHz, 800-1200 Hz, M = 64 "
+         "(W, A from vv_dsp_czt_params_for_freq_range)",
+         x=xr, w=np.array([W], np.complex64), a=np.array([A], np.complex64), kiss=ref.czt(xr, 64, W, A),
+         np64=sp_czt(xr.astype(np.float64), m=64, w=eff(W), a=eff(A)))
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal(64).astype(np.float32)
+    c = (0.05 * rng.standard_normal(64)).astype(np.float32)
+    X = np.fft.fft(x.astype(np.float64))
+    C = np.zeros(64)
+    C[0], C[1:32] = c[0], 2 * c[1:32].astype(np.float64)
+    H = np.exp(np.real(np.fft.fft(C)))
+    save("cepstrum_n64", man, "cepstrum of 64 N(0,1) seed 8; minimum phase of a 0.05 N(0,1) cepstrum",
+         x=x, ceps_kiss=ref.cepstrum(x), ceps_np64=np.real(np.fft.ifft(np.log(np.abs(X) + 1e-12))),
+         c=c, iceps_kiss=ref.icepstrum_minphase(c), iceps_np64=np.real(np.fft.ifft(H)),
+         minph_kiss=ref.minphase_from_cepstrum(c), minph_np64=H)
+
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
     print("wrote", len(man), "golden sets")

@@ -228,3 +228,21 @@ def test_cepstrum_fused_vs_chain(vdev, monkeypatch, n):
     torch.cuda.synchronize()
     for u, v in zip(a, b):
         assert _normwise(u.cpu().numpy(), v.cpu().numpy()) <= 2e-6
+
+
+def test_czt_cepstrum_golden(amd, golden):
+    """The committed fixtures through the C API: CZT at the reference harness
+    tolerance (rtol = atol = 2e-4) of both the f64 result and the reference's own
+    output; the cepstrum family within 1e-5 of f64 (normwise)."""
+    g = golden("czt_testpy_n32")
+    y = amd.czt(g["x"], 32, complex(g["w"][0]), 1.0 + 0j)
+    np.testing.assert_allclose(y, g["np64"], rtol=2e-4, atol=2e-4)
+    np.testing.assert_allclose(y, g["kiss"], rtol=2e-4, atol=2e-4)
+    g = golden("czt_zoom_n32_m64")
+    y = amd.czt(g["x"], 64, complex(g["w"][0]), complex(g["a"][0]))
+    np.testing.assert_allclose(y, g["np64"], rtol=2e-4, atol=2e-4)
+    np.testing.assert_allclose(y, g["kiss"], rtol=2e-4, atol=2e-4)
+    g = golden("cepstrum_n64")
+    assert _normwise(amd.cepstrum(g["x"]), g["ceps_np64"]) <= 1e-5
+    assert _normwise(amd.icepstrum_minphase(g["c"]), g["iceps_np64"]) <= 1e-5
+    assert _normwise(amd.minphase_from_cepstrum(g["c"]), g["minph_np64"]) <= 1e-5

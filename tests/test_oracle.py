@@ -251,3 +251,24 @@ def test_oracle_spectral_utils_bitexact_vs_reference(orc, ref):
     assert ref._util("fftshift", np.zeros(0, np.float32))[0] == 2
     assert ref._util("phase_unwrap", np.zeros(0, np.float32))[0] == 2
     assert ref._util("phase_wrap", np.zeros(0, np.float32))[0] == 0
+
+
+def test_oracle_czt_cepstrum_golden(orc, golden):
+    """The committed CZT / cepstrum fixtures (tests/golden/make_golden.py section 8):
+    the restatement reproduces the reference outputs bit for bit, and those sit
+    within the reference harness tolerance of SciPy / NumPy f64 (rtol = atol =
+    2e-4 for CZT, python/test_czt.py)."""
+    g = golden("czt_testpy_n32")
+    w = complex(g["w"][0])
+    assert np.array_equal(orc.czt(g["x"], 32, w, 1.0 + 0j), g["kiss"])
+    np.testing.assert_allclose(g["kiss"], g["np64"], rtol=2e-4, atol=2e-4)
+    g = golden("czt_zoom_n32_m64")
+    W, A = complex(g["w"][0]), complex(g["a"][0])
+    assert np.array_equal(orc.czt(g["x"], 64, W, A), g["kiss"])
+    np.testing.assert_allclose(g["kiss"], g["np64"], rtol=2e-4, atol=2e-4)
+    g = golden("cepstrum_n64")
+    assert np.array_equal(orc.cepstrum(g["x"]), g["ceps_kiss"])
+    assert np.array_equal(orc.icepstrum_minphase(g["c"]), g["iceps_kiss"])
+    assert np.array_equal(orc.minphase_from_cepstrum(g["c"]), g["minph_kiss"])
+    for k in ("ceps", "iceps", "minph"):
+        np.testing.assert_allclose(g[k + "_kiss"], g[k + "_np64"], rtol=1e-4, atol=1e-4)
