@@ -1,13 +1,14 @@
-#!/bin/bash
-# Iteration run on the GPU box: parity tests, then kernel micro-benchmarks.
+# quick GPU iteration: selected tests then selected kbench cases
+#   bash scripts/gpu_iter.sh "<pytest -k expr or file list>" "<kbench cases>"
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q --timeout=600 ${PYTEST_ARGS} ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest $1 -x -v --timeout 120 --timeout-method thread > gpurun_out/iter_tests.log 2>&1
 rc=$?
-echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
-tail -15 gpurun_out/gpu_tests.log
-if [ $rc -le 1 ]; then
-  timeout -k 10 300 python scripts/kbench.py ${KBENCH_ARGS} > gpurun_out/kbench.log 2>&1
-  echo "kbench rc=$?" >> gpurun_out/kbench.log
-  cat gpurun_out/kbench.log
+tail -15 gpurun_out/iter_tests.log
+[ $rc -ne 0 ] && exit $rc
+if [ -n "$2" ]; then
+  timeout -k 10 400 python -u scripts/kbench.py --reps 10 --rounds 2 --cases "$2" > gpurun_out/iter_kbench.log 2>&1
+  rc=$?
+  cat gpurun_out/iter_kbench.log | tail -30
+  exit $rc
 fi

@@ -75,6 +75,16 @@ def case_stft(nch, seconds, complex_out=False, env=None):
     return (lambda: st.spectrogram(sig, out=out, complex_out=complex_out)), byts, (sig, out, st)
 
 
+def case_stft_n(nch, seconds, nfft, hop, sr=16000):
+    """magnitude rows at any nfft (non-power-of-two: frame gather + mixed-radix FFT + |X|)"""
+    n = seconds * sr
+    sig = torch.rand(nch, n, device="cuda") * 2 - 1
+    st = vv.Stft(nfft, hop)
+    fr = st.frames(n)
+    out = torch.empty(nch, fr, nfft, device="cuda")
+    return (lambda: st.spectrogram(sig, out=out)), nch * n * 4 + nch * fr * nfft * 4, (sig, out, st)
+
+
 def case_stft_power(nch, seconds):
     """power rows [ch][frame][513] (STFT mode 2, the mel kernel's input)"""
     n = seconds * 48000
@@ -340,6 +350,12 @@ CASES = {
     "blue48000unf": with_env(lambda: case_c2c(48000, 1024), "VVHIP_BLUE_UNFUSED", "1"),
     "blue48000old": with_env(lambda: case_c2c(48000, 1024), "VVHIP_FS_OLD", "1"),
     "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),
+    # mixed-radix (7-smooth non-power-of-two) lengths; *nomix: the f64 DFT kernel / Bluestein
+    **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
+    **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
+    "stft400": lambda: case_stft_n(32, 600, 400, 160),
+    **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 1000)},
+    "stft480": lambda: case_stft_n(32, 600, 480, 120, sr=48000),
     "c2c4096": lambda: case_c2c(4096, 16384),
     "c2c256": lambda: case_c2c(256, 262144),
     "r2c1024": lambda: case_r2c(1024, 131072),

@@ -1,0 +1,132 @@
+"""Mixed-radix FFT (mixed_fft.hip) for 7-smooth lengths that are not powers of
+two, n <= 4096 -- the lengths the reference sends through its O(n^2) DFT
+(src/spectral/fft_kiss.c:76-92, :114-116).
+
+Bars: the reference harness's per-bin tolerance against NumPy f64
+(python/test_fft.py:37-38, rtol = atol = 5e-5), normwise within 4x the error of
+SciPy's own f32 FFT, and at least as close to f64 as the reference (Kiss
+restatement, elementwise) where the oracle runs fast; the device batched,
+in-place and R2C/C2R entry points; and STFT frames of 400 / 480 samples.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import tolerances
+from vvapi import C2C, R2C, C2R, FWD, BWD
+
+pytestmark = pytest.mark.gpu
+
+SMOOTH = [6, 12, 45, 96, 100, 343, 400, 480, 625, 960, 1000, 1536, 2000, 2187, 2401, 3000, 3125, 3969, 4000]
+
+
+def _nw(y, ref):
+    return float(np.max(np.abs(y - ref)) / np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("n", SMOOTH)
+def test_mixed_c2c_vs_numpy(amd, orc, n):
+    import scipy.fft
+    r, a = tolerances()
+    rng = np.random.default_rng(5000 + n)
+    x = (rng.random(n) - 0.5 + 1j * (rng.random(n) - 0.5)).astype(np.complex64)
+    x64 = x.astype(np.complex128)
+    for d, npf, spf in ((FWD, np.fft.fft, scipy.fft.fft), (BWD, np.fft.ifft, scipy.fft.ifft)):
+        ref = npf(x64)
+        y = amd.fft(x, C2C, d)
+        np.testing.assert_allclose(y, ref, rtol=r, atol=a)
+        assert _nw(y, ref) <= max(4 * _nw(spf(x), ref), 1e-6), (d, _nw(y, ref), _nw(spf(x), ref))
+        if n <= 1000:
+            k = orc.fft(x, C2C, d)
+            assert np.all(np.abs(y - ref) <= np.abs(k - ref) + a + r * np.abs(ref))
+
+
+@pytest.mark.parametrize("n", [6, 100, 400, 480, 1000, 2000, 3000, 4000])
+def test_mixed_real_vs_numpy(amd, n):
+    r, a = tolerances()
+    rng = np.random.default_rng(6000 + n)
+    xr = (rng.random(n) - 0.5).astype(np.float32)
+    ref = np.fft.rfft(xr.astype(np.float64))
+    X = amd.fft(xr, R2C)
+    assert X.shape == (n // 2 + 1,) and X[-1].imag == 0.0
+    np.testing.assert_allclose(X, ref, rtol=r, atol=a)
+    Xin = ref.astype(np.complex64)
+    y = amd.fft(Xin, C2R, BWD, n=n)
+    np.testing.assert_allclose(y, np.fft.irfft(Xin.astype(np.complex128), n=n), rtol=r, atol=a)
+
+
+@pytest.mark.parametrize("n,b", [(400, 37), (480, 1), (45, 1000), (4000, 9), (2187, 5), (960, 513)])
+def test_mixed_batched_device(vdev, n, b):
+    """Batched device plans, batches that leave slots of a workgroup idle,
+    both directions and in place (in == out)."""
+    import torch
+    rng = np.random.default_rng(n * 7 + b)
+    x = (rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)
+    xd = torch.from_numpy(x).cuda()
+    x64 = x.astype(np.complex128)
+    yf = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xd).cpu().numpy()
+    yb = vdev.FftPlan(n, vdev.C2C, vdev.BWD, batch=b)(xd).cpu().numpy()
+    assert _nw(yf, np.fft.fft(x64, axis=1)) <= 2e-6
+    assert _nw(yb, np.fft.ifft(x64, axis=1)) <= 2e-6
+    xi = xd.clone()
+    vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xi, out=xi)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(xi.cpu().numpy(), yf)
+
+
+@pytest.mark.parametrize("n", [100, 400, 1000, 3000])
+def test_mixed_matches_dft_kernel(vdev, monkeypatch, n):
+    """The mixed-radix result agrees with the exact-angle f64 DFT kernel (n < 1025)
+    or Bluestein (VVHIP_NO_MIXED=1 selects them) to f32 FFT accuracy."""
+    import torch
+    rng = np.random.default_rng(n + 11)
+    b = 4
+    x = torch.from_numpy((rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)).cuda()
+    ym = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(x).cpu().numpy()
+    monkeypatch.setenv("VVHIP_NO_MIXED", "1")
+    yo = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(x).cpu().numpy()
+    assert _nw(ym, yo) <= 2e-6
+
+
+@pytest.mark.parametrize("nfft,hop", [(400, 160), (480, 120), (960, 240), (2000, 500)])
+def test_stft_smooth_nfft(amd, orc, nfft, hop):
+    """STFT magnitudes with speech-style non-power-of-two frames (the frame
+    gather + mixed-radix FFT + |X| path) against NumPy f64 and the reference."""
+    r, a = tolerances()
+    rng = np.random.default_rng(nfft * 3 + hop)
+    x = rng.uniform(-1, 1, 7 * nfft + 13).astype(np.float32)
+    mag = amd.spectrogram(x, nfft, hop)
+    ref = orc.spectrogram(x, nfft, hop)
+    assert mag.shape == ref.shape
+    w = orc.window(1, nfft).astype(np.float64)
+    pad = np.concatenate([x.astype(np.float64), np.zeros(nfft)])
+    np_mag = np.abs(np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(ref.shape[0])]) * w, axis=1))
+    np.testing.assert_allclose(mag, np_mag, rtol=r, atol=a)
+    assert np.all(np.abs(mag - np_mag) <= np.abs(ref - np_mag) + a + r * np_mag)
+
+
+@pytest.mark.parametrize("nfft,hop,nch,n", [(400, 160, 3, 16000), (480, 120, 2, 4801), (2000, 500, 2, 1999),
+                                           (45, 45, 1, 1000), (7, 3, 2, 50)])
+def test_stft_smooth_device_kinds(vdev, nfft, hop, nch, n):
+    """Multi-channel device STFT at smooth nfft, all three row kinds (magnitude,
+    complex, power bins 0..nfft/2) from the one fused mixed-radix kernel,
+    against NumPy f64 on the reference's frames (stft.c:112-144)."""
+    import torch
+    r, a = 5e-5, 5e-5
+    rng = np.random.default_rng(nfft + n)
+    x = rng.uniform(-1, 1, (nch, n)).astype(np.float32)
+    st = vdev.Stft(nfft, hop)
+    xd = torch.from_numpy(x).cuda()
+    mag = st.spectrogram(xd).cpu().numpy()
+    cpx = st.spectrogram(xd, complex_out=True).cpu().numpy()
+    pw = st.power(xd).cpu().numpy()
+    fr = st.frames(n)
+    w = (0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(nfft - 1) * np.arange(nfft, dtype=np.float32)))
+    for c in range(nch):
+        pad = np.concatenate([x[c].astype(np.float64), np.zeros(nfft)])
+        frames = np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w.astype(np.float64)
+        X = np.fft.fft(frames, axis=1)
+        np.testing.assert_allclose(cpx[c], X, rtol=r, atol=a)
+        np.testing.assert_allclose(mag[c], np.abs(X), rtol=r, atol=a)
+        np.testing.assert_allclose(pw[c], np.abs(X[:, :nfft // 2 + 1]) ** 2, rtol=2 * r, atol=2 * a * nfft)

@@ -1,0 +1,424 @@
+// mixed_fft.hip -- batched mixed-radix FFT for 7-smooth lengths that are not
+// powers of two (n = 2^a 3^b 5^c 7^d, 6 <= n <= 4096) on gfx950.
+//
+// The reference runs every non-power-of-two length through its O(n^2) DFT
+// (src/spectral/fft_kiss.c:76-92, dispatched at :114-116, and for all C2R).
+// The common audio lengths are 7-smooth (STFT frames of 400, 480, 960 or 2000
+// samples; 44100 = 2^2 3^2 5^2 7^2), so this kernel replaces that O(n^2) work
+// with a Stockham autosort FFT whose radices are read from a per-length plan:
+//
+//   pass p, radix R, Ns = product of the earlier radices, butterfly j < n/R:
+//     inputs   j + r*n/R                        (r < R)
+//     twiddle  W_{Ns*R}^{(j mod Ns)*r} = W_n^{r*(j mod Ns)*n/(Ns*R)}
+//     outputs  (j div Ns)*Ns*R + (j mod Ns) + r*Ns
+//
+// One transform lives in LDS (n float2) and is owned by T threads, each holding
+// at most 16 points per pass in VGPRs: a pass reads all of a thread's
+// butterflies, synchronises, and writes them back in place.  The W_n table
+// (rounded once from double on the host, tables.hip) is staged in LDS with the
+// transforms.  Radix-2/4/8 butterflies are the exact in-register DFTs of
+// fft_core.hpp; radix 3/5/7 use the symmetric-pair form with constants written
+// to 20 digits.  The inverse is conj(FFT(conj x)), then the caller's scale.
+//
+// Loads and stores are lane-contiguous (coalesced); a transform is read whole
+// into LDS before any of it is written, so in == out is safe.
+#include "fft_core.hpp"
+#include "vvhip_internal.hpp"
+
+#include <cstdlib>
+
+namespace vvh {
+
+namespace {
+
+constexpr int MIX_MAXP = 12;    // 3^7 = 2187 needs 7 passes; 4096-bounded lengths fit in 12
+constexpr int MIX_MAXN = 4096;
+constexpr int MIX_PTS = 16;     // points per thread per pass at most
+#ifndef VVH_MIX_LB
+#define VVH_MIX_LB 1
+#endif
+constexpr int LB = VVH_MIX_LB;
+
+struct MixedPlan {
+    int n;
+    int np;
+    int radix[MIX_MAXP];
+    int ns[MIX_MAXP];
+    int tstep[MIX_MAXP];   // n / (Ns * R): W_{Ns R}^m = W_n^(m * tstep)
+    float rns[MIX_MAXP];   // 1 / Ns for the butterfly index split
+};
+
+// cos / sin(2*pi*j/R) for the odd radices, j = 1 .. (R-1)/2
+template <int R>
+struct OddC;
+template <>
+struct OddC<3> {
+    __device__ static constexpr float c(int) { return -0.5f; }
+    __device__ static constexpr float s(int) { return 0.86602540378443864676f; }
+};
+template <>
+struct OddC<5> {
+    __device__ static constexpr float c(int j) { return j == 1 ? 0.30901699437494742410f : -0.80901699437494742410f; }
+    __device__ static constexpr float s(int j) { return j == 1 ? 0.95105651629515357212f : 0.58778525229247312917f; }
+};
+template <>
+struct OddC<7> {
+    __device__ static constexpr float c(int j) {
+        return j == 1 ? 0.62348980185873353053f : j == 2 ? -0.22252093395631440429f : -0.90096886790241912624f;
+    }
+    __device__ static constexpr float s(int j) {
+        return j == 1 ? 0.78183148246802980871f : j == 2 ? 0.97492791218182360702f : 0.43388373911755812048f;
+    }
+};
+
+// forward DFT of odd length R over symmetric pairs s_m = x_m + x_{R-m},
+// d_m = x_m - x_{R-m}:  X_k = x0 + sum_m cos(2 pi k m / R) s_m - i sum_m sin(2 pi k m / R) d_m,
+// X_{R-k} the same with +i.
+template <int R>
+__device__ __forceinline__ void odd_dft(float2* v) {
+    constexpr int H = (R - 1) / 2;
+    float2 s[H], d[H];
+#pragma unroll
+    for (int m = 1; m <= H; ++m) {
+        s[m - 1] = cadd(v[m], v[R - m]);
+        d[m - 1] = csub(v[m], v[R - m]);
+    }
+    const float2 x0 = v[0];
+    float2 sum = x0;
+#pragma unroll
+    for (int m = 0; m < H; ++m) sum = cadd(sum, s[m]);
+    v[0] = sum;
+#pragma unroll
+    for (int k = 1; k <= H; ++k) {
+        vf2_t a = pk(x0), b = vf2_t{0.0f, 0.0f};
+#pragma unroll
+        for (int m = 1; m <= H; ++m) {
+            const int j = (k * m) % R;
+            const int jj = j <= H ? j : R - j;            // cos symmetric, sin antisymmetric
+            const float c = OddC<R>::c(jj);
+            const float sn = j <= H ? OddC<R>::s(jj) : -OddC<R>::s(jj);
+            a = a + pk(s[m - 1]) * c;
+            b = b + pk(d[m - 1]) * sn;
+        }
+        // X_k = a - i b = (a.x + b.y, a.y - b.x);  X_{R-k} = a + i b
+        v[k] = cadd_i<false>(upk(a), upk(b));
+        v[R - k] = cadd_i<true>(upk(a), upk(b));
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void dft_fwd(float2* v) {
+    if constexpr (R == 2 || R == 4 || R == 8)
+        Dft<R, true>::run(v);
+    else
+        odd_dft<R>(v);
+}
+
+template <int T>
+__device__ __forceinline__ void msync() {
+    xsync<T>();
+}
+
+// Where a transform's points come from and go to.
+//   MODE 0: complex rows (nout bins out, scaled; the inverse by conjugation).
+//   MODE 4: real rows, two per complex transform (z = a + i b), nout bins of
+//           each row out through the split X_a = (Z[k] + conj Z[-k]) / 2,
+//           X_b = -i (Z[k] - conj Z[-k]) / 2.
+//   MODE 1/2/3: STFT frames of a [ch][n] signal, frames (2j, 2j+1) of one
+//           channel per complex transform (frame f starts at sample f*hop, zero
+//           past the end, times the window: frame_gather's single rounded
+//           product) -> |X| rows (1), complex rows (2) or |X|^2 for bins
+//           0..n/2 (3).  Pairs never span channels.
+struct MixIO {
+    const void* in;
+    float2* out;
+    long long nout, in_dist, out_dist, rows;
+    float scale;
+    float isign;   // -1 for the inverse: conj(FFT(conj x))
+    // STFT
+    long long sig_n, ch_stride, frames, ppc, hop, out_ch_stride;
+    const float* win;
+    int var;   // A/B switch (VVHIP_MIX_VAR)
+};
+
+template <int MODE>
+struct Row {
+    const float2* cin;
+    const float *ra, *rb;   // real rows / frame starts (rb = ra when there is no second)
+    const float* win;
+    long long lima, limb;   // STFT: samples of each frame inside the signal
+    bool has_b;
+    float2 *ca, *cb;
+    float *fa, *fb;
+
+    __device__ __forceinline__ void open(const MixIO& io, long long f, int n) {
+        if constexpr (MODE == 0) {
+            cin = reinterpret_cast<const float2*>(io.in) + f * io.in_dist;
+            ca = io.out + f * io.out_dist;
+        } else if constexpr (MODE == 4) {
+            const long long a = 2 * f;
+            has_b = a + 1 < io.rows;
+            ra = reinterpret_cast<const float*>(io.in) + a * io.in_dist;
+            rb = has_b ? ra + io.in_dist : ra;
+            ca = io.out + a * io.out_dist;
+            cb = ca + io.out_dist;
+        } else {
+            const long long c = f / io.ppc, fra = 2 * (f - c * io.ppc);
+            has_b = fra + 1 < io.frames;
+            const long long st = fra * io.hop;
+            ra = reinterpret_cast<const float*>(io.in) + c * io.ch_stride + st;
+            rb = ra + io.hop;
+            lima = io.sig_n - st;
+            limb = has_b ? lima - io.hop : 0;
+            win = io.win;
+            const long long w = MODE == 3 ? n / 2 + 1 : n;
+            const long long o = c * io.out_ch_stride + fra * w;
+            ca = reinterpret_cast<float2*>(io.out) + o;
+            cb = ca + w;
+            fa = reinterpret_cast<float*>(io.out) + o;
+            fb = fa + w;
+        }
+    }
+    __device__ __forceinline__ float2 load(const MixIO& io, int e) const {
+        if constexpr (MODE == 0) {   // the inverse conjugates (a sign, no branch)
+            const float2 x = cin[e];
+            return make_float2(x.x, x.y * io.isign);
+        } else if constexpr (MODE == 4) {
+            const float a = ra[e], b = rb[e];
+            return make_float2(a, has_b ? b : 0.0f);
+        } else {
+            // past the signal's end a load reads the window instead (always
+            // mapped) and the value is zeroed: no branch around the loads
+            const bool ia = e < lima, ib = e < limb;
+            const float a = *(ia ? ra + e : win + e), b = *(ib ? rb + e : win + e);
+            const float w = win[e];
+            return make_float2((ia ? a : 0.0f) * w, (ib ? b : 0.0f) * w);
+        }
+    }
+    // all outputs of the transform in buf (natural order), lane-contiguous
+    template <int T>
+    __device__ __forceinline__ void emit(const MixIO& io, const float2* buf, int t, int n) const {
+        if constexpr (MODE == 0) {
+            const float sx = io.scale, sy = io.scale * io.isign;
+            for (int e = t; e < io.nout; e += T) {
+                const float2 x = buf[e];
+                ca[e] = make_float2(x.x * sx, x.y * sy);
+            }
+        } else {
+            const int lim = (MODE == 4) ? (int)io.nout : (MODE == 3 ? n / 2 + 1 : n);
+            const float h = (MODE == 4) ? 0.5f * io.scale : 0.5f;
+            for (int e = t; e < lim; e += T) {
+                const float2 z = buf[e], m = buf[e == 0 ? 0 : n - e];
+                const float2 xa = make_float2((z.x + m.x) * h, (z.y - m.y) * h);
+                const float2 xb = make_float2((z.y + m.y) * h, (m.x - z.x) * h);
+                if constexpr (MODE == 4 || MODE == 2) {
+                    ca[e] = xa;
+                    if (has_b) cb[e] = xb;
+                } else if constexpr (MODE == 1) {
+                    fa[e] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xa.x, xa.x, xa.y * xa.y));
+                    if (has_b) fb[e] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xb.x, xb.x, xb.y * xb.y));
+                } else {
+                    fa[e] = __builtin_fmaf(xa.x, xa.x, xa.y * xa.y);
+                    if (has_b) fb[e] = __builtin_fmaf(xb.x, xb.x, xb.y * xb.y);
+                }
+            }
+        }
+    }
+};
+
+// Copy a transform in (a plain strided loop measured 1.3x faster than loading
+// all of a thread's points first: 400-point rows 0.26 vs 0.35 ms per GiB).
+template <int T, int MODE>
+__device__ __forceinline__ void mload(float2* buf, int t, int n, const MixIO& io, const Row<MODE>& row, bool act) {
+    if (act)
+        for (int e = t; e < n; e += T) buf[e] = row.load(io, e);
+    msync<T>();
+}
+
+// One middle Stockham pass of radix R on the LDS-resident transform `buf`.
+template <int R, int T>
+__device__ __forceinline__ void mpass(float2* buf, const float2* tab, int t, int n, int Ns, int tstep, float rns,
+                                      bool act) {
+    constexpr int MAXB = (MIX_PTS + R - 1) / R;
+    const int nb = n / R;
+    float2 v[MAXB][R];
+    if (act) {
+#pragma unroll
+        for (int b = 0; b < MAXB; ++b) {
+            const int j = t + b * T;
+            if (j < nb) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[b][r] = buf[j + r * nb];
+            }
+        }
+    }
+    msync<T>();
+    if (act) {
+#pragma unroll
+        for (int b = 0; b < MAXB; ++b) {
+            const int j = t + b * T;
+            if (j < nb) {
+                int q = (int)((float)j * rns);
+                int k = j - q * Ns;
+                if (k >= Ns) { k -= Ns; ++q; }
+                else if (k < 0) { k += Ns; --q; }
+                if (Ns > 1) {
+                    const int kt = k * tstep;
+#pragma unroll
+                    for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tab[r * kt]);
+                }
+                dft_fwd<R>(v[b]);
+                float2* dst = buf + q * Ns * R + k;
+#pragma unroll
+                for (int r = 0; r < R; ++r) dst[r * Ns] = v[b][r];
+            }
+        }
+    }
+    msync<T>();
+}
+
+#define VVH_MIX_RADIX_SWITCH(RAD, CALL) \
+    switch (RAD) {                      \
+        case 2: CALL(2); break;         \
+        case 3: CALL(3); break;         \
+        case 4: CALL(4); break;         \
+        case 5: CALL(5); break;         \
+        case 7: CALL(7); break;         \
+        default: CALL(8); break;        \
+    }
+
+template <int T, int MODE>
+__global__ void __launch_bounds__(256, LB)
+k_fft_mixed(MixedPlan pl, MixIO io, long long batch, const float2* __restrict__ gtab) {
+    constexpr int F = 256 / T;
+    extern __shared__ float2 sm[];
+    const int n = pl.n;
+    float2* tab = sm;
+    const int lt = threadIdx.x, slot = lt / T, t = lt % T;
+    float2* buf = sm + n + slot * n;
+    for (int i = lt; i < n; i += 256) tab[i] = gtab[i];
+    __syncthreads();
+    const long long stride = (long long)gridDim.x * F;
+    for (long long f0 = (long long)blockIdx.x * F; f0 < batch; f0 += stride) {
+        const long long f = f0 + slot;
+        const bool act = f < batch;
+        Row<MODE> row;
+        if (act) row.open(io, f, n);
+        mload<T, MODE>(buf, t, n, io, row, act);
+        // one call site for every pass: the radix switch is instantiated once
+        for (int p = 0; p < pl.np; ++p) {
+            const int Ns = pl.ns[p], ts = pl.tstep[p];
+            const float rn = pl.rns[p];
+#define VVH_MM(RR) mpass<RR, T>(buf, tab, t, n, Ns, ts, rn, act)
+            VVH_MIX_RADIX_SWITCH(pl.radix[p], VVH_MM)
+#undef VVH_MM
+        }
+        if (act) row.template emit<T>(io, buf, t, n);
+        msync<T>();   // the next transform's loads overwrite buf
+    }
+}
+
+// radices largest first: 8s, then a 4 or 2, then 7, 5, 3
+bool make_plan(long long n, MixedPlan* pl) {
+    if (n < 2 || n > MIX_MAXN) return false;
+    int m = (int)n, np = 0;
+    int rad[32];
+    while (m % 8 == 0) { rad[np++] = 8; m /= 8; }
+    if (m % 4 == 0) { rad[np++] = 4; m /= 4; }
+    if (m % 2 == 0) { rad[np++] = 2; m /= 2; }
+    for (int p : {7, 5, 3})
+        while (m % p == 0) { rad[np++] = p; m /= p; }
+    if (m != 1 || np > MIX_MAXP) return false;
+    pl->n = (int)n;
+    pl->np = np;
+    int ns = 1;
+    for (int p = 0; p < np; ++p) {
+        pl->radix[p] = rad[p];
+        pl->ns[p] = ns;
+        pl->tstep[p] = (int)n / (ns * rad[p]);
+        pl->rns[p] = 1.0f / (float)ns;
+        ns *= rad[p];
+    }
+    return true;
+}
+
+int mixed_threads(long long n) { return n <= 256 ? 16 : n <= 512 ? 32 : n <= 1024 ? 64 : 256; }
+
+template <int T, int MODE>
+hipError_t run_mixed_t(const MixedPlan& pl, const MixIO& io, long long batch, hipStream_t s) {
+    const float2* tab = twiddle_table(pl.n);
+    if (!tab) return hipErrorOutOfMemory;
+    constexpr int F = 256 / T;
+    const size_t lds = sizeof(float2) * (size_t)pl.n * (1 + F);
+    const long long work = (batch + F - 1) / F;
+    const int grid = persistent_grid((const void*)k_fft_mixed<T, MODE>, 256, lds, work);
+    hipLaunchKernelGGL((k_fft_mixed<T, MODE>), dim3(grid), dim3(256), lds, s, pl, io, batch, tab);
+    return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t run_mixed(const MixedPlan& pl, MixIO io, long long batch, hipStream_t s) {
+    const char* ev = getenv("VVHIP_MIX_VAR");
+    io.var = ev ? atoi(ev) : 0;
+    switch (mixed_threads(pl.n)) {
+        case 16: return run_mixed_t<16, MODE>(pl, io, batch, s);
+        case 32: return run_mixed_t<32, MODE>(pl, io, batch, s);
+        case 64: return run_mixed_t<64, MODE>(pl, io, batch, s);
+        default: return run_mixed_t<256, MODE>(pl, io, batch, s);
+    }
+}
+
+}  // namespace
+
+bool mixed_supported(long long n) {
+    MixedPlan pl;
+    return (n & (n - 1)) != 0 && make_plan(n, &pl);
+}
+
+hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
+                            long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s) {
+    MixedPlan pl;
+    if (!make_plan(n, &pl)) return hipErrorInvalidValue;
+    if (batch <= 0) return hipSuccess;
+    MixIO io{};
+    io.in = in;
+    io.out = out;
+    io.nout = nout;
+    io.in_dist = in_dist;
+    io.out_dist = out_dist;
+    io.rows = batch;
+    io.scale = scale;
+    io.isign = fwd ? 1.0f : -1.0f;
+    if (real_in) {   // real rows in pairs (forward only: R2C)
+        if (!fwd || nout > n / 2 + 1) return hipErrorInvalidValue;
+        return run_mixed<4>(pl, io, (batch + 1) / 2, s);
+    }
+    return run_mixed<0>(pl, io, batch, s);
+}
+
+hipError_t launch_stft_mixed(long long nfft, long long hop, int kind, const float* sig, long long n, long long nch,
+                             long long ch_stride, long long frames, const float* win, void* out,
+                             long long out_ch_stride, hipStream_t s) {
+    MixedPlan pl;
+    if (!make_plan(nfft, &pl) || kind < 0 || kind > 2) return hipErrorInvalidValue;
+    const long long ppc = (frames + 1) / 2;
+    const long long batch = nch * ppc;
+    if (batch <= 0) return hipSuccess;
+    MixIO io{};
+    io.in = sig;
+    io.out = reinterpret_cast<float2*>(out);
+    io.sig_n = n;
+    io.ch_stride = ch_stride;
+    io.frames = frames;
+    io.ppc = ppc;
+    io.hop = hop;
+    io.out_ch_stride = out_ch_stride;
+    io.win = win;
+    switch (kind) {
+        case 0: return run_mixed<1>(pl, io, batch, s);
+        case 1: return run_mixed<2>(pl, io, batch, s);
+        default: return run_mixed<3>(pl, io, batch, s);
+    }
+}
+
+}  // namespace vvh

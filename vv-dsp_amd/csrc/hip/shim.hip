@@ -182,10 +182,18 @@ static size_t fft_out_elems_bytes(const vvhip_fft* p) {
     }
 }
 
-// Non-power-of-two DFT: the exact-angle f64 O(n^2) kernel for short lengths,
-// Bluestein over the power-of-two kernels from BLUESTEIN_MIN on.
+// Non-power-of-two DFT: the mixed-radix kernel for 7-smooth n <= 4096, else the
+// exact-angle f64 O(n^2) kernel for short lengths and Bluestein over the
+// power-of-two kernels from BLUESTEIN_MIN on.  VVHIP_NO_MIXED=1 skips the
+// mixed-radix kernel (A/B and the tests that compare the two).
+static bool use_mixed(long long n) {
+    const char* e = getenv("VVHIP_NO_MIXED");
+    return !(e && *e == '1') && mixed_supported(n);
+}
 static hipError_t dft_any(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
                           long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s) {
+    if (use_mixed(n))
+        return launch_fft_mixed(n, fwd, in, real_in, out, nout, batch, in_dist, out_dist, scale, s);
     if (n >= BLUESTEIN_MIN && bluestein_supported(n))
         return launch_bluestein(n, fwd, in, real_in, out, nout, batch, in_dist, out_dist, scale, s);
     return launch_dft_naive(n, fwd, in, real_in, out, nout, batch, in_dist, out_dist, scale, s);
@@ -212,7 +220,7 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
         }
         const void* src = in;
         Scratch tmp(s);
-        if (in == out) {
+        if (in == out && !use_mixed(N)) {   // the mixed-radix kernel reads a transform whole before writing it
             HIPCHK(tmp.alloc(8 * n * batch), ST_INTERNAL);
             HIPCHK(hipMemcpyAsync(tmp.p, in, 8 * n * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
             src = tmp.p;
@@ -407,6 +415,12 @@ static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch
     if (stft_fused_supported(NF)) {
         HIPCHK(launch_stft(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch, (long long)ch_stride,
                            (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
+               ST_INTERNAL);
+        return ST_OK;
+    }
+    if (use_mixed(NF)) {   // 7-smooth nfft <= 4096: frames, FFT and |X| in one kernel
+        HIPCHK(launch_stft_mixed(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch,
+                                 (long long)ch_stride, (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
                ST_INTERNAL);
         return ST_OK;
     }

@@ -29,6 +29,16 @@ constexpr long long BLUESTEIN_MIN = 1025;   // below: the f64 O(n^2) DFT (exact-
 bool bluestein_supported(long long n);
 hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
                             long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s);
+// Mixed-radix Stockham FFT (mixed_fft.hip) for 7-smooth non-power-of-two n
+// <= 4096; same contract as launch_dft_naive, and in == out is allowed.
+bool mixed_supported(long long n);
+hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
+                            long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s);
+// STFT rows through the mixed-radix kernel (frames gathered and windowed on
+// load, |X| / complex / power bins 0..n/2 on store): kind as launch_stft.
+hipError_t launch_stft_mixed(long long nfft, long long hop, int kind, const float* sig, long long n, long long nch,
+                             long long ch_stride, long long frames, const float* win, void* out,
+                             long long out_ch_stride, hipStream_t s);
 // real[batch][n] -> complex[batch][n] (imaginary 0)
 hipError_t launch_promote_real(const float* in, float2* out, long long count, hipStream_t s);
 
