@@ -347,6 +347,9 @@ CASES = {
     "c2c2p13": lambda: case_c2c(1 << 13, 8192),
     "c2c2p22": lambda: case_c2c(1 << 22, 16),
     "blue48000": lambda: case_c2c(48000, 1024),
+    "blue48000nomix": with_env(lambda: case_c2c(48000, 1024), "VVHIP_NO_MIXED", "1"),
+    "mix44100": lambda: case_c2c(44100, 1024),
+    "mix96000": lambda: case_c2c(96000, 512),
     "blue48000unf": with_env(lambda: case_c2c(48000, 1024), "VVHIP_BLUE_UNFUSED", "1"),
     "blue48000old": with_env(lambda: case_c2c(48000, 1024), "VVHIP_FS_OLD", "1"),
     "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),

@@ -130,3 +130,56 @@ def test_stft_smooth_device_kinds(vdev, nfft, hop, nch, n):
         np.testing.assert_allclose(cpx[c], X, rtol=r, atol=a)
         np.testing.assert_allclose(mag[c], np.abs(X), rtol=r, atol=a)
         np.testing.assert_allclose(pw[c], np.abs(X[:, :nfft // 2 + 1]) ** 2, rtol=2 * r, atol=2 * a * nfft)
+
+
+LARGE = [4800, 11025, 16807, 24576 * 3, 44100, 48000, 88200, 96000]
+
+
+@pytest.mark.parametrize("n", LARGE)
+def test_mixed_fourstep_c2c(amd, n):
+    """7-smooth n > 4096: four-step over two mixed-radix passes.  Normwise
+    within 4x SciPy's f32 FFT error against f64, both directions, round trip."""
+    import scipy.fft
+    rng = np.random.default_rng(n)
+    x = (rng.random(n) - 0.5 + 1j * (rng.random(n) - 0.5)).astype(np.complex64)
+    for d, npf, spf in ((FWD, np.fft.fft, scipy.fft.fft), (BWD, np.fft.ifft, scipy.fft.ifft)):
+        ref = npf(x.astype(np.complex128))
+        y = amd.fft(x, C2C, d)
+        assert _nw(y, ref) <= max(4 * _nw(spf(x), ref), 1e-6), (d, _nw(y, ref), _nw(spf(x), ref))
+    assert _nw(amd.fft(amd.fft(x, C2C, FWD), C2C, BWD), x) <= 1e-5
+
+
+@pytest.mark.parametrize("n", [4800, 48000, 96000])
+def test_mixed_fourstep_real(amd, n):
+    import scipy.fft
+    rng = np.random.default_rng(n + 5)
+    xr = (rng.random(n) - 0.5).astype(np.float32)
+    ref = np.fft.rfft(xr.astype(np.float64))
+    X = amd.fft(xr, R2C)
+    assert X.shape == (n // 2 + 1,) and X[-1].imag == 0.0
+    assert _nw(X, ref) <= max(4 * _nw(scipy.fft.rfft(xr), ref), 1e-6)
+    assert _nw(amd.fft(X, C2R, BWD, n=n), xr) <= 1e-5
+
+
+@pytest.mark.parametrize("n,b,chunk_mb", [(48000, 5, ""), (44100, 3, "1"), (4800, 33, "0")])
+def test_mixed_fourstep_batched(vdev, monkeypatch, n, b, chunk_mb):
+    """Batched device plans through the four-step (chunks of one transform
+    with VVHIP_MIX_CHUNK_MB=1), in place, and against Bluestein
+    (VVHIP_NO_MIXED=1) to f32 FFT accuracy."""
+    import torch
+    rng = np.random.default_rng(n + b)
+    x = (rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)
+    xd = torch.from_numpy(x).cuda()
+    monkeypatch.setenv("VVHIP_MIX_CHUNK_MB", chunk_mb)
+    yf = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xd).cpu().numpy()
+    yb = vdev.FftPlan(n, vdev.C2C, vdev.BWD, batch=b)(xd).cpu().numpy()
+    x64 = x.astype(np.complex128)
+    for i in range(b):
+        assert _nw(yf[i], np.fft.fft(x64[i])) <= 2e-6, i
+        assert _nw(yb[i], np.fft.ifft(x64[i])) <= 2e-6, i
+    xi = xd.clone()
+    vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xi, out=xi)
+    np.testing.assert_array_equal(xi.cpu().numpy(), yf)
+    monkeypatch.setenv("VVHIP_NO_MIXED", "1")
+    yo = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xd).cpu().numpy()
+    assert _nw(yf, yo) <= 4e-6

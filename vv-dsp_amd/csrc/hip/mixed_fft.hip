@@ -318,6 +318,94 @@ k_fft_mixed(MixedPlan pl, MixIO io, long long batch, const float2* __restrict__ 
     }
 }
 
+// ------------------------------------------------------------------------
+// Four-step for 7-smooth n > 4096 (n = N1 * N2, both <= 4096): the columns
+// pass takes N2 columns of length N1 (x[n1 * N2 + n2]), FFTs them and applies
+// W_n^(n2 * k1) into an intermediate [N1][N2]; the rows pass FFTs each row
+// k1 along n2 and stores X[k1 + N1 * k2].  The strided side of each pass is
+// cooperative over the workgroup: its F transform slots own F adjacent
+// columns (rows), so for one element index the workgroup touches F adjacent
+// complex values (128 B at F = 16) instead of one per transform.
+// ------------------------------------------------------------------------
+struct FsIO {
+    const void* in;
+    float2* mid;
+    float2* out;
+    long long in_dist, out_dist, nout, n;
+    int N1, N2, real_in;
+    float scale, isign;
+    const float2* twn;        // W_n, n entries
+    long long groups_per_b;   // ceil(N2 / F) (columns) or ceil(N1 / F) (rows)
+};
+
+template <int T, int PASS>
+__global__ void __launch_bounds__(256)
+k_fft_mixed_fs(MixedPlan pl, FsIO io, long long groups, const float2* __restrict__ gtab) {
+    constexpr int F = 256 / T;
+    extern __shared__ float2 sm[];
+    const int m = pl.n;   // this pass's FFT length: N1 (columns) or N2 (rows)
+    float2* tab = sm;
+    const int lt = threadIdx.x, slot = lt / T, t = lt % T;
+    float2* buf = sm + m + slot * m;
+    float2* bufs = sm + m;
+    for (int i = lt; i < m; i += 256) tab[i] = gtab[i];
+    __syncthreads();
+    const int N1 = io.N1, N2 = io.N2;
+    const int width = PASS == 0 ? N2 : N1;   // columns or rows per transform of the batch
+    for (long long g = blockIdx.x; g < groups; g += gridDim.x) {
+        const long long b = g / io.groups_per_b;
+        const int i0 = (int)(g - b * io.groups_per_b) * F;
+        if constexpr (PASS == 0) {
+            const float* rin = reinterpret_cast<const float*>(io.in) + b * io.in_dist;
+            const float2* cin = reinterpret_cast<const float2*>(io.in) + b * io.in_dist;
+            for (int idx = lt; idx < m * F; idx += 256) {
+                const int e = idx / F, sl = idx % F, col = i0 + sl;
+                if (col < N2) {
+                    const long long o = (long long)e * N2 + col;
+                    float2 x;
+                    if (io.real_in) x = make_float2(rin[o], 0.0f);
+                    else { x = cin[o]; x.y *= io.isign; }
+                    bufs[sl * m + e] = x;
+                }
+            }
+        } else {
+            if (i0 + slot < N1) {
+                const float2* src = io.mid + (b * N1 + i0 + slot) * (long long)N2;
+                for (int e = t; e < m; e += T) buf[e] = src[e];
+            }
+        }
+        __syncthreads();
+        const bool act = i0 + slot < width;
+        for (int p = 0; p < pl.np; ++p) {
+            const int Ns = pl.ns[p], ts = pl.tstep[p];
+            const float rn = pl.rns[p];
+#define VVH_MM(RR) mpass<RR, T>(buf, tab, t, m, Ns, ts, rn, act)
+            VVH_MIX_RADIX_SWITCH(pl.radix[p], VVH_MM)
+#undef VVH_MM
+        }
+        __syncthreads();   // the stores read every slot's buffer
+        if constexpr (PASS == 0) {
+            float2* dst = io.mid + b * io.n;
+            for (int idx = lt; idx < m * F; idx += 256) {
+                const int k1 = idx / F, sl = idx % F, col = i0 + sl;
+                if (col < N2) dst[(long long)k1 * N2 + col] = cmul(bufs[sl * m + k1], io.twn[col * k1]);
+            }
+        } else {
+            float2* dst = io.out + b * io.out_dist;
+            const float sx = io.scale, sy = io.scale * io.isign;
+            for (int idx = lt; idx < m * F; idx += 256) {
+                const int k2 = idx / F, sl = idx % F, k1 = i0 + sl;
+                const long long k = k1 + (long long)N1 * k2;
+                if (k1 < N1 && k < io.nout) {
+                    const float2 x = bufs[sl * m + k2];
+                    dst[k] = make_float2(x.x * sx, x.y * sy);
+                }
+            }
+        }
+        __syncthreads();   // the next group's loads overwrite the buffers
+    }
+}
+
 // radices largest first: 8s, then a 4 or 2, then 7, 5, 3
 bool make_plan(long long n, MixedPlan* pl) {
     if (n < 2 || n > MIX_MAXN) return false;
@@ -368,18 +456,102 @@ hipError_t run_mixed(const MixedPlan& pl, MixIO io, long long batch, hipStream_t
     }
 }
 
+template <int T, int PASS>
+hipError_t run_fs_t(const MixedPlan& pl, const FsIO& io0, long long batch, hipStream_t s) {
+    const float2* tab = twiddle_table(pl.n);
+    if (!tab) return hipErrorOutOfMemory;
+    constexpr int F = 256 / T;
+    FsIO io = io0;
+    io.groups_per_b = ((PASS == 0 ? io.N2 : io.N1) + F - 1) / F;
+    const long long groups = batch * io.groups_per_b;
+    const size_t lds = sizeof(float2) * (size_t)pl.n * (1 + F);
+    const int grid = persistent_grid((const void*)k_fft_mixed_fs<T, PASS>, 256, lds, groups);
+    hipLaunchKernelGGL((k_fft_mixed_fs<T, PASS>), dim3(grid), dim3(256), lds, s, pl, io, groups, tab);
+    return hipGetLastError();
+}
+
+template <int PASS>
+hipError_t run_fs(const MixedPlan& pl, const FsIO& io, long long batch, hipStream_t s) {
+    switch (mixed_threads(pl.n)) {
+        case 16: return run_fs_t<16, PASS>(pl, io, batch, s);
+        case 32: return run_fs_t<32, PASS>(pl, io, batch, s);
+        case 64: return run_fs_t<64, PASS>(pl, io, batch, s);
+        default: return run_fs_t<256, PASS>(pl, io, batch, s);
+    }
+}
+
+// n = N1 * N2 with both factors plannable, max(N1, N2) smallest (N1 <= N2)
+bool fs_split(long long n, int* n1, int* n2) {
+    if (n <= MIX_MAXN || n > (long long)MIX_MAXN * MIX_MAXN) return false;
+    MixedPlan pl;
+    int best = 0;
+    for (long long a = 2; a * a <= n; ++a) {
+        if (n % a || !make_plan(a, &pl) || !make_plan(n / a, &pl)) continue;
+        best = (int)a;   // ascending: the last admissible a is the most balanced
+    }
+    if (!best) return false;
+    *n1 = best;
+    *n2 = (int)(n / best);
+    return true;
+}
+
 }  // namespace
 
 bool mixed_supported(long long n) {
+    if ((n & (n - 1)) == 0) return false;
     MixedPlan pl;
-    return (n & (n - 1)) != 0 && make_plan(n, &pl);
+    int n1, n2;
+    return make_plan(n, &pl) || fs_split(n, &n1, &n2);
+}
+
+// four-step over an intermediate of at most VVHIP_MIX_CHUNK_MB (default: the
+// whole batch) per chunk of transforms
+static hipError_t launch_fft_mixed_fs(long long n, int fwd, const void* in, int real_in, float2* out,
+                                      long long nout, long long batch, long long in_dist, long long out_dist,
+                                      float scale, hipStream_t s) {
+    int n1, n2;
+    MixedPlan p1, p2;
+    if (!fs_split(n, &n1, &n2) || !make_plan(n1, &p1) || !make_plan(n2, &p2)) return hipErrorInvalidValue;
+    const float2* twn = twiddle_table((int)n);
+    if (!twn) return hipErrorOutOfMemory;
+    const char* ec = getenv("VVHIP_MIX_CHUNK_MB");
+    const long long cmb = ec ? atoll(ec) : 0;
+    long long chunk = cmb > 0 ? (cmb << 20) / (8 * n) : batch;
+    if (chunk < 1) chunk = 1;
+    if (chunk > batch) chunk = batch;
+    float2* mid = nullptr;
+    hipError_t e = hipMallocAsync((void**)&mid, sizeof(float2) * (size_t)n * (size_t)chunk, s);
+    if (e != hipSuccess) return e;
+    FsIO io{};
+    io.mid = mid;
+    io.nout = nout;
+    io.n = n;
+    io.N1 = n1;
+    io.N2 = n2;
+    io.real_in = real_in;
+    io.scale = scale;
+    io.isign = fwd ? 1.0f : -1.0f;
+    io.twn = twn;
+    io.in_dist = in_dist;
+    io.out_dist = out_dist;
+    for (long long c = 0; c < batch && e == hipSuccess; c += chunk) {
+        const long long nb = batch - c < chunk ? batch - c : chunk;
+        io.in = real_in ? (const void*)(reinterpret_cast<const float*>(in) + c * in_dist)
+                        : (const void*)(reinterpret_cast<const float2*>(in) + c * in_dist);
+        io.out = out + c * out_dist;
+        e = run_fs<0>(p1, io, nb, s);
+        if (e == hipSuccess) e = run_fs<1>(p2, io, nb, s);
+    }
+    (void)hipFreeAsync(mid, s);
+    return e;
 }
 
 hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
                             long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s) {
-    MixedPlan pl;
-    if (!make_plan(n, &pl)) return hipErrorInvalidValue;
     if (batch <= 0) return hipSuccess;
+    MixedPlan pl;
+    if (!make_plan(n, &pl))
+        return launch_fft_mixed_fs(n, fwd, in, real_in, out, nout, batch, in_dist, out_dist, scale, s);
     MixIO io{};
     io.in = in;
     io.out = out;
