@@ -88,6 +88,10 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_fir_apply_fft_device(vv_dsp_fir_plan* p, c
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_fir_apply_direct_device(vv_dsp_fir_plan* p, const vv_dsp_real* d_x,
                                                               vv_dsp_real* d_y, size_t n, size_t nch,
                                                               size_t x_stride, size_t y_stride, void* stream);
+/* vv_dsp_filtfilt_fir over nch rows (filter/common.c:23-80), bit-identical */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_filtfilt_fir_device(vv_dsp_fir_plan* p, const vv_dsp_real* d_x,
+                                                          vv_dsp_real* d_y, size_t n, size_t nch, size_t x_stride,
+                                                          size_t y_stride, void* stream);
 
 /* Hilbert analytic signal of `batch` contiguous real[N] rows -> cpx[batch][N] */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_hilbert_analytic_device(const vv_dsp_real* d_x, size_t N, size_t batch,

@@ -20,7 +20,7 @@
  *   vvhip_fft_*  : the FFT backend vtable slot, src/spectral/fft_backend.h:32-38
  *                  (make_plan / execute / free_plan / is_available)
  *   vvhip_stft_* : src/spectral/stft.c:30-144 (create, process, reconstruct, spectrogram)
- *   vvhip_fir_*  : src/filter/fir.c:75-196 (apply_fft, apply)
+ *   vvhip_fir_*  : src/filter/fir.c:75-196 (apply_fft, apply), filter/common.c:23-80 (filtfilt)
  *   vvhip_hilbert_*: src/spectral/hilbert.c:14-75
  *   vvhip_dct_*  : src/spectral/dct.c:86-136
  *   vvhip_czt_*  : src/spectral/czt.c:44-178 (exec_cpx, exec_real)
@@ -140,6 +140,11 @@ int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_ou
 int vvhip_mel_host(vvhip_mel* m, const float* in, size_t frames, float* out, int kind);
 
 /* Block length (real FFT size) the overlap-save path uses for a signal of n samples. */
+/* zero-phase filtering (filter/common.c:23-80): reflection pad, direct form
+ * forward and backward in the reference's summation order (bit-identical) */
+int vvhip_fir_filtfilt_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n, size_t nch, size_t x_stride,
+                              size_t y_stride, void* stream);
+int vvhip_fir_filtfilt_host(vvhip_fir* f, const float* x, float* y, size_t n);
 size_t vvhip_fir_block_size(vvhip_fir* f, size_t n);
 
 /* ---- Hilbert analytic signal (hilbert.c:14-75) ---- */

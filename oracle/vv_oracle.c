@@ -406,6 +406,44 @@ int orc_fir_apply_fft(const float* h, size_t taps, const float* x, float* y, siz
     return 0;
 }
 
+/* common.c:6-80 -- zero-phase FIR: reflection padding of num_taps-1 samples,
+ * the stateless direct form forward, reverse, again, reverse, centre.  Written
+ * as a restatement of the published algorithm, index by index (the reflection
+ * clamps to x[n-1] / x[0] once the pad exceeds the signal). */
+int orc_filtfilt_fir(const float* h, size_t taps, const float* x, float* y, size_t n) {
+    if (!h || !x || !y) return 1;
+    if (taps == 0) return 2;
+    if (n == 0) return 0;   /* the reference reads x[-1] here; nothing to produce */
+    const size_t pad = taps - 1, m = n + 2 * pad;
+    float* e = (float*)malloc(m * sizeof(float));
+    float* a = (float*)malloc(m * sizeof(float));
+    float* b = (float*)malloc(m * sizeof(float));
+    if (!e || !a || !b) { free(e); free(a); free(b); return 4; }
+    for (size_t i = 0; i < n; ++i) e[pad + i] = x[i];
+    for (size_t i = 0; i < pad; ++i) {
+        e[pad - 1 - i] = x[(i + 1 <= n ? i + 1 : n) - 1];
+        e[pad + n + i] = x[i + 1 <= n ? n - 1 - i : 0];
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+        const float* s = pass ? b : e;
+        float* d = a;
+        float* tmp = (float*)malloc(m * sizeof(float));
+        if (!tmp) { free(e); free(a); free(b); return 4; }
+        for (size_t i = 0; i < m; ++i) {
+            float acc = 0;
+            const size_t kmax = i + 1 < taps ? i + 1 : taps;
+            for (size_t k = 0; k < kmax; ++k) acc += h[k] * s[i - k];
+            tmp[i] = acc;
+        }
+        for (size_t i = 0; i < m; ++i) d[i] = tmp[m - 1 - i];   /* reverse */
+        free(tmp);
+        if (!pass) memcpy(b, a, m * sizeof(float));
+    }
+    memcpy(y, a + pad, n * sizeof(float));
+    free(e); free(a); free(b);
+    return 0;
+}
+
 /* ---- mel / MFCC (src/features/mel.c) ------------------------------------- */
 /* mel.c:14-20 */
 float orc_hz_to_mel(float hz) {

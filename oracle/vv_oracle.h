@@ -55,6 +55,8 @@ int orc_fir_apply(const float* h, size_t taps, float* history, size_t* hist_idx,
                   const float* x, float* y, size_t n);
 /* Single-block FFT convolution exactly as :75-135 (its C2R is O(Nfft^2): small n only). */
 int orc_fir_apply_fft(const float* h, size_t taps, const float* x, float* y, size_t n);
+/* filter/common.c:6-80 vv_dsp_filtfilt_fir */
+int orc_filtfilt_fir(const float* h, size_t taps, const float* x, float* y, size_t n);
 
 /* Mel / MFCC (src/features/mel.c; HTK variant, the only one the reference builds) */
 /* ---- framing (src/core/framing.c) ---- */

@@ -213,3 +213,37 @@ def test_oracle_not_linked_into_product(amd_lib_path):
     assert all(s.startswith(("vv_dsp_", "vvhip_")) or s in ("_init", "_fini") for s in funcs), funcs
     ldd = subprocess.run(["ldd", amd_lib_path], capture_output=True, text=True).stdout
     assert "oracle" not in ldd and "vvref" not in ldd
+
+
+def test_windows_bitexact_host_setup(cpu_lib, ref):
+    """vv_dsp_window_{boxcar,hann,hamming} (window.c:16-49): one-time host
+    tables with the reference's float arithmetic, bit-identical to the compiled
+    reference, with its argument checks (window_tests.c:104-115: N = 0 ->
+    INVALID_SIZE, NULL -> NULL_POINTER)."""
+    import numpy as np
+    for kind in (0, 1, 2):
+        for n in (1, 2, 8, 17, 400, 1024, 4096):
+            st, w = cpu_lib.window(kind, n)
+            st_r, w_r = ref.window(kind, n)
+            assert st == st_r == OK
+            assert np.array_equal(w, w_r), (kind, n)
+        assert cpu_lib.window(kind, 0)[0] == ref.window(kind, 0)[0] == ERR_SIZE
+        assert cpu_lib.window(kind, 4, null_out=True)[0] == ERR_NULL
+    st, w = cpu_lib.window(1, 8)   # gtest/test_window.cpp:154-178, 1e-6
+    exp = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(8) / 7)
+    assert np.max(np.abs(w - exp)) <= 1e-6
+
+
+def test_filtfilt_argument_checks(cpu_lib, ref):
+    """common.c:28-29: NULL -> NULL_POINTER, num_taps = 0 -> INVALID_SIZE
+    (no GPU needed: checked before any device work)."""
+    import numpy as np
+    L = cpu_lib.lib
+    h = np.ones(3, np.float32)
+    x = np.ones(8, np.float32)
+    y = np.zeros(8, np.float32)
+    for lib in (L, ref.lib):
+        assert lib.vv_dsp_filtfilt_fir(None, C.c_size_t(3), x.ctypes.data_as(C.c_void_p), y.ctypes.data_as(C.c_void_p),
+                                       C.c_size_t(8)) == ERR_NULL
+        assert lib.vv_dsp_filtfilt_fir(h.ctypes.data_as(C.c_void_p), C.c_size_t(0), x.ctypes.data_as(C.c_void_p),
+                                       y.ctypes.data_as(C.c_void_p), C.c_size_t(8)) == ERR_SIZE

@@ -506,7 +506,7 @@ def test_golden_dct(amd, golden):
         np.testing.assert_allclose(xi, g["x"], rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 8, 63, 64, 257, 1024, 8192])
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 40, 63, 64, 257, 400, 1000, 1024, 4800, 8192])
 def test_dct_types_vs_formula(amd, n):
     import scipy.fft
     rng = np.random.default_rng(n)
@@ -721,7 +721,7 @@ def test_hilbert_batched_device(vdev, n):
         np.testing.assert_allclose(z.real, x, rtol=0, atol=0)   # the real part is the input itself
 
 
-@pytest.mark.parametrize("n", [2, 4, 16, 32, 128, 256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("n", [2, 4, 16, 32, 40, 128, 256, 400, 512, 1000, 1024, 2048, 4096])
 def test_dct2_batched_device(vdev, n):
     """DCT-II over a batch of rows (two rows per complex FFT where the FFT can
     be mirror-paired) vs scipy.fft.dct(type 2)/2 in f64 (dct.c:21-30)."""

@@ -372,6 +372,20 @@ class VvDsp(_CztMixin):
         assert self.lib.vv_dsp_window_hann(n, _fp(w)) == OK
         return w
 
+    def window(self, kind, n, null_out=False):
+        """vv_dsp_window_{boxcar,hann,hamming} (kind = the STFT enum) -> (status, w)"""
+        f = (self.lib.vv_dsp_window_boxcar, self.lib.vv_dsp_window_hann, self.lib.vv_dsp_window_hamming)[kind]
+        w = np.zeros(max(n, 1), np.float32)
+        return f(C.c_size_t(n), None if null_out else _fp(w)), w[:n]
+
+    def filtfilt(self, h, x):
+        """vv_dsp_filtfilt_fir (filter/common.c:23-80) -> (status, y)"""
+        h = np.ascontiguousarray(h, np.float32)
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros(max(len(x), 1), np.float32)
+        st = self.lib.vv_dsp_filtfilt_fir(_fp(h), C.c_size_t(len(h)), _fp(x), _fp(y), C.c_size_t(len(x)))
+        return st, y[:len(x)]
+
     # ---- mel / MFCC (include/vv_dsp/features/mel.h) ---------------------
     def _mel_setup(self):
         L = self.lib
@@ -592,6 +606,15 @@ class Oracle(_CztMixin):
         L.orc_overlap_add.argtypes = [_f32p, _f32p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t]
         frame = np.ascontiguousarray(frame, np.float32)
         return L.orc_overlap_add(_fp(frame), _fp(out), len(out), len(frame), hop, index)
+
+    def filtfilt(self, h, x):
+        L = self.lib
+        L.orc_filtfilt_fir.argtypes = [_f32p, C.c_size_t, _f32p, _f32p, C.c_size_t]
+        h = np.ascontiguousarray(h, np.float32)
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.zeros(max(len(x), 1), np.float32)
+        assert L.orc_filtfilt_fir(_fp(h), len(h), _fp(x), _fp(y), len(x)) == 0
+        return y[:len(x)]
 
     def fir_apply(self, h, x, fft=False):
         h = np.ascontiguousarray(h, np.float32)

@@ -548,17 +548,24 @@ constexpr int DIRECT_TILE = 1024;
 constexpr int DIRECT_TAPS = 4096;
 constexpr int DIRECT_OPT = DIRECT_TILE / 256;   // outputs per thread
 
+// SRC 0: x[i] for 0 <= i < n, samples before x[0] from `prefix` (taps-1 per
+//        channel, prefix_stride apart; NULL: zeros), zero past n.
+// SRC 1: the reflect-padded input of vv_dsp_filtfilt_fir (common.c:6-21):
+//        output i is sample pad + i of ext = [reflection | x | reflection] with
+//        pad = taps - 1, so every tap lands inside ext; `xn` is x's length.
+// REV:   output i is stored at y[n - 1 - i] (the filtfilt reversals).
+template <int SRC, bool REV>
 __global__ void __launch_bounds__(256)
 k_fir_direct(const float* __restrict__ h, long long taps, const float* __restrict__ x,
              float* __restrict__ y, long long n, long long x_stride, long long y_stride,
-             const float* __restrict__ prefix, long long tiles_per_ch) {
+             const float* __restrict__ prefix, long long prefix_stride, long long xn, long long tiles_per_ch) {
     __shared__ float hs[DIRECT_TAPS];
     __shared__ float xs[DIRECT_TILE + DIRECT_TAPS];
     const long long c = blockIdx.x / tiles_per_ch;
     const long long i0 = (blockIdx.x % tiles_per_ch) * DIRECT_TILE;
     const long long lm1 = taps - 1;
     const float* xc = x + c * x_stride;
-    const float* pc = prefix ? prefix + c * lm1 : nullptr;
+    const float* pc = prefix ? prefix + c * prefix_stride : nullptr;
     float acc[DIRECT_OPT];
 #pragma unroll
     for (int j = 0; j < DIRECT_OPT; ++j) acc[j] = 0.0f;
@@ -571,8 +578,18 @@ k_fir_direct(const float* __restrict__ h, long long taps, const float* __restric
         for (int e = threadIdx.x; e < DIRECT_TILE + tt - 1; e += 256) {
             const long long idx = base + e;   // >= -lm1
             float v;
-            if (idx < 0) v = pc ? pc[lm1 + idx] : 0.0f;
-            else v = (idx < n) ? xc[idx] : 0.0f;
+            if constexpr (SRC == 0) {
+                if (idx < 0) v = pc ? pc[lm1 + idx] : 0.0f;
+                else v = (idx < n) ? xc[idx] : 0.0f;
+            } else {
+                // ext[pad + idx]: left pad ext[pad-1-i] = x[min(i+1, xn) - 1],
+                // right pad ext[pad+xn+i] = x[i + 1 <= xn ? xn-1-i : 0]
+                long long src;
+                if (idx < 0) src = (-idx < xn ? -idx : xn) - 1;
+                else if (idx < xn) src = idx;
+                else src = (idx - xn + 1 <= xn) ? 2 * xn - 1 - idx : 0;
+                v = (idx < n) ? xc[src] : 0.0f;
+            }
             xs[e] = v;
         }
         __syncthreads();
@@ -595,7 +612,7 @@ k_fir_direct(const float* __restrict__ h, long long taps, const float* __restric
 #pragma unroll
     for (int j = 0; j < DIRECT_OPT; ++j) {
         const long long i = i0 + threadIdx.x + 256 * j;
-        if (i < n) yc[i] = acc[j];
+        if (i < n) yc[REV ? n - 1 - i : i] = acc[j];
     }
 }
 
@@ -605,8 +622,29 @@ hipError_t launch_fir_direct(const float* h, long long taps, const float* x, flo
     const long long tiles = (n + DIRECT_TILE - 1) / DIRECT_TILE;
     if (tiles * nch <= 0) return hipSuccess;
     if (taps < 1 || tiles * nch > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_fir_direct, dim3((unsigned)(tiles * nch)), dim3(256), 0, s, h, taps, x, y, n,
-                       x_stride, y_stride, prefix, tiles);
+    hipLaunchKernelGGL((k_fir_direct<0, false>), dim3((unsigned)(tiles * nch)), dim3(256), 0, s, h, taps, x, y, n,
+                       x_stride, y_stride, prefix, taps - 1, n, tiles);
+    return hipGetLastError();
+}
+
+// vv_dsp_filtfilt_fir (common.c:23-80) over nch rows of n samples: the forward
+// pass writes the n + pad outputs of ext that the backward pass reads, already
+// reversed (tmp_rev[j] = tmp[ext_n - 1 - j]); the backward pass is then a plain
+// direct form over tmp_rev whose first pad samples are its history, and its n
+// outputs are stored reversed into y.  Both passes keep the reference's
+// summation order (acc = 0, += h[k] * s[i-k], k ascending, no FMA); every
+// output needed has all its taps inside ext, so the reference's maxk bound
+// never cuts a sum short and the results are bit-identical.
+hipError_t launch_filtfilt(const float* h, long long taps, const float* x, float* y, long long n, long long nch,
+                           long long x_stride, long long y_stride, float* tmp, hipStream_t s) {
+    const long long pad = taps - 1, m = n + pad;
+    const long long t1 = (m + DIRECT_TILE - 1) / DIRECT_TILE, t2 = (n + DIRECT_TILE - 1) / DIRECT_TILE;
+    if (n <= 0 || nch <= 0) return hipSuccess;
+    if (taps < 1 || t1 * nch > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_fir_direct<1, true>), dim3((unsigned)(t1 * nch)), dim3(256), 0, s, h, taps, x, tmp, m,
+                       x_stride, m, (const float*)nullptr, 0LL, n, t1);
+    hipLaunchKernelGGL((k_fir_direct<0, true>), dim3((unsigned)(t2 * nch)), dim3(256), 0, s, h, taps,
+                       (const float*)(tmp + pad), y, n, m, y_stride, (const float*)tmp, m, n, t2);
     return hipGetLastError();
 }
 

@@ -842,6 +842,34 @@ int vvhip_fir_apply_host(vvhip_fir* f, const float* x, float* y, size_t n, const
     return ST_OK;
 }
 
+int vvhip_fir_filtfilt_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n, size_t nch, size_t x_stride,
+                              size_t y_stride, void* stream) {
+    if (!f || !d_x || !d_y) return ST_NULL;
+    if (n == 0 || nch == 0) return ST_OK;
+    hipStream_t s = (hipStream_t)stream;
+    Scratch tmp(s);
+    HIPCHK(tmp.alloc(sizeof(float) * (n + f->taps - 1) * nch), ST_INTERNAL);
+    HIPCHK(launch_filtfilt(f->d_h, (long long)f->taps, d_x, d_y, (long long)n, (long long)nch, (long long)x_stride,
+                           (long long)y_stride, (float*)tmp.p, s),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_fir_filtfilt_host(vvhip_fir* f, const float* x, float* y, size_t n) {
+    if (!f || !x || !y) return ST_NULL;
+    std::lock_guard<std::mutex> host_lock(f->host_mu);
+    if (n == 0) return ST_OK;
+    if (!f->stream) HIPCHK(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking), ST_INTERNAL);
+    HIPCHK(f->bx.ensure(sizeof(float) * n), ST_INTERNAL);
+    HIPCHK(f->by.ensure(sizeof(float) * n), ST_INTERNAL);
+    HIPCHK(hipMemcpyAsync(f->bx.p, x, sizeof(float) * n, hipMemcpyHostToDevice, f->stream), ST_INTERNAL);
+    int st = vvhip_fir_filtfilt_device(f, (const float*)f->bx.p, (float*)f->by.p, n, 1, n, n, f->stream);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(y, f->by.p, sizeof(float) * n, hipMemcpyDeviceToHost, f->stream), ST_INTERNAL);
+    HIPCHK(hipStreamSynchronize(f->stream), ST_INTERNAL);
+    return ST_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Hilbert
 // ---------------------------------------------------------------------------
@@ -1096,7 +1124,9 @@ static int dct_run(const float* d_in, float* d_out, size_t n, size_t batch, int 
         HIPCHK(hipStreamSynchronize(s), ST_INTERNAL);
         if (h) return ST_NAN;
     }
-    const bool fast = is_pow2(n) && n >= 4 && n <= 8192;
+    // Makhoul re-ordering + a real FFT: power-of-two n, and even 7-smooth n
+    // through the mixed-radix kernels (odd n would need the other permutation)
+    const bool fast = (is_pow2(n) && n >= 4 && n <= 8192) || (n % 2 == 0 && n >= 4 && use_mixed(N));
     if (fast && type == 2 && dir > 0) {
         const float2* tw4n = twiddle_table((int)(4 * n));
         if (!tw4n) return fail(ST_INTERNAL, "dct twiddles");

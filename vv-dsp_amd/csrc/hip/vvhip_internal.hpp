@@ -137,6 +137,9 @@ hipError_t launch_fir_ols(long long nfft, long long taps, const float2* H, const
 hipError_t launch_fir_direct(const float* h, long long taps, const float* x, float* y, long long n,
                              long long nch, long long x_stride, long long y_stride,
                              const float* prefix, hipStream_t s);
+// vv_dsp_filtfilt_fir over nch rows (common.c:23-80); tmp: nch * (n + taps - 1) floats
+hipError_t launch_filtfilt(const float* h, long long taps, const float* x, float* y, long long n, long long nch,
+                           long long x_stride, long long y_stride, float* tmp, hipStream_t s);
 // overlap-save glue for filters beyond the fused kernels (N > 8192, four-step FFTs):
 // rows q < rows of pair p0 + q over (channel, pair) items, ppc pairs per channel,
 // row = z[e] = (x[2j*lout - le + e], x[(2j+1)*lout - le + e]) zero outside [0, n)

@@ -6,12 +6,15 @@
  *   vv_dsp_fir_apply_fft (:75-135)  -> overlap-save FFT convolution, zero state;
  *   vv_dsp_fir_apply     (:160-196) -> direct form in the reference's summation
  *                                      order (bit-identical), continuing from and
- *                                      updating the ring-buffer history. */
+ *                                      updating the ring-buffer history;
+ *   vv_dsp_filtfilt_fir  (filter/common.c:23-80) -> reflection-padded forward and
+ *                                      backward direct form, bit-identical. */
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "vv_dsp/vv_dsp_amd.h"
+#include "vv_dsp/filter/common.h"
 #include "vv_dsp/filter/fir.h"
 #include "vv_dsp_hip.h"
 
@@ -162,4 +165,25 @@ vv_dsp_status vv_dsp_fir_apply_direct_device(vv_dsp_fir_plan* p, const vv_dsp_re
                                              void* stream) {
     if (!p || !d_x || !d_y) return VV_DSP_ERROR_NULL_POINTER;
     return (vv_dsp_status)vvhip_fir_apply_device(p->dev, d_x, d_y, n, nch, x_stride, y_stride, NULL, 1, stream);
+}
+
+vv_dsp_status vv_dsp_filtfilt_fir_device(vv_dsp_fir_plan* p, const vv_dsp_real* d_x, vv_dsp_real* d_y, size_t n,
+                                         size_t nch, size_t x_stride, size_t y_stride, void* stream) {
+    if (!p || !d_x || !d_y) return VV_DSP_ERROR_NULL_POINTER;
+    return (vv_dsp_status)vvhip_fir_filtfilt_device(p->dev, d_x, d_y, n, nch, x_stride, y_stride, stream);
+}
+
+/* filter/common.c:23-80.  Argument checks in the reference's order; an empty
+ * signal is a no-op (the reference's reflection would read input[-1]). */
+vv_dsp_status vv_dsp_filtfilt_fir(const vv_dsp_real* coeffs, size_t num_taps, const vv_dsp_real* input,
+                                  vv_dsp_real* output, size_t num_samples) {
+    if (!coeffs || !input || !output) return VV_DSP_ERROR_NULL_POINTER;
+    if (num_taps == 0) return VV_DSP_ERROR_INVALID_SIZE;
+    if (num_samples == 0) return VV_DSP_OK;
+    vvhip_fir* f = NULL;
+    vv_dsp_status s = (vv_dsp_status)vvhip_fir_create(coeffs, num_taps, &f);
+    if (s != VV_DSP_OK) return s;
+    s = (vv_dsp_status)vvhip_fir_filtfilt_host(f, input, output, num_samples);
+    vvhip_fir_destroy(f);
+    return s;
 }

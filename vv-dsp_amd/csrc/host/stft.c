@@ -9,6 +9,7 @@
 
 #include "vv_dsp/vv_dsp_amd.h"
 #include "vv_dsp/spectral/stft.h"
+#include "vv_dsp/window.h"
 #include "vv_dsp_hip.h"
 
 struct vv_dsp_stft {
@@ -19,22 +20,14 @@ struct vv_dsp_stft {
     vvhip_stft* dev;
 };
 
-/* window.c:16-49 (boxcar / hann / hamming) */
+/* stft.c:21-28: the window by type (window.c:16-49 arithmetic, vv_dsp/window.h) */
 static vv_dsp_status make_window(vv_dsp_stft_window wt, size_t n, vv_dsp_real* w) {
-    if (wt == VV_DSP_STFT_WIN_BOXCAR) {
-        for (size_t i = 0; i < n; ++i) w[i] = 1.0f;
-        return VV_DSP_OK;
+    switch (wt) {
+        case VV_DSP_STFT_WIN_BOXCAR: return vv_dsp_window_boxcar(n, w);
+        case VV_DSP_STFT_WIN_HANN: return vv_dsp_window_hann(n, w);
+        case VV_DSP_STFT_WIN_HAMMING: return vv_dsp_window_hamming(n, w);
+        default: return VV_DSP_ERROR_OUT_OF_RANGE;
     }
-    if (wt != VV_DSP_STFT_WIN_HANN && wt != VV_DSP_STFT_WIN_HAMMING) return VV_DSP_ERROR_OUT_OF_RANGE;
-    if (n == 1) {
-        w[0] = 1.0f;
-        return VV_DSP_OK;
-    }
-    const vv_dsp_real a = (wt == VV_DSP_STFT_WIN_HANN) ? 0.5f : 0.54f;
-    const vv_dsp_real b = (wt == VV_DSP_STFT_WIN_HANN) ? 0.5f : 0.46f;
-    const vv_dsp_real step = (vv_dsp_real)(2.0 * 3.141592653589793238462643383279502884) / (vv_dsp_real)(n - 1);
-    for (size_t i = 0; i < n; ++i) w[i] = a - b * cosf(step * (vv_dsp_real)i);
-    return VV_DSP_OK;
 }
 
 vv_dsp_status vv_dsp_stft_create(const vv_dsp_stft_params* params, vv_dsp_stft** out) {

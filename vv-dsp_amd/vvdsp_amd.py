@@ -62,6 +62,7 @@ def lib():
     L.vv_dsp_fir_plan_destroy.argtypes = [_vp]
     L.vv_dsp_fir_apply_fft_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]
     L.vv_dsp_fir_apply_direct_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]
+    L.vv_dsp_filtfilt_fir_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp]
     L.vv_dsp_hilbert_analytic_device.argtypes = [_vp, _sz, _sz, _vp, _vp]
     L.vv_dsp_dct_make_plan.argtypes = [_sz, C.c_int, C.c_int, C.POINTER(_vp)]
     L.vv_dsp_dct_execute_device.argtypes = [_vp, _vp, _vp, _sz, _vp]
@@ -281,6 +282,20 @@ class FirPlan:
             out = torch.empty_like(x2)
         f = lib().vv_dsp_fir_apply_direct_device if direct else lib().vv_dsp_fir_apply_fft_device
         _check(f(self.h, _ptr(x2), _ptr(out), n, nch, x2.stride(0), out.stride(0), _stream(stream)), "fir_apply")
+        return out if x.dim() == 2 else out[0]
+
+    def filtfilt(self, x, out=None, stream=None):
+        """Zero-phase filtering (vv_dsp_filtfilt_fir, filter/common.c:23-80) of
+        x: (nch, n) float32 device tensor -> y (nch, n), bit-identical per row."""
+        x2 = x if x.dim() == 2 else x.unsqueeze(0)
+        nch, n = x2.shape
+        if x2.dtype != torch.float32 or x2.stride(1) != 1:
+            raise VvError("filtfilt input: float32 rows with unit sample stride")
+        if out is None:
+            out = torch.empty_like(x2)
+        _expect(out, torch.float32, nch * n, "filtfilt output")
+        _check(lib().vv_dsp_filtfilt_fir_device(self.h, _ptr(x2), _ptr(out), n, nch, x2.stride(0), out.stride(0),
+                                                _stream(stream)), "filtfilt_device")
         return out if x.dim() == 2 else out[0]
 
     def __del__(self):
