@@ -115,6 +115,16 @@ def case_fir(nch, n, taps=257):
     return (lambda: p(x, out=y)), 2 * nch * n * 4, (x, y, p)
 
 
+def case_fir_direct(nch, n, taps=257, filtfilt=False):
+    """bit-exact direct form (vv_dsp_fir_apply / vv_dsp_filtfilt_fir): bytes = one read + one write"""
+    h = lowpass(taps)
+    x = torch.rand(nch, n, device="cuda") * 2 - 1
+    y = torch.empty_like(x)
+    p = vv.FirPlan(h)
+    fn = (lambda: p.filtfilt(x, out=y)) if filtfilt else (lambda: p(x, out=y, direct=True))
+    return fn, 2 * nch * n * 4, (x, y, p)
+
+
 def case_mel(kind, frames=3599936):
     """log-mel (kind 0) / MFCC (kind 1) from power rows [frames][513] (40 mels, 13 coeffs)"""
     if "pw513" not in _SHARED:
@@ -382,6 +392,10 @@ CASES = {
     "stftc": lambda: case_stft(8, 600, complex_out=True),
     "stftcold": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_POW_OLD", "1"),
     "fir": lambda: case_fir(8, 1 << 24),
+    "firdirect": lambda: case_fir_direct(8, 1 << 24),
+    "firdirectlds": with_env(lambda: case_fir_direct(8, 1 << 24), "VVHIP_FIR_DIRECT_LDS", "1"),
+    "filtfilt": lambda: case_fir_direct(8, 1 << 24, filtfilt=True),
+    "filtfiltlds": with_env(lambda: case_fir_direct(8, 1 << 24, filtfilt=True), "VVHIP_FIR_DIRECT_LDS", "1"),
     "firspan": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_REG", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "hilbert1024": lambda: case_hilbert(1024, 65536),

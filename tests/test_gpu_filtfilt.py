@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("taps,n", [(9, 64), (1, 10), (2, 1), (5, 3), (33, 20), (257, 4000), (64, 1000),
-                                    (1000, 300), (4097, 9000), (257, 100003)])
+                                    (1000, 300), (4097, 9000), (257, 100003), (257, 100000), (15, 65536)])
 def test_filtfilt_bitexact(amd, ref, taps, n):
     rng = np.random.default_rng(taps * 7 + n)
     h = (rng.standard_normal(taps) * 0.2).astype(np.float32)
@@ -37,7 +37,7 @@ def test_filtfilt_empty_is_noop(amd):
     assert st == 0 and y.size == 0
 
 
-@pytest.mark.parametrize("nch,n,taps", [(3, 5000, 257), (2, 7, 33)])
+@pytest.mark.parametrize("nch,n,taps", [(3, 5000, 257), (2, 7, 33), (3, 20000, 257), (2, 40000, 16)])
 def test_filtfilt_device_batched(vdev, ref, nch, n, taps):
     import torch
     rng = np.random.default_rng(nch + n)

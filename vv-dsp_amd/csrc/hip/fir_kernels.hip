@@ -616,12 +616,167 @@ k_fir_direct(const float* __restrict__ h, long long taps, const float* __restric
     }
 }
 
+// ------------------------------------------------------------------------
+// Direct form from registers (k_fir_reg): the same sums in the same order,
+// without LDS.  A thread owns 16 consecutive outputs o0..o0+15 (a workgroup
+// 4096) and runs the taps in tiles of 16.  For tile u0 its window is
+// E[j] = s[o0 - u0 - 16 + j], j < 32, held as 24 register pairs
+// Q[j] = (E[j], E[j+8]), so that the products for outputs (r, r+8) at tap
+// u0+k are ONE packed multiply Q[16+r-k] * h[u0+k] (v_pk_mul_f32 with the tap
+// broadcast by op_sel) and the sums one packed add: 16 VALU per 16 MACs, every
+// product and sum separately rounded (the multiply is an asm statement, so no
+// FMA can form).  The next tile's window is the previous one shifted by 16:
+// eight pairs carry over, sixteen new samples come in (dwordx4 loads, L1/L2
+// hits).  Tiles touching the signal's edges load element by element through
+// the kernel's source rule (prefix / zeros / reflection), so results equal
+// k_fir_direct's bit for bit.
+// ------------------------------------------------------------------------
+constexpr int REG_OPT = 16;                 // outputs per thread
+constexpr int REG_TILE = 256 * REG_OPT;     // outputs per workgroup
+
+template <int SRC>
+__device__ __forceinline__ float fir_fetch(const float* xc, const float* pc, long long idx, long long n, long long lm1,
+                                           long long xn) {
+    if constexpr (SRC == 0) {
+        // the last tap tile's window reaches up to 15 samples before -lm1: those
+        // are never multiplied by a tap, and must not be read past the prefix
+        if (idx < 0) return (pc && idx >= -lm1) ? pc[lm1 + idx] : 0.0f;
+        return idx < n ? xc[idx] : 0.0f;
+    } else {
+        if (idx >= n) return 0.0f;
+        long long src;
+        if (idx < 0) src = (-idx < xn ? -idx : xn) - 1;
+        else if (idx < xn) src = idx;
+        else src = (idx - xn + 1 <= xn) ? 2 * xn - 1 - idx : 0;
+        return xc[src];
+    }
+}
+
+template <int SRC, bool REV>
+__global__ void __launch_bounds__(256)
+k_fir_reg(const float* __restrict__ h, long long taps, const float* __restrict__ x, float* __restrict__ y, long long n,
+          long long x_stride, long long y_stride, const float* __restrict__ prefix, long long prefix_stride,
+          long long xn, long long tiles_per_ch, int aligned) {
+    const long long c = blockIdx.x / tiles_per_ch;
+    const long long ob = (blockIdx.x % tiles_per_ch) * REG_TILE;
+    const long long o0 = ob + (long long)threadIdx.x * REG_OPT;
+    const long long lm1 = taps - 1;
+    const long long hi_ok = SRC == 1 ? (xn < n ? xn : n) : n;   // [0, hi_ok): plain loads
+    const float* xc = x + c * x_stride;
+    const float* pc = prefix ? prefix + c * prefix_stride : nullptr;
+    vf2_t acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = vf2_t{0.0f, 0.0f};
+    vf2_t Q[24];
+    // tile 0 window: E[j] = s[o0 - 16 + j], j < 32
+    {
+        float E[32];
+        const bool fast = aligned && ob - 16 >= 0 && ob + REG_TILE <= hi_ok;
+        if (fast) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const vf4_t v = *reinterpret_cast<const vf4_t*>(xc + o0 - 16 + 4 * q);
+                E[4 * q] = v.x; E[4 * q + 1] = v.y; E[4 * q + 2] = v.z; E[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) E[j] = fir_fetch<SRC>(xc, pc, o0 - 16 + j, n, lm1, xn);
+        }
+#pragma unroll
+        for (int j = 0; j < 24; ++j) Q[j] = vf2_t{E[j], E[j + 8]};
+    }
+    const long long full = taps / 16;
+    for (long long t = 0;; ++t) {
+        const long long u0 = 16 * t;
+        const int kn = t < full ? 16 : (int)(taps - u0);   // taps in this tile
+        vf2_t H[8];
+        if (kn == 16) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const vf4_t v = *reinterpret_cast<const vf4_t*>(h + u0 + 4 * q);
+                H[2 * q] = vf2_t{v.x, v.y};
+                H[2 * q + 1] = vf2_t{v.z, v.w};
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const vf2_t p = (k & 1) ? pk_mul_bcast<1>(Q[16 + r - k], H[k >> 1])
+                                            : pk_mul_bcast<0>(Q[16 + r - k], H[k >> 1]);
+                    acc[r] = acc[r] + p;
+                }
+            }
+        } else {   // the last, partial tile: exactly the remaining taps
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (k < kn) {
+                    const float hk = h[u0 + k];
+                    const vf2_t hh = vf2_t{hk, hk};
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) acc[r] = acc[r] + pk_mul_bcast<0>(Q[16 + r - k], hh);
+                }
+            }
+        }
+        if (u0 + 16 >= taps) break;
+        // next window: E'[j] = s[o0 - u0 - 32 + j]; Q'[16+j] = Q[j], Q'[8+j] = (N[8+j], E[j]), Q'[j] = (N[j], N[j+8])
+        float N[16];
+        const long long lo = ob - u0 - 32;
+        const bool fast = aligned && lo >= 0 && ob + REG_TILE - u0 - 16 <= hi_ok;
+        if (fast) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const vf4_t v = *reinterpret_cast<const vf4_t*>(xc + o0 - u0 - 32 + 4 * q);
+                N[4 * q] = v.x; N[4 * q + 1] = v.y; N[4 * q + 2] = v.z; N[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) N[j] = fir_fetch<SRC>(xc, pc, o0 - u0 - 32 + j, n, lm1, xn);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Q[16 + j] = Q[j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Q[8 + j] = vf2_t{N[8 + j], Q[16 + j].x};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Q[j] = vf2_t{N[j], N[j + 8]};
+    }
+    float* yc = y + c * y_stride;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const long long ia = o0 + r, ib = o0 + r + 8;
+        if (ia < n) yc[REV ? n - 1 - ia : ia] = acc[r].x;
+        if (ib < n) yc[REV ? n - 1 - ib : ib] = acc[r].y;
+    }
+}
+
+template <int SRC, bool REV>
+static hipError_t run_fir_reg(const float* h, long long taps, const float* x, float* y, long long n, long long nch,
+                              long long x_stride, long long y_stride, const float* prefix, long long prefix_stride,
+                              long long xn, hipStream_t s) {
+    const long long tiles = (n + REG_TILE - 1) / REG_TILE;
+    if (tiles * nch <= 0) return hipSuccess;
+    if (taps < 1 || tiles * nch > 0x7fffffffLL) return hipErrorInvalidValue;
+    // the 16 B tap loads need 16 B aligned taps; the fast sample loads 16 B
+    // aligned rows (a 4-float multiple stride)
+    if ((uintptr_t)h & 15) return hipErrorInvalidValue;
+    const int aligned = ((uintptr_t)x & 15) == 0 && (x_stride & 3) == 0;
+    hipLaunchKernelGGL((k_fir_reg<SRC, REV>), dim3((unsigned)(tiles * nch)), dim3(256), 0, s, h, taps, x, y, n,
+                       x_stride, y_stride, prefix, prefix_stride, xn, tiles, aligned);
+    return hipGetLastError();
+}
+
+static bool fir_reg_enabled() {
+    const char* e = getenv("VVHIP_FIR_DIRECT_LDS");   // A/B: 1 = the LDS kernel
+    return !(e && *e == '1');
+}
+
 hipError_t launch_fir_direct(const float* h, long long taps, const float* x, float* y, long long n,
                              long long nch, long long x_stride, long long y_stride,
                              const float* prefix, hipStream_t s) {
     const long long tiles = (n + DIRECT_TILE - 1) / DIRECT_TILE;
     if (tiles * nch <= 0) return hipSuccess;
     if (taps < 1 || tiles * nch > 0x7fffffffLL) return hipErrorInvalidValue;
+    if (fir_reg_enabled() && ((uintptr_t)h & 15) == 0)
+        return run_fir_reg<0, false>(h, taps, x, y, n, nch, x_stride, y_stride, prefix, taps - 1, n, s);
     hipLaunchKernelGGL((k_fir_direct<0, false>), dim3((unsigned)(tiles * nch)), dim3(256), 0, s, h, taps, x, y, n,
                        x_stride, y_stride, prefix, taps - 1, n, tiles);
     return hipGetLastError();
@@ -641,6 +796,11 @@ hipError_t launch_filtfilt(const float* h, long long taps, const float* x, float
     const long long t1 = (m + DIRECT_TILE - 1) / DIRECT_TILE, t2 = (n + DIRECT_TILE - 1) / DIRECT_TILE;
     if (n <= 0 || nch <= 0) return hipSuccess;
     if (taps < 1 || t1 * nch > 0x7fffffffLL) return hipErrorInvalidValue;
+    if (fir_reg_enabled() && ((uintptr_t)h & 15) == 0) {
+        hipError_t e = run_fir_reg<1, true>(h, taps, x, tmp, m, nch, x_stride, m, nullptr, 0, n, s);
+        if (e != hipSuccess) return e;
+        return run_fir_reg<0, true>(h, taps, tmp + pad, y, n, nch, m, y_stride, tmp, m, n, s);
+    }
     hipLaunchKernelGGL((k_fir_direct<1, true>), dim3((unsigned)(t1 * nch)), dim3(256), 0, s, h, taps, x, tmp, m,
                        x_stride, m, (const float*)nullptr, 0LL, n, t1);
     hipLaunchKernelGGL((k_fir_direct<0, true>), dim3((unsigned)(t2 * nch)), dim3(256), 0, s, h, taps,
