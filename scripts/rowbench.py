@@ -118,12 +118,13 @@ def main():
     del xr, X, p, pi
 
     # ---- a6: large power of two (four-step) and Bluestein -----------------------------
-    for n, B, label in ((1 << 20, 64, "fft_c2c_2^20"), (48000, 1024, "fft_c2c_48000_bluestein")):
+    for n, B, label in ((1 << 20, 64, "fft_c2c_2^20"), (48000, 1024, "fft_c2c_48000_mixed_fourstep"),
+                        (48001, 1024, "fft_c2c_48001_bluestein")):
         x = torch.complex(torch.rand(B, n, device="cuda") - 0.5, torch.rand(B, n, device="cuda") - 0.5)
         y = torch.empty_like(x)
         p = vv.FftPlan(n, vv.C2C, vv.FWD, batch=B)
         ms = gpu_time(lambda: p(x, out=y), a.reps)
-        if n == 48000:
+        if n in (48000, 48001):
             # the reference's O(n^2) DFT needs minutes at n = 48000: time it at n = 4800 and scale by n^2
             xh = (rng.random(4800) + 1j * rng.random(4800)).astype(np.complex64)
             c = cpu(lambda: ref.fft(xh, C2C, FWD), 1, budget=2.0)
@@ -135,10 +136,38 @@ def main():
                        16 * n * B, "transforms", c,
                        note="algorithmic bytes = one read + one write; the kernel chain moves "
                             + ("5x that (3 transposes, 2 FFT passes)" if n == 1 << 20 else
+                               "2x that (two mixed-radix passes, 200 x 240)" if n == 48000 else
                                "~5x that over the padded length (Bluestein)")
                             + "; the reference runs " + ("Kiss radix-2" if n == 1 << 20 else
                                                          "its O(n^2) DFT (timed at n = 4800, x100)")))
         del x, y, p
+
+    # ---- a6/a7: 7-smooth non-power-of-two lengths (mixed radix) -------------------------
+    for n in (400, 480, 1000, 3000):
+        B = (1 << 26) // n
+        x = torch.complex(torch.rand(B, n, device="cuda") - 0.5, torch.rand(B, n, device="cuda") - 0.5)
+        y = torch.empty_like(x)
+        p = vv.FftPlan(n, vv.C2C, vv.FWD, batch=B)
+        ms = gpu_time(lambda: p(x, out=y), a.reps)
+        xh = (rng.random(n) + 1j * rng.random(n)).astype(np.complex64)
+        out.append(row(f"fft_c2c_{n}_mixed", f"a6 vv_dsp_fft_execute C2C, n = {n} (mixed radix)",
+                       (f"{B} x {n} c2c fwd", B), ms, 16 * n * B, "transforms",
+                       cpu(lambda: ref.fft(xh, C2C, FWD), 1, budget=1.0),
+                       note="the reference runs its O(n^2) DFT (fft_kiss.c:76-92) for every non-power-of-two n"))
+        del x, y, p
+    torch.cuda.empty_cache()
+    st4 = vv.Stft(400, 160)
+    n = 600 * 16000
+    sig = torch.rand(32, n, device="cuda") * 2 - 1
+    fr = st4.frames(n)
+    o = torch.empty(32, fr, 400, device="cuda")
+    ms = gpu_time(lambda: st4.spectrogram(sig, out=o), a.reps)
+    sh = rng.uniform(-1, 1, 60 * 16000).astype(np.float32)
+    out.append(row("stft_mag_400_hop160_32ch", "a11 vv_dsp_stft_spectrogram, nfft 400 / hop 160 (mixed radix)",
+                   ("32 ch x 600 s at 16 kHz", 32 * fr), ms, 32 * n * 4 + 32 * fr * 1600, "frames",
+                   cpu(lambda: ref.spectrogram(sh, 400, 160), st4.frames(60 * 16000), budget=2.0)))
+    del sig, o, st4
+    torch.cuda.empty_cache()
 
     # ---- a9-a13: STFT magnitude / power / complex, ISTFT ------------------------------
     st = vv.Stft(1024, 256)
@@ -224,7 +253,13 @@ def main():
     ms = gpu_time(lambda: fp(xf, out=yf, direct=True), max(2, a.reps // 4))
     out.append(row("fir_direct_257_config4", "a19 vv_dsp_fir_apply (direct form, bit-exact)",
                    ("8 ch x 2^24", nch * n), ms, 8 * nch * n, "samples", cpu(lambda: ref.fir_apply(h, xs), 65536),
-                   note="compute-bound: 257 multiply-adds per sample in the reference's order, no FMA"))
+                   note="VALU-bound: 257 multiply-adds per sample in the reference's order, no FMA (k_fir_reg)"))
+    ms = gpu_time(lambda: fp.filtfilt(xf, out=yf), max(2, a.reps // 4))
+    xs2 = xs[:16384]
+    out.append(row("filtfilt_257_config4", "FIR caller vv_dsp_filtfilt_fir (common.c:23-80, bit-exact)",
+                   ("8 ch x 2^24", nch * n), ms, 8 * nch * n, "samples",
+                   cpu(lambda: ref.filtfilt(h, xs2), 16384),
+                   note="two direct-form passes over the reflection-padded signal"))
     del xf, yf, fp
 
     # ---- f4 (CZT, czt.c:44-178) and the cepstrum family (8b callers) ---------------------
