@@ -355,6 +355,9 @@ CASES = {
     "c2c2p17": lambda: case_c2c(1 << 17, 512),
     "c2c2p17old": with_env(lambda: case_c2c(1 << 17, 512), "VVHIP_FS_OLD", "1"),
     "c2c2p13": lambda: case_c2c(1 << 13, 8192),
+    "c2c2p13fs": with_env(lambda: case_c2c(1 << 13, 8192), "VVHIP_C2C_MAX", "4096"),
+    "c2c2p13b": lambda: case_c2c(1 << 13, 8192, fwd=False),
+    "r2c2p14": lambda: case_r2c(1 << 14, 4096),
     "c2c2p22": lambda: case_c2c(1 << 22, 16),
     "blue48000": lambda: case_c2c(48000, 1024),
     "blue48000nomix": with_env(lambda: case_c2c(48000, 1024), "VVHIP_NO_MIXED", "1"),
@@ -368,6 +371,7 @@ CASES = {
     **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
     "stft400": lambda: case_stft_n(32, 600, 400, 160),
     **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 1000)},
+    **{f"r2cmix{n}full": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_MIX_R2C_FULL", "1") for n in (400, 1000)},
     "stft480": lambda: case_stft_n(32, 600, 480, 120, sr=48000),
     "c2c4096": lambda: case_c2c(4096, 16384),
     "c2c256": lambda: case_c2c(256, 262144),

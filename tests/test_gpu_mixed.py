@@ -183,3 +183,15 @@ def test_mixed_fourstep_batched(vdev, monkeypatch, n, b, chunk_mb):
     monkeypatch.setenv("VVHIP_NO_MIXED", "1")
     yo = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xd).cpu().numpy()
     assert _nw(yf, yo) <= 4e-6
+
+
+@pytest.mark.parametrize("n", [400, 1000, 4800])
+def test_mixed_real_batch_invariant(vdev, amd, n):
+    """A row's R2C result does not depend on the batch it is computed in: the
+    batched device plan's rows equal single-row host calls bit for bit."""
+    import torch
+    rng = np.random.default_rng(n + 77)
+    x = (rng.random((5, n)) - 0.5).astype(np.float32)
+    X = vdev.FftPlan(n, vdev.R2C, vdev.FWD, batch=5)(torch.from_numpy(x).cuda()).cpu().numpy()
+    for i in (0, 3, 4):
+        np.testing.assert_array_equal(X[i], amd.fft(x[i], R2C))

@@ -17,6 +17,8 @@
 #include "fft_core.hpp"
 #include "vvhip_internal.hpp"
 
+#include <cstdlib>
+
 namespace vvh {
 
 // ------------------------------------------------------------------------
@@ -87,7 +89,14 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     return hipGetLastError();
 }
 
-bool c2c_supported(long long n) { return n >= 2 && n <= 4096 && (n & (n - 1)) == 0; }
+// 8192: one workgroup of 512 threads per transform, the transform in 70 KB of
+// LDS (gfx950 gives one workgroup up to 160 KB).  16384 would need 1024
+// threads at <= 128 VGPRs and spills: it stays on the two-pass four-step.
+bool c2c_supported(long long n) {
+    const char* e = getenv("VVHIP_C2C_MAX");   // A/B: 4096 sends 8192 to the two-pass four-step
+    const long long mx = e && *e ? atoll(e) : 8192;
+    return n >= 2 && n <= mx && n <= 8192 && (n & (n - 1)) == 0;
+}
 
 hipError_t launch_c2c(long long n, int fwd, const float2* in, float2* out, long long batch,
                       long long in_dist, long long out_dist, float scale, hipStream_t s) {
@@ -97,7 +106,7 @@ hipError_t launch_c2c(long long n, int fwd, const float2* in, float2* out, long 
                    : run_c2c<NN, false>(in, out, batch, in_dist, out_dist, scale, s);
     switch (n) {
         VVH_C2C(2) VVH_C2C(4) VVH_C2C(8) VVH_C2C(16) VVH_C2C(32) VVH_C2C(64) VVH_C2C(128)
-        VVH_C2C(256) VVH_C2C(512) VVH_C2C(1024) VVH_C2C(2048) VVH_C2C(4096)
+        VVH_C2C(256) VVH_C2C(512) VVH_C2C(1024) VVH_C2C(2048) VVH_C2C(4096) VVH_C2C(8192)
         default: return hipErrorInvalidValue;
     }
 #undef VVH_C2C

@@ -419,6 +419,8 @@ bool c2c_large_supported(long long n) { return n > 4096 && n <= (1LL << 24) && (
 hipError_t launch_c2c_large(long long n, int fwd, const float2* in, float2* out, long long batch, hipStream_t s) {
     if (!c2c_large_supported(n)) return hipErrorInvalidValue;
     if (batch <= 0) return hipSuccess;
+    if (c2c_supported(n))   // 8192: one pass in LDS (fft_kernels.hip)
+        return launch_c2c(n, fwd, in, out, batch, n, n, 1.0f / (float)n, s);
     int lg = 0;
     while ((1LL << lg) < n) ++lg;
     if (lg <= 20 && env_ll("VVHIP_FS_OLD", 0) == 0) return launch_c2c_twopass(n, lg, fwd, in, out, batch, s);

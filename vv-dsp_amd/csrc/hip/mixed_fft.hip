@@ -121,9 +121,9 @@ __device__ __forceinline__ void msync() {
 
 // Where a transform's points come from and go to.
 //   MODE 0: complex rows (nout bins out, scaled; the inverse by conjugation).
-//   MODE 4: real rows, two per complex transform (z = a + i b), nout bins of
-//           each row out through the split X_a = (Z[k] + conj Z[-k]) / 2,
-//           X_b = -i (Z[k] - conj Z[-k]) / 2.
+//   MODE 4: real rows (imaginary zero), nout bins out.
+//   MODE 5: real rows of length 2n through an n-point transform of
+//           z[m] = x[2m] + i x[2m+1] and the split step (nout <= n + 1 bins).
 //   MODE 1/2/3: STFT frames of a [ch][n] signal, frames (2j, 2j+1) of one
 //           channel per complex transform (frame f starts at sample f*hop, zero
 //           past the end, times the window: frame_gather's single rounded
@@ -138,6 +138,7 @@ struct MixIO {
     // STFT
     long long sig_n, ch_stride, frames, ppc, hop, out_ch_stride;
     const float* win;
+    const float2* twn;   // MODE 5: W_n^k, k < n (n = 2 * the transform length)
     int var;   // A/B switch (VVHIP_MIX_VAR)
 };
 
@@ -155,13 +156,9 @@ struct Row {
         if constexpr (MODE == 0) {
             cin = reinterpret_cast<const float2*>(io.in) + f * io.in_dist;
             ca = io.out + f * io.out_dist;
-        } else if constexpr (MODE == 4) {
-            const long long a = 2 * f;
-            has_b = a + 1 < io.rows;
-            ra = reinterpret_cast<const float*>(io.in) + a * io.in_dist;
-            rb = has_b ? ra + io.in_dist : ra;
-            ca = io.out + a * io.out_dist;
-            cb = ca + io.out_dist;
+        } else if constexpr (MODE == 4 || MODE == 5) {
+            ra = reinterpret_cast<const float*>(io.in) + f * io.in_dist;
+            ca = io.out + f * io.out_dist;
         } else {
             const long long c = f / io.ppc, fra = 2 * (f - c * io.ppc);
             has_b = fra + 1 < io.frames;
@@ -184,8 +181,9 @@ struct Row {
             const float2 x = cin[e];
             return make_float2(x.x, x.y * io.isign);
         } else if constexpr (MODE == 4) {
-            const float a = ra[e], b = rb[e];
-            return make_float2(a, has_b ? b : 0.0f);
+            return make_float2(ra[e], 0.0f);
+        } else if constexpr (MODE == 5) {   // z[m] = x[2m] + i x[2m+1]
+            return make_float2(ra[2 * e], ra[2 * e + 1]);
         } else {
             // past the signal's end a load reads the window instead (always
             // mapped) and the value is zeroed: no branch around the loads
@@ -198,20 +196,28 @@ struct Row {
     // all outputs of the transform in buf (natural order), lane-contiguous
     template <int T>
     __device__ __forceinline__ void emit(const MixIO& io, const float2* buf, int t, int n) const {
-        if constexpr (MODE == 0) {
+        if constexpr (MODE == 0 || MODE == 4) {
             const float sx = io.scale, sy = io.scale * io.isign;
             for (int e = t; e < io.nout; e += T) {
                 const float2 x = buf[e];
                 ca[e] = make_float2(x.x * sx, x.y * sy);
             }
+        } else if constexpr (MODE == 5) {
+            // real length 2n from the n-point transform of its even/odd pairs:
+            // X[k] = (Z[k] + conj Z[n-k])/2 + W_2n^k (-i (Z[k] - conj Z[n-k])/2), k <= n
+            for (int e = t; e < io.nout; e += T) {
+                const float2 A = buf[e < n ? e : 0], B = cconj(buf[e == 0 || e == n ? 0 : n - e]);
+                const float2 X = split_fwd(A, B, io.twn[e]);
+                ca[e] = make_float2(X.x * io.scale, X.y * io.scale);
+            }
         } else {
-            const int lim = (MODE == 4) ? (int)io.nout : (MODE == 3 ? n / 2 + 1 : n);
-            const float h = (MODE == 4) ? 0.5f * io.scale : 0.5f;
+            const int lim = MODE == 3 ? n / 2 + 1 : n;
+            const float h = 0.5f;
             for (int e = t; e < lim; e += T) {
                 const float2 z = buf[e], m = buf[e == 0 ? 0 : n - e];
                 const float2 xa = make_float2((z.x + m.x) * h, (z.y - m.y) * h);
                 const float2 xb = make_float2((z.y + m.y) * h, (m.x - z.x) * h);
-                if constexpr (MODE == 4 || MODE == 2) {
+                if constexpr (MODE == 2) {
                     ca[e] = xa;
                     if (has_b) cb[e] = xb;
                 } else if constexpr (MODE == 1) {
@@ -561,9 +567,21 @@ hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, f
     io.rows = batch;
     io.scale = scale;
     io.isign = fwd ? 1.0f : -1.0f;
-    if (real_in) {   // real rows in pairs (forward only: R2C)
-        if (!fwd || nout > n / 2 + 1) return hipErrorInvalidValue;
-        return run_mixed<4>(pl, io, (batch + 1) / 2, s);
+    // Real rows are not paired across the batch (unlike STFT frames), so a row's
+    // result does not depend on the batch it came in.  Even n with a plannable
+    // n/2 (forward, the R2C case): the n/2-point transform of the row's
+    // even/odd pairs and the split step (MODE 5, half the FFT work); otherwise
+    // the row with imaginary part zero (MODE 4).
+    if (real_in) {
+        MixedPlan ph;
+        const char* eh = getenv("VVHIP_MIX_R2C_FULL");   // A/B: 1 = MODE 4 for even n too
+        const bool half = fwd && n % 2 == 0 && nout <= n / 2 + 1 && !(eh && *eh == '1') && make_plan(n / 2, &ph);
+        if (half) {
+            io.twn = twiddle_table((int)n);
+            if (!io.twn) return hipErrorOutOfMemory;
+            return run_mixed<5>(ph, io, batch, s);
+        }
+        return run_mixed<4>(pl, io, batch, s);
     }
     return run_mixed<0>(pl, io, batch, s);
 }
