@@ -358,6 +358,12 @@ CASES = {
     "c2c2p13fs": with_env(lambda: case_c2c(1 << 13, 8192), "VVHIP_C2C_MAX", "4096"),
     "c2c2p13b": lambda: case_c2c(1 << 13, 8192, fwd=False),
     "r2c2p14": lambda: case_r2c(1 << 14, 4096),
+    "r2c2p14fs": with_env(lambda: case_r2c(1 << 14, 4096), "VVHIP_C2C_MAX", "4096"),
+    "c2r2p14": lambda: case_c2r(1 << 14, 4096),
+    "r2c2p16": lambda: case_r2c(1 << 16, 1024),
+    "r2c2p16old": with_env(lambda: case_r2c(1 << 16, 1024), "VVHIP_REAL_PROMOTE", "1"),
+    "c2r2p16": lambda: case_c2r(1 << 16, 1024),
+    "c2r2p16old": with_env(lambda: case_c2r(1 << 16, 1024), "VVHIP_REAL_PROMOTE", "1"),
     "c2c2p22": lambda: case_c2c(1 << 22, 16),
     "blue48000": lambda: case_c2c(48000, 1024),
     "blue48000nomix": with_env(lambda: case_c2c(48000, 1024), "VVHIP_NO_MIXED", "1"),

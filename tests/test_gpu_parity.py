@@ -98,7 +98,7 @@ def test_c2c_large_pow2(amd, n):
     assert _normwise(amd.fft(x, C2C, BWD), refb) <= max(4 * _normwise(scipy.fft.ifft(x), refb), 1e-6)
 
 
-@pytest.mark.parametrize("n", [16384, 1 << 18])
+@pytest.mark.parametrize("n", [16384, 32768, 1 << 18])
 def test_real_large_pow2(amd, n):
     import scipy.fft
     rng = np.random.default_rng(n + 7)
@@ -506,7 +506,7 @@ def test_golden_dct(amd, golden):
         np.testing.assert_allclose(xi, g["x"], rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 8, 40, 63, 64, 257, 400, 1000, 1024, 4800, 8192])
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 40, 63, 64, 257, 400, 1000, 1024, 4800, 8192, 16384])
 def test_dct_types_vs_formula(amd, n):
     import scipy.fft
     rng = np.random.default_rng(n)

@@ -282,7 +282,12 @@ static hipError_t run_c2r(const float2* in, float* out, long long batch, long lo
     return hipGetLastError();
 }
 
-bool r2c_supported(long long n) { return n >= 4 && n <= 8192 && (n & (n - 1)) == 0; }
+// real 16384: the 8192-point complex kernel geometry (512 threads, 70 KB of LDS)
+bool r2c_supported(long long n) {
+    const char* e = getenv("VVHIP_C2C_MAX");   // A/B: 4096 keeps real 16384 on the promote + four-step path
+    const long long mx = e && *e ? 2 * atoll(e) : 16384;
+    return n >= 4 && n <= mx && n <= 16384 && (n & (n - 1)) == 0;
+}
 
 #define VVH_REAL_SWITCH(CALL)                                                                   \
     switch (n / 2) {                                                                            \
@@ -290,6 +295,7 @@ bool r2c_supported(long long n) { return n >= 4 && n <= 8192 && (n & (n - 1)) ==
         case 16: return CALL(16); case 32: return CALL(32); case 64: return CALL(64);           \
         case 128: return CALL(128); case 256: return CALL(256); case 512: return CALL(512);     \
         case 1024: return CALL(1024); case 2048: return CALL(2048); case 4096: return CALL(4096); \
+        case 8192: return CALL(8192);                                                           \
         default: return hipErrorInvalidValue;                                                   \
     }
 
@@ -353,6 +359,78 @@ hipError_t launch_dft_naive(long long n, int fwd, const void* in, int real_in, f
     if (kblocks * batch <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_dft_naive, dim3((unsigned)(kblocks * batch)), dim3(256), 0, s, n, fwd, in,
                        real_in, out, nout, in_dist, out_dist, scale, tab, kblocks);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------
+// Real transforms above the fused kernels (pow2 n = 2M > 16384): the M-point
+// complex transform of z[m] = x[2m] + i x[2m+1] (the real rows reinterpreted,
+// no copy) and the split step, as k_r2c / k_c2r do in registers.  W_n^k from
+// the two-level table lo[k & mask] * hi[k >> lo_bits].
+// ------------------------------------------------------------------------
+__device__ __forceinline__ float2 tw_split_at(const float2* __restrict__ tab, long long k, int lo_bits) {
+    const long long mask = (1LL << lo_bits) - 1;
+    return cmul(tab[k & mask], tab[(1LL << lo_bits) + (k >> lo_bits)]);
+}
+
+// Z: [batch][M] -> X: [batch][M+1] (bins 0..n/2 of the real rows)
+__global__ void k_real_split_fwd(const float2* __restrict__ Z, float2* __restrict__ X, long long M, long long batch,
+                                 const float2* __restrict__ tab, int lo_bits) {
+    const long long nh = M + 1, total = nh * batch;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long f = i / nh, k = i - f * nh;
+        const float2* z = Z + f * M;
+        float2 x;
+        if (k == 0 || k == M) {   // DC and Nyquist (fft_kiss.c:141-143: imaginary part 0)
+            const float2 a = z[0];
+            x = make_float2(k == 0 ? a.x + a.y : a.x - a.y, 0.0f);
+        } else {
+            x = split_fwd(z[k], cconj(z[M - k]), tw_split_at(tab, k, lo_bits));
+        }
+        X[i] = x;
+    }
+}
+
+// X: [batch][M+1] -> V: [batch][M], the inverse split (imaginary parts of DC and
+// Nyquist ignored, the fft_kiss.c:158-171 result), before the M-point inverse
+__global__ void k_real_split_inv(const float2* __restrict__ X, float2* __restrict__ V, long long M, long long batch,
+                                 const float2* __restrict__ tab, int lo_bits) {
+    const long long total = M * batch;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long f = i / M, k = i - f * M;
+        const float2* x = X + f * (M + 1);
+        float2 A = x[k], B;
+        if (k == 0) {
+            A.y = 0.0f;
+            B = make_float2(x[M].x, 0.0f);
+        } else {
+            B = x[M - k];
+        }
+        V[i] = split_inv(A, B, tw_split_at(tab, k, lo_bits));
+    }
+}
+
+static unsigned grid_for(long long total) {
+    long long b = (total + 255) / 256;
+    return (unsigned)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
+}
+
+hipError_t launch_real_split_fwd(const float2* Z, float2* X, long long M, long long batch, hipStream_t s) {
+    int lo_bits = 0;
+    const float2* tab = twiddle_split(2 * M, &lo_bits);
+    if (!tab) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL(k_real_split_fwd, dim3(grid_for((M + 1) * batch)), dim3(256), 0, s, Z, X, M, batch, tab,
+                       lo_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_real_split_inv(const float2* X, float2* V, long long M, long long batch, hipStream_t s) {
+    int lo_bits = 0;
+    const float2* tab = twiddle_split(2 * M, &lo_bits);
+    if (!tab) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL(k_real_split_inv, dim3(grid_for(M * batch)), dim3(256), 0, s, X, V, M, batch, tab, lo_bits);
     return hipGetLastError();
 }
 

@@ -186,6 +186,10 @@ static size_t fft_out_elems_bytes(const vvhip_fft* p) {
 // exact-angle f64 O(n^2) kernel for short lengths and Bluestein over the
 // power-of-two kernels from BLUESTEIN_MIN on.  VVHIP_NO_MIXED=1 skips the
 // mixed-radix kernel (A/B and the tests that compare the two).
+static bool env_flag(const char* name) {
+    const char* e = getenv(name);
+    return e && *e == '1';
+}
 static bool use_mixed(long long n) {
     const char* e = getenv("VVHIP_NO_MIXED");
     return !(e && *e == '1') && mixed_supported(n);
@@ -235,6 +239,14 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
             HIPCHK(launch_r2c(N, (const float*)in, (float2*)out, B, N, NH, s), ST_INTERNAL);
             return ST_OK;
         }
+        if (is_pow2(n) && n > 8192 && c2c_large_supported(N / 2) && !env_flag("VVHIP_REAL_PROMOTE")) {
+            // the n/2-point C2C of the rows as complex pairs, then the split step
+            Scratch Z(s);
+            HIPCHK(Z.alloc(8 * (n / 2) * batch), ST_INTERNAL);
+            HIPCHK(launch_c2c_large(N / 2, 1, (const float2*)in, (float2*)Z.p, B, s), ST_INTERNAL);
+            HIPCHK(launch_real_split_fwd((const float2*)Z.p, (float2*)out, N / 2, B, s), ST_INTERNAL);
+            return ST_OK;
+        }
         if (is_pow2(n) && n > 8192) {   // promote, four-step C2C, keep bins 0..n/2 (fft_kiss.c:120-147)
             if (!c2c_large_supported(N)) return fail(ST_UNSUP, "R2C power-of-two length > 2^24 not supported");
             Scratch z(s), Z(s);
@@ -253,6 +265,14 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
     // C2R: cpx[n/2+1] -> real[n]
     if (r2c_supported(N)) {
         HIPCHK(launch_c2r(N, (const float2*)in, (float*)out, B, NH, N, s), ST_INTERNAL);
+        return ST_OK;
+    }
+    if (is_pow2(n) && n > 8192 && c2c_large_supported(N / 2) && !env_flag("VVHIP_REAL_PROMOTE")) {
+        // inverse split step, then the n/2-point inverse C2C straight into the real rows
+        Scratch V(s);
+        HIPCHK(V.alloc(8 * (n / 2) * batch), ST_INTERNAL);
+        HIPCHK(launch_real_split_inv((const float2*)in, (float2*)V.p, N / 2, B, s), ST_INTERNAL);
+        HIPCHK(launch_c2c_large(N / 2, 0, (const float2*)V.p, (float2*)out, B, s), ST_INTERNAL);
         return ST_OK;
     }
     if (is_pow2(n) && n > 8192 && !c2c_large_supported(N))
@@ -1126,7 +1146,7 @@ static int dct_run(const float* d_in, float* d_out, size_t n, size_t batch, int 
     }
     // Makhoul re-ordering + a real FFT: power-of-two n, and even 7-smooth n
     // through the mixed-radix kernels (odd n would need the other permutation)
-    const bool fast = (is_pow2(n) && n >= 4 && n <= 8192) || (n % 2 == 0 && n >= 4 && use_mixed(N));
+    const bool fast = (is_pow2(n) && n >= 4 && n <= 16384) || (n % 2 == 0 && n >= 4 && use_mixed(N));
     if (fast && type == 2 && dir > 0) {
         const float2* tw4n = twiddle_table((int)(4 * n));
         if (!tw4n) return fail(ST_INTERNAL, "dct twiddles");

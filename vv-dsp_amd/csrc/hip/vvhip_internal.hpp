@@ -39,6 +39,10 @@ hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, f
 hipError_t launch_stft_mixed(long long nfft, long long hop, int kind, const float* sig, long long n, long long nch,
                              long long ch_stride, long long frames, const float* win, void* out,
                              long long out_ch_stride, hipStream_t s);
+// Real pow2 n = 2M above the fused kernels: split steps around an M-point C2C
+// (fft_kernels.hip).  fwd: Z [batch][M] -> X [batch][M+1]; inv: X -> V [batch][M].
+hipError_t launch_real_split_fwd(const float2* Z, float2* X, long long M, long long batch, hipStream_t s);
+hipError_t launch_real_split_inv(const float2* X, float2* V, long long M, long long batch, hipStream_t s);
 // real[batch][n] -> complex[batch][n] (imaginary 0)
 hipError_t launch_promote_real(const float* in, float2* out, long long count, hipStream_t s);
 
