@@ -340,7 +340,8 @@ struct FsIO {
     long long in_dist, out_dist, nout, n;
     int N1, N2, real_in;
     float scale, isign;
-    const float2* twn;        // W_n, n entries
+    const float2* twn;        // W_n two-level: lo[m & (2^lo_bits - 1)] * hi[m >> lo_bits]
+    int lo_bits;
     long long groups_per_b;   // ceil(N2 / F) (columns) or ceil(N1 / F) (rows)
 };
 
@@ -394,7 +395,11 @@ k_fft_mixed_fs(MixedPlan pl, FsIO io, long long groups, const float2* __restrict
             float2* dst = io.mid + b * io.n;
             for (int idx = lt; idx < m * F; idx += 256) {
                 const int k1 = idx / F, sl = idx % F, col = i0 + sl;
-                if (col < N2) dst[(long long)k1 * N2 + col] = cmul(bufs[sl * m + k1], io.twn[col * k1]);
+                if (col < N2) {
+                    const int tw = col * k1;   // < n <= 2^24
+                    const float2 w = cmul(io.twn[tw & ((1 << io.lo_bits) - 1)], io.twn[(1 << io.lo_bits) + (tw >> io.lo_bits)]);
+                    dst[(long long)k1 * N2 + col] = cmul(bufs[sl * m + k1], w);
+                }
             }
         } else {
             float2* dst = io.out + b * io.out_dist;
@@ -518,7 +523,8 @@ static hipError_t launch_fft_mixed_fs(long long n, int fwd, const void* in, int 
     int n1, n2;
     MixedPlan p1, p2;
     if (!fs_split(n, &n1, &n2) || !make_plan(n1, &p1) || !make_plan(n2, &p2)) return hipErrorInvalidValue;
-    const float2* twn = twiddle_table((int)n);
+    int lo_bits = 0;
+    const float2* twn = twiddle_split(n, &lo_bits);   // sqrt(n)-sized, not an n-entry table
     if (!twn) return hipErrorOutOfMemory;
     const char* ec = getenv("VVHIP_MIX_CHUNK_MB");
     const long long cmb = ec ? atoll(ec) : 0;
@@ -538,6 +544,7 @@ static hipError_t launch_fft_mixed_fs(long long n, int fwd, const void* in, int 
     io.scale = scale;
     io.isign = fwd ? 1.0f : -1.0f;
     io.twn = twn;
+    io.lo_bits = lo_bits;
     io.in_dist = in_dist;
     io.out_dist = out_dist;
     for (long long c = 0; c < batch && e == hipSuccess; c += chunk) {

@@ -83,13 +83,13 @@ const double2* twiddle_table_d(long long n) {
 }
 
 // Two-level W_n^k for large n: lo[j] = W_n^j (j < 2^lo_bits), then
-// hi[j] = W_n^(j << lo_bits) (j < n >> lo_bits); W_n^k = lo[k & mask] * hi[k >> lo_bits].
+// hi[j] = W_n^(j << lo_bits) (j < ceil(n / 2^lo_bits)); W_n^k = lo[k & mask] * hi[k >> lo_bits].
 const float2* twiddle_split(long long n, int* lo_bits) {
     int lg = 0;
     while ((1LL << lg) < n) ++lg;
     const int lb = (lg + 1) / 2;
     *lo_bits = lb;
-    const long long nlo = 1LL << lb, nhi = n >> lb;
+    const long long nlo = 1LL << lb, nhi = (n + nlo - 1) >> lb;   // k < n for any n (not only powers of two)
     return (const float2*)cached(KIND_SPLIT, n, sizeof(float2) * (nlo + nhi), [=](unsigned char* b) {
         float2* h = reinterpret_cast<float2*>(b);
         double c, s;
