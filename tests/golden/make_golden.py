@@ -145,10 +145,68 @@ def main():
          c=c, iceps_kiss=ref.icepstrum_minphase(c), iceps_np64=np.real(np.fft.ifft(H)),
          minph_kiss=ref.minphase_from_cepstrum(c), minph_np64=H)
 
+    round2_sets(ref, man)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
     print("wrote", len(man), "golden sets")
 
 
+def filtfilt_f64(h, x):
+    """filter/common.c:6-80 in float64 (reflection pad of taps-1, direct form
+    forward, reverse, again, reverse, centre): the f64 counterpart of the
+    reference's float result."""
+    h = h.astype(np.float64)
+    x = x.astype(np.float64)
+    n, pad = len(x), len(h) - 1
+    left = [x[min(i + 1, n) - 1] for i in range(pad)][::-1]
+    right = [x[n - 1 - i if i + 1 <= n else 0] for i in range(pad)]
+    e = np.concatenate([np.array(left, np.float64), x, np.array(right, np.float64)])
+    t = np.convolve(e, h)[: len(e)][::-1]
+    t2 = np.convolve(t, h)[: len(e)][::-1]
+    return t2[pad: pad + n]
+
+
+def round2_sets(ref, man):
+    """Round-2 fixtures: zero-phase FIR (filter/common.c), 7-smooth non-power-of-two
+    FFT lengths (the reference's O(n^2) DFT, fft_kiss.c:76-92) and an STFT with
+    400-sample frames."""
+    h9 = ref.fir_design_lowpass(9, 0.25, 1)
+    xq = np.where(np.arange(64) % 8 < 4, 1.0, -1.0).astype(np.float32)
+    rng = np.random.default_rng(11)
+    h257 = ref.fir_design_lowpass(257, 0.25, FIRWIN_HANNING)
+    xg = rng.standard_normal(4096).astype(np.float32)
+    save("filtfilt", man, "vv_dsp_filtfilt_fir: 9-tap Hamming fc 0.25 on the filter_tests.c:62-80 square wave; "
+                          "257-tap Hann fc 0.25 on 4096 N(0,1) seed 11",
+         h9=h9, xq=xq, yq_kiss=ref.filtfilt(h9, xq)[1], yq_np64=filtfilt_f64(h9, xq),
+         h257=h257, xg=xg, yg_kiss=ref.filtfilt(h257, xg)[1], yg_np64=filtfilt_f64(h257, xg))
+    rng = np.random.default_rng(12)
+    x400 = (rng.random(400) - 0.5 + 1j * (rng.random(400) - 0.5)).astype(np.complex64)
+    xr480 = (rng.random(480) - 0.5).astype(np.float32)
+    save("fft_smooth_400_480", man, "c2c n = 400 (fwd, bwd) and r2c n = 480, uniform[-0.5,0.5) seed 12: the "
+                                    "reference's O(n^2) DFT and NumPy f64",
+         x=x400, c2c_fwd_kiss=ref.fft(x400, C2C, FWD), c2c_fwd_np64=np.fft.fft(x400.astype(np.complex128)),
+         c2c_bwd_kiss=ref.fft(x400, C2C, BWD), c2c_bwd_np64=np.fft.ifft(x400.astype(np.complex128)),
+         xr=xr480, r2c_kiss=ref.fft(xr480, R2C), r2c_np64=np.fft.rfft(xr480.astype(np.float64)))
+    rng = np.random.default_rng(13)
+    xs = rng.uniform(-1, 1, 16000).astype(np.float32)
+    mag = ref.spectrogram(xs, 400, 160)
+    w = 0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(399) * np.arange(400, dtype=np.float32))
+    pad = np.concatenate([xs.astype(np.float64), np.zeros(400)])
+    fr = mag.shape[0]
+    np_mag = np.abs(np.fft.fft(np.stack([pad[f * 160: f * 160 + 400] for f in range(fr)]) * w.astype(np.float64),
+                               axis=1))
+    save("stft_16000_n400_h160", man, "stft spectrogram 16000 samples uniform[-1,1) seed 13, 400/160 Hann "
+                                      "(non-power-of-two frames)",
+         x=xs, kiss=mag, np64=np_mag.astype(np.float64))
+
+
 if __name__ == "__main__":
-    main()
+    if "--round2-only" in sys.argv:   # add the round-2 sets without rewriting the others
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            m = json.load(f)
+        round2_sets(VvDsp(REF), m)
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(m, f, indent=1, sort_keys=True)
+        print("manifest now", len(m), "sets")
+    else:
+        main()

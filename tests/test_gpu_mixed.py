@@ -195,3 +195,23 @@ def test_mixed_real_batch_invariant(vdev, amd, n):
     X = vdev.FftPlan(n, vdev.R2C, vdev.FWD, batch=5)(torch.from_numpy(x).cuda()).cpu().numpy()
     for i in (0, 3, 4):
         np.testing.assert_array_equal(X[i], amd.fft(x[i], R2C))
+
+
+def test_round2_golden_gpu(amd, golden):
+    """The committed round-2 fixtures through the C ABI: 400-point c2c and
+    480-point r2c, and the 400/160 STFT, against NumPy f64 at the harness
+    tolerance (rtol = atol = 5e-5), and at least as close as the reference's own
+    O(n^2) f32 DFT; zero-phase FIR bit-identical to the reference."""
+    r, a = tolerances()
+    g = golden("fft_smooth_400_480")
+    for key, y in (("c2c_fwd", amd.fft(g["x"], C2C, FWD)), ("c2c_bwd", amd.fft(g["x"], C2C, BWD)),
+                   ("r2c", amd.fft(g["xr"], R2C))):
+        ref, kiss = g[key + "_np64"], g[key + "_kiss"]
+        np.testing.assert_allclose(y, ref, rtol=r, atol=a)
+        assert np.all(np.abs(y - ref) <= np.abs(kiss - ref) + a + r * np.abs(ref))
+    g = golden("stft_16000_n400_h160")
+    mag = amd.spectrogram(g["x"], 400, 160)
+    np.testing.assert_allclose(mag, g["np64"], rtol=r, atol=a)
+    g = golden("filtfilt")
+    assert np.array_equal(amd.filtfilt(g["h9"], g["xq"])[1], g["yq_kiss"])
+    assert np.array_equal(amd.filtfilt(g["h257"], g["xg"])[1], g["yg_kiss"])

@@ -291,3 +291,24 @@ def test_oracle_filtfilt_bitexact_vs_reference(orc, ref):
     x = np.where(np.arange(64) % 8 < 4, 1.0, -1.0).astype(np.float32)
     y = orc.filtfilt(h, x)
     assert abs(float(np.mean(y[9:55]))) < 0.2
+
+
+def test_oracle_round2_golden(orc, golden):
+    """Round-2 fixtures (tests/golden/make_golden.py round2_sets): the
+    restatement reproduces the reference's zero-phase FIR, its O(n^2) DFT at the
+    7-smooth lengths 400 / 480 and its STFT with 400-sample frames bit for bit,
+    and the float64 counterparts sit where the reference's own f32 arithmetic
+    puts them (filtfilt within 1e-5; the f32 DFT within 2e-3 at these sizes)."""
+    g = golden("filtfilt")
+    assert np.array_equal(orc.filtfilt(g["h9"], g["xq"]), g["yq_kiss"])
+    assert np.array_equal(orc.filtfilt(g["h257"], g["xg"]), g["yg_kiss"])
+    np.testing.assert_allclose(g["yq_kiss"], g["yq_np64"], atol=1e-5)
+    np.testing.assert_allclose(g["yg_kiss"], g["yg_np64"], atol=1e-5)
+    g = golden("fft_smooth_400_480")
+    assert np.array_equal(orc.fft(g["x"], C2C, FWD), g["c2c_fwd_kiss"])
+    assert np.array_equal(orc.fft(g["x"], C2C, BWD), g["c2c_bwd_kiss"])
+    assert np.array_equal(orc.fft(g["xr"], R2C), g["r2c_kiss"])
+    np.testing.assert_allclose(g["c2c_fwd_kiss"], g["c2c_fwd_np64"], atol=2e-3)
+    g = golden("stft_16000_n400_h160")
+    assert np.array_equal(orc.spectrogram(g["x"], 400, 160), g["kiss"])
+    np.testing.assert_allclose(g["kiss"], g["np64"], atol=2e-3)
