@@ -655,6 +655,16 @@ __device__ __forceinline__ void st16_nt_counted(vf4_t* p, vf4_t v) {
 __device__ __forceinline__ void st4_counted(float* p, float v) {
     asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
+// the same store from lane 0 alone (exec narrowed inside the asm, so it is
+// still exactly one counted instruction per wave and no other lane writes
+// anywhere: a shared dummy target would take every wave's 63 spare lanes)
+__device__ __forceinline__ void st4_lane0_counted(float* p, float v) {
+    unsigned long long keep;
+    asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, 1\n\tglobal_store_dword %1, %2, off\n\ts_mov_b64 exec, %0"
+                 : "=&s"(keep)
+                 : "v"(p), "v"(v)
+                 : "memory");
+}
 // dword streaming store at wave-uniform base (SGPR pair) + 32-bit lane offset + IMM
 // (13-bit signed immediate: -4096..4095)
 template <int IMM>

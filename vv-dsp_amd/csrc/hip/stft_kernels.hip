@@ -253,12 +253,11 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
             row(eb, sb, rb);
         }
         if constexpr (MODE == 2) {
-            // bin N/2 = NB * (R/2): even slot j = 0, r = R/2, lane 0; the
-            // other lanes' copies go to the sink (one store per row, counted)
+            // bin N/2 = NB * (R/2): even slot j = 0, r = R/2, lane 0 (one
+            // lane-0 store per row, counted; rb is the sink for a missing frame)
             static_assert(N / 2 == NB * (R / 2), "Nyquist bin in lane 0 of an even block");
-            float* const sk = sink + 8192 + t;
-            st4_counted(t == 0 ? (float*)ra + N / 2 : sk, ea[0][R / 2]);
-            st4_counted(t == 0 ? (float*)rb + N / 2 : sk, eb[0][R / 2]);
+            st4_lane0_counted((float*)ra + N / 2, ea[0][R / 2]);
+            st4_lane0_counted((float*)rb + N / 2, eb[0][R / 2]);
         }
     }
 }
