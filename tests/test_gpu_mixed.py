@@ -106,7 +106,8 @@ def test_stft_smooth_nfft(amd, orc, nfft, hop):
     assert np.all(np.abs(mag - np_mag) <= np.abs(ref - np_mag) + a + r * np_mag)
 
 
-@pytest.mark.parametrize("nfft,hop,nch,n", [(400, 160, 3, 16000), (480, 120, 2, 4801), (2000, 500, 2, 1999),
+@pytest.mark.parametrize("nfft,hop,nch,n", [(400, 160, 3, 16000), (400, 160, 5, 4481), (480, 120, 2, 4801),
+                                           (960, 240, 2, 9601), (960, 480, 3, 900), (2000, 500, 2, 1999),
                                            (45, 45, 1, 1000), (7, 3, 2, 50)])
 def test_stft_smooth_device_kinds(vdev, nfft, hop, nch, n):
     """Multi-channel device STFT at smooth nfft, all three row kinds (magnitude,
@@ -215,3 +216,27 @@ def test_round2_golden_gpu(amd, golden):
     g = golden("filtfilt")
     assert np.array_equal(amd.filtfilt(g["h9"], g["xq"])[1], g["yq_kiss"])
     assert np.array_equal(amd.filtfilt(g["h257"], g["xg"])[1], g["yg_kiss"])
+
+
+@pytest.mark.parametrize("nfft,hop,nch,n", [(400, 160, 4, 48000), (480, 160, 3, 20011), (960, 320, 2, 30001)])
+def test_stft_speech_register_kernel_vs_generic(vdev, monkeypatch, nfft, hop, nch, n):
+    """The two-pass register kernel for 400 / 480 / 960-point frames
+    (k_stft_sq) against the generic mixed-radix kernel (VVHIP_STFT_SQ=0, read
+    per call) on the same device input: all three row kinds, within f32
+    rounding of each other."""
+    import torch
+    rng = np.random.default_rng(nfft * 7 + n)
+    xd = torch.from_numpy(rng.uniform(-1, 1, (nch, n)).astype(np.float32)).cuda()
+    st = vdev.Stft(nfft, hop)
+
+    def rows():
+        return (st.spectrogram(xd).cpu().numpy(), st.spectrogram(xd, complex_out=True).cpu().numpy(),
+                st.power(xd).cpu().numpy())
+
+    fast = rows()
+    monkeypatch.setenv("VVHIP_STFT_SQ", "0")
+    gen = rows()
+    for f, g in zip(fast, gen):
+        assert f.shape == g.shape
+        scale = np.abs(g).max()
+        assert np.abs(f - g).max() <= 2e-6 * scale

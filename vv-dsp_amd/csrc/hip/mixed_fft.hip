@@ -417,6 +417,236 @@ k_fft_mixed_fs(MixedPlan pl, FsIO io, long long groups, const float2* __restrict
     }
 }
 
+// ------------------------------------------------------------------------
+// STFT frames of n = N1 * N2 (both <= 32) in registers: the speech lengths
+// 400 = 20 x 20, 480 = 20 x 24, 960 = 30 x 32.  The generic kernel above runs
+// a runtime radix plan through LDS with a barrier per pass and is bound by
+// that (400-point STFT: 0.31 of the HBM roofline); here a transform (a frame
+// pair, as MODE 1-3 above) is owned by max(N1, N2) lanes of one wave and
+// takes two register passes with one LDS exchange:
+//   pass 1, lane m2 < N2:  N1-point DFT of x[m1 N2 + m2] over m1, times W_n^(m2 k1)
+//   pass 2, lane k1 < N1:  N2-point DFT over m2 -> X[k1 + N1 k2]
+// The N-point DFTs are composed at compile time (R = A x B, constant
+// twiddles), the W_n factors come from the n-entry table in LDS.  Results go
+// back to LDS in natural order and the wave writes its pairs' rows as one
+// contiguous run (rows a and b of consecutive pairs are adjacent).
+// ------------------------------------------------------------------------
+constexpr double cx_pi = 3.14159265358979323846264338327950288;
+// cos / sin(2 pi j / R) in double at compile time (Taylor series on [-pi, pi])
+constexpr double cx_cos2pi(int j, int R) {
+    j %= R;
+    double x = 2.0 * cx_pi * (double)j / (double)R;
+    if (2 * j > R) x -= 2.0 * cx_pi;
+    double term = 1.0, sum = 1.0;
+    for (int i = 1; i < 24; ++i) {
+        term *= -x * x / ((2.0 * i - 1.0) * (2.0 * i));
+        sum += term;
+    }
+    return sum;
+}
+constexpr double cx_sin2pi(int j, int R) {
+    j %= R;
+    double x = 2.0 * cx_pi * (double)j / (double)R;
+    if (2 * j > R) x -= 2.0 * cx_pi;
+    double term = x, sum = x;
+    for (int i = 1; i < 24; ++i) {
+        term *= -x * x / ((2.0 * i) * (2.0 * i + 1.0));
+        sum += term;
+    }
+    return sum;
+}
+
+// v * W_R^J (forward, W_R = exp(-2 pi i / R)); quarter and half turns exact
+template <int J, int R>
+__device__ __forceinline__ float2 twk(float2 v) {
+    constexpr int m = J % R;
+    if constexpr (m == 0) {
+        return v;
+    } else if constexpr (2 * m == R) {
+        return upk(-pk(v));
+    } else if constexpr (4 * m == R) {
+        return cmul_mi(v);
+    } else if constexpr (4 * m == 3 * R) {
+        return cmul_pi(v);
+    } else {
+        constexpr float c = (float)cx_cos2pi(m, R), s = (float)-cx_sin2pi(m, R);
+        return cmul(v, make_float2(c, s));
+    }
+}
+
+template <int R>
+struct RegFac {   // R = A * B for the composite DFT (A = 1: a base case)
+    static constexpr bool BASE = R == 1 || R == 2 || R == 3 || R == 4 || R == 5 || R == 7 || R == 8 || R == 16;
+    static constexpr int A = BASE ? 1 : R % 8 == 0 ? 8 : R % 4 == 0 ? 4 : R % 2 == 0 ? 2 : R % 3 == 0 ? 3 : R % 5 == 0 ? 5 : 7;
+    static constexpr int B = BASE ? R : R / A;
+};
+
+// forward DFT of length R on registers, natural order in and out
+template <int R>
+__device__ __forceinline__ void reg_dft(float2* v) {
+    if constexpr (RegFac<R>::BASE) {
+        if constexpr (R == 1) {
+        } else if constexpr (R == 2 || R == 4 || R == 8 || R == 16) {
+            Dft<R, true>::run(v);
+        } else {
+            odd_dft<R>(v);
+        }
+    } else {
+        constexpr int A = RegFac<R>::A, B = RegFac<R>::B;
+        float2 y[A][B];
+        static_for<0, B>([&](auto m2c) {
+            constexpr int m2 = decltype(m2c)::value;
+            float2 col[A];
+#pragma unroll
+            for (int m1 = 0; m1 < A; ++m1) col[m1] = v[m1 * B + m2];
+            reg_dft<A>(col);
+            static_for<0, A>([&](auto k1c) {
+                constexpr int k1 = decltype(k1c)::value;
+                y[k1][m2] = twk<k1 * m2, R>(col[k1]);
+            });
+        });
+#pragma unroll
+        for (int k1 = 0; k1 < A; ++k1) {
+            reg_dft<B>(y[k1]);
+#pragma unroll
+            for (int k2 = 0; k2 < B; ++k2) v[k1 + A * k2] = y[k1][k2];
+        }
+    }
+}
+
+template <int N1, int N2>
+struct Sq {
+    static constexpr int N = N1 * N2;
+    static constexpr int TT = N1 > N2 ? N1 : N2;   // lanes per transform
+    static constexpr int TPW = 64 / TT;            // transforms per wave
+    static constexpr int P2 = N2 + 1;              // padded pass-1 row (k1 rows of N2)
+    static constexpr int LT = N1 * P2 > N ? N1 * P2 : N;   // float2 per transform
+    static constexpr int LDS = 4 * TPW * LT + N + N / 2;   // + the W_n table and the window
+    // workgroups per CU the LDS allows, at most 3 (<= 168 VGPRs without spills;
+    // 4 would need <= 128 and spills): latency-bound, so occupancy matters
+    static constexpr int FIT = (160 * 1024) / (8 * LDS);
+    static constexpr int LB = FIT < 3 ? (FIT < 1 ? 1 : FIT) : 3;
+};
+
+// MODE 1 |X| rows, 2 complex rows, 3 |X|^2 for bins 0..n/2 (as k_fft_mixed)
+template <int N1, int N2, int MODE>
+__global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, long long pairs, const float2* __restrict__ gtab) {
+    using S = Sq<N1, N2>;
+    constexpr int n = S::N, TT = S::TT, TPW = S::TPW, P2 = S::P2, LT = S::LT;
+    constexpr int W = MODE == 3 ? n / 2 + 1 : n;   // bins per row
+    __shared__ float2 sm[S::LDS];
+    float2* const tab = sm + 4 * TPW * LT;
+    float* const lwin = reinterpret_cast<float*>(tab + n);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        tab[i] = gtab[i];
+        lwin[i] = io.win[i];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slot = lane / TT, t = lane - slot * TT;
+    const bool lane_ok = slot < TPW;
+    float2* const wbuf = sm + wave * TPW * LT;
+    float2* const L = wbuf + (lane_ok ? slot : 0) * LT;
+    __syncthreads();
+    const long long step = (long long)gridDim.x * 4 * TPW;
+    for (long long g = ((long long)blockIdx.x * 4 + wave) * TPW; g < pairs; g += step) {
+        // pass 1: lane t < N2 of slot `slot` on pair g + slot
+        {
+            const long long q = g + slot;
+            if (lane_ok && q < pairs && t < N2) {
+                const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
+                const long long st = fra * io.hop;
+                const float* ra = reinterpret_cast<const float*>(io.in) + c * io.ch_stride + st;
+                const float* rb = ra + io.hop;
+                const long long lima = io.sig_n - st;
+                const long long limb = fra + 1 < io.frames ? lima - io.hop : 0;
+                float2 v[N1];
+                if (limb >= n) {   // both frames inside the signal: base + immediate loads
+                    const float* pa = ra + t;
+                    const float* pb = rb + t;
+#pragma unroll
+                    for (int m1 = 0; m1 < N1; ++m1) {
+                        const float w = lwin[m1 * N2 + t];
+                        v[m1] = make_float2(pa[m1 * N2] * w, pb[m1 * N2] * w);
+                    }
+                } else {
+#pragma unroll
+                    for (int m1 = 0; m1 < N1; ++m1) {
+                        const int s = m1 * N2 + t;
+                        // past the end a load reads the window (always mapped), zeroed
+                        const bool ia = s < lima, ib = s < limb;
+                        const float a = *(ia ? ra + s : io.win + s), b = *(ib ? rb + s : io.win + s);
+                        const float w = lwin[s];
+                        v[m1] = make_float2((ia ? a : 0.0f) * w, (ib ? b : 0.0f) * w);
+                    }
+                }
+                reg_dft<N1>(v);
+#pragma unroll
+                for (int k1 = 0; k1 < N1; ++k1) L[k1 * P2 + t] = k1 == 0 ? v[0] : cmul(v[k1], tab[k1 * t]);
+            }
+        }
+        xsync<64>();
+        // pass 2: lane t < N1 on row k1 = t
+        if (lane_ok && g + slot < pairs && t < N1) {
+            float2 u[N2];
+#pragma unroll
+            for (int m2 = 0; m2 < N2; ++m2) u[m2] = L[t * P2 + m2];
+            reg_dft<N2>(u);
+#pragma unroll
+            for (int k2 = 0; k2 < N2; ++k2) L[t + N1 * k2] = u[k2];
+        }
+        xsync<64>();
+        // rows a and b of each of the wave's pairs: 2W adjacent bins, the whole wave on each
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            const long long q = g + s;
+            if (q >= pairs) break;   // wave-uniform
+            const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
+            const int lim = fra + 1 < io.frames ? 2 * W : W;
+            const long long bs = c * io.out_ch_stride + fra * W;
+            const float2* X = wbuf + s * LT;
+#pragma unroll 4
+            for (int o = lane; o < 2 * W; o += 64) {
+                if (o < lim) {
+                    const bool isb = o >= W;
+                    const int e = isb ? o - W : o;
+                    const float2 z = X[e], m = X[e == 0 ? 0 : n - e];
+                    const float h = 0.5f;
+                    const float2 x = isb ? make_float2((z.y + m.y) * h, (m.x - z.x) * h)
+                                         : make_float2((z.x + m.x) * h, (z.y - m.y) * h);
+                    if constexpr (MODE == 2) {
+                        io.out[bs + o] = x;
+                    } else {
+                        float* fo = reinterpret_cast<float*>(io.out) + bs + o;
+                        if constexpr (MODE == 1) *fo = __builtin_amdgcn_sqrtf(__builtin_fmaf(x.x, x.x, x.y * x.y));
+                        else *fo = __builtin_fmaf(x.x, x.x, x.y * x.y);
+                    }
+                }
+            }
+        }
+        xsync<64>();   // the next group's pass 1 overwrites the buffers
+    }
+}
+
+template <int N1, int N2, int MODE>
+hipError_t run_stft_sq(const MixIO& io, long long pairs, hipStream_t s) {
+    const float2* tab = twiddle_table(N1 * N2);
+    if (!tab) return hipErrorOutOfMemory;
+    constexpr int TPW = Sq<N1, N2>::TPW;
+    const long long work = (pairs + 4 * TPW - 1) / (4 * TPW);
+    const int grid = persistent_grid((const void*)k_stft_sq<N1, N2, MODE>, 256, 0, work);
+    hipLaunchKernelGGL((k_stft_sq<N1, N2, MODE>), dim3(grid), dim3(256), 0, s, io, pairs, tab);
+    return hipGetLastError();
+}
+
+template <int N1, int N2>
+hipError_t run_stft_sq_kind(int kind, const MixIO& io, long long pairs, hipStream_t s) {
+    switch (kind) {
+        case 0: return run_stft_sq<N1, N2, 1>(io, pairs, s);
+        case 1: return run_stft_sq<N1, N2, 2>(io, pairs, s);
+        default: return run_stft_sq<N1, N2, 3>(io, pairs, s);
+    }
+}
+
 // radices largest first: 8s, then a 4 or 2, then 7, 5, 3
 bool make_plan(long long n, MixedPlan* pl) {
     if (n < 2 || n > MIX_MAXN) return false;
@@ -611,6 +841,13 @@ hipError_t launch_stft_mixed(long long nfft, long long hop, int kind, const floa
     io.hop = hop;
     io.out_ch_stride = out_ch_stride;
     io.win = win;
+    // speech lengths: the two-pass register kernel (VVHIP_STFT_SQ=0: the generic one, A/B)
+    const char* esq = getenv("VVHIP_STFT_SQ");
+    if (!(esq && *esq == '0')) {
+        if (nfft == 400) return run_stft_sq_kind<20, 20>(kind, io, batch, s);
+        if (nfft == 480) return run_stft_sq_kind<20, 24>(kind, io, batch, s);
+        if (nfft == 960) return run_stft_sq_kind<30, 32>(kind, io, batch, s);
+    }
     switch (kind) {
         case 0: return run_mixed<1>(pl, io, batch, s);
         case 1: return run_mixed<2>(pl, io, batch, s);
