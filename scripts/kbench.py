@@ -379,6 +379,8 @@ CASES = {
     **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 1000)},
     **{f"r2cmix{n}full": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_MIX_R2C_FULL", "1") for n in (400, 1000)},
     "stft480": lambda: case_stft_n(32, 600, 480, 120, sr=48000),
+    **{f"mix{n}gen": with_env(lambda n=n: case_c2c(n, (1 << 26) // n), "VVHIP_STFT_SQ", "0") for n in (400, 480, 960)},
+    "mix960": lambda: case_c2c(960, (1 << 26) // 960),
     "stft960": lambda: case_stft_n(32, 600, 960, 240, sr=48000),
     # *gen: the generic mixed-radix kernel instead of the two-pass register one
     **{f"stft{nf}gen": with_env(lambda nf=nf, h=h, sr=sr: case_stft_n(32, 600, nf, h, sr=sr), "VVHIP_STFT_SQ", "0")
