@@ -376,7 +376,8 @@ CASES = {
     **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
     **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
     "stft400": lambda: case_stft_n(32, 600, 400, 160),
-    **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 1000)},
+    **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 960, 1000)},
+    **{f"r2cmix{n}gen": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_STFT_SQ", "0") for n in (400, 960)},
     **{f"r2cmix{n}full": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_MIX_R2C_FULL", "1") for n in (400, 1000)},
     "stft480": lambda: case_stft_n(32, 600, 480, 120, sr=48000),
     **{f"mix{n}gen": with_env(lambda n=n: case_c2c(n, (1 << 26) // n), "VVHIP_STFT_SQ", "0") for n in (400, 480, 960)},

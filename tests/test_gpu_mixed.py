@@ -263,3 +263,23 @@ def test_c2c_register_kernel_vs_generic(vdev, monkeypatch, n, b, fwd):
     assert np.abs(fast - ref).max() <= 2e-6 * scale * np.sqrt(n)
     assert np.abs(fast - gen).max() <= 2e-6 * scale * np.sqrt(n)
     np.testing.assert_array_equal(inplace.cpu().numpy(), fast)
+
+
+@pytest.mark.parametrize("n,b", [(400, 1001), (480, 3), (960, 77)])
+def test_r2c_register_kernel_vs_generic(vdev, monkeypatch, n, b):
+    """Real rows of 400 / 480 / 960 (the n/2-point transform of even/odd pairs
+    plus the split step) through the register kernel against the generic
+    mixed-radix kernel (VVHIP_STFT_SQ=0) and NumPy f64."""
+    import torch
+    rng = np.random.default_rng(3 * n + b)
+    x = rng.uniform(-1, 1, (b, n)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    plan = vdev.FftPlan(n, vdev.R2C, vdev.FWD, batch=b)
+    fast = plan(xd).cpu().numpy()
+    monkeypatch.setenv("VVHIP_STFT_SQ", "0")
+    gen = plan(xd).cpu().numpy()
+    ref = np.fft.rfft(x.astype(np.float64), axis=1)
+    scale = np.abs(ref).max()
+    assert fast.shape == ref.shape
+    assert np.abs(fast - ref).max() <= 2e-6 * scale * np.sqrt(n)
+    assert np.abs(fast - gen).max() <= 2e-6 * scale * np.sqrt(n)

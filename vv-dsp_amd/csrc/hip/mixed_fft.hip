@@ -528,7 +528,8 @@ struct Sq {
     static constexpr int LB = FIT < 3 ? (FIT < 1 ? 1 : FIT) : 3;
 };
 
-// MODE 0 c2c rows (`pairs` = rows); STFT frame pairs: MODE 1 |X| rows, 2 complex
+// MODE 0 c2c rows (`pairs` = rows), MODE 5 real rows of 2n (even/odd pairs
+// + split step, as k_fft_mixed); STFT frame pairs: MODE 1 |X| rows, 2 complex
 // rows, 3 |X|^2 for bins 0..n/2 (as k_fft_mixed).  A wave reads its rows whole
 // before it writes them, so in == out is safe.
 template <int N1, int N2, int MODE>
@@ -541,7 +542,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, lon
     float* const lwin = reinterpret_cast<float*>(tab + n);
     for (int i = threadIdx.x; i < n; i += 256) {
         tab[i] = gtab[i];
-        if constexpr (MODE != 0) lwin[i] = io.win[i];
+        if constexpr (MODE != 0 && MODE != 5) lwin[i] = io.win[i];
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / TT, t = lane - slot * TT;
@@ -554,18 +555,24 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, lon
         // pass 1: lane t < N2 of slot `slot` on pair g + slot
         {
             const long long q = g + slot;
-            if (MODE == 0 && lane_ok && q < pairs && t < N2) {   // complex row q (the inverse by conjugation)
-                const float2* x = reinterpret_cast<const float2*>(io.in) + q * io.in_dist + t;
+            if ((MODE == 0 || MODE == 5) && lane_ok && q < pairs && t < N2) {
                 float2 v[N1];
+                if constexpr (MODE == 0) {   // complex row q (the inverse by conjugation)
+                    const float2* x = reinterpret_cast<const float2*>(io.in) + q * io.in_dist + t;
 #pragma unroll
-                for (int m1 = 0; m1 < N1; ++m1) {
-                    const float2 a = x[m1 * N2];
-                    v[m1] = make_float2(a.x, a.y * io.isign);
+                    for (int m1 = 0; m1 < N1; ++m1) {
+                        const float2 a = x[m1 * N2];
+                        v[m1] = make_float2(a.x, a.y * io.isign);
+                    }
+                } else {   // real row q of length 2n: z[m] = x[2m] + i x[2m+1]
+                    const float* x = reinterpret_cast<const float*>(io.in) + q * io.in_dist + 2 * t;
+#pragma unroll
+                    for (int m1 = 0; m1 < N1; ++m1) v[m1] = make_float2(x[2 * m1 * N2], x[2 * m1 * N2 + 1]);
                 }
                 reg_dft<N1>(v);
 #pragma unroll
                 for (int k1 = 0; k1 < N1; ++k1) L[k1 * P2 + t] = k1 == 0 ? v[0] : cmul(v[k1], tab[k1 * t]);
-            } else if (MODE != 0 && lane_ok && q < pairs && t < N2) {
+            } else if (MODE != 0 && MODE != 5 && lane_ok && q < pairs && t < N2) {
                 const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
                 const long long st = fra * io.hop;
                 const float* ra = reinterpret_cast<const float*>(io.in) + c * io.ch_stride + st;
@@ -608,6 +615,20 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, lon
             for (int k2 = 0; k2 < N2; ++k2) L[t + N1 * k2] = u[k2];
         }
         xsync<64>();
+        if constexpr (MODE == 5) {   // split step: X[k] = (Z[k] + conj Z[n-k])/2 + W_2n^k (-i (Z[k] - conj Z[n-k])/2)
+#pragma unroll
+            for (int s = 0; s < TPW; ++s) {
+                const long long q = g + s;
+                if (q >= pairs) break;   // wave-uniform
+                const float2* X = wbuf + s * LT;
+                float2* y = io.out + q * io.out_dist;
+                for (int e = lane; e < io.nout; e += 64) {
+                    const float2 A = X[e < n ? e : 0], B = cconj(X[e == 0 || e == n ? 0 : n - e]);
+                    const float2 Y = split_fwd(A, B, io.twn[e]);
+                    y[e] = make_float2(Y.x * io.scale, Y.y * io.scale);
+                }
+            }
+        }
         if constexpr (MODE == 0) {   // the wave's rows, scaled (and conjugated back for the inverse)
             const float sx = io.scale, sy = io.scale * io.isign;
 #pragma unroll
@@ -624,7 +645,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, lon
         }
         // rows a and b of each of the wave's pairs: 2W adjacent bins, the whole wave on each
 #pragma unroll
-        for (int s = 0; s < (MODE == 0 ? 0 : TPW); ++s) {
+        for (int s = 0; s < (MODE == 0 || MODE == 5 ? 0 : TPW); ++s) {
             const long long q = g + s;
             if (q >= pairs) break;   // wave-uniform
             const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
@@ -673,6 +694,18 @@ bool sq_c2c(long long n, const MixIO& io, long long batch, hipStream_t s, hipErr
         case 400: *e = run_stft_sq<20, 20, 0>(io, batch, s); return true;
         case 480: *e = run_stft_sq<20, 24, 0>(io, batch, s); return true;
         case 960: *e = run_stft_sq<30, 32, 0>(io, batch, s); return true;
+        default: return false;
+    }
+}
+
+// real rows of 2n (n = 200, 240, 480: R2C at 400, 480, 960) through the register kernel
+bool sq_r2c(long long n2, const MixIO& io, long long batch, hipStream_t s, hipError_t* e) {
+    const char* esq = getenv("VVHIP_STFT_SQ");   // 0: the generic kernel (A/B)
+    if (esq && *esq == '0') return false;
+    switch (n2) {
+        case 400: *e = run_stft_sq<10, 20, 5>(io, batch, s); return true;
+        case 480: *e = run_stft_sq<12, 20, 5>(io, batch, s); return true;
+        case 960: *e = run_stft_sq<20, 24, 5>(io, batch, s); return true;
         default: return false;
     }
 }
@@ -855,6 +888,8 @@ hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, f
         if (half) {
             io.twn = twiddle_table((int)n);
             if (!io.twn) return hipErrorOutOfMemory;
+            hipError_t e = hipSuccess;
+            if (sq_r2c(n, io, batch, s, &e)) return e;
             return run_mixed<5>(ph, io, batch, s);
         }
         return run_mixed<4>(pl, io, batch, s);
