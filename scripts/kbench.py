@@ -380,7 +380,9 @@ CASES = {
     **{f"r2cmix{n}gen": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_STFT_SQ", "0") for n in (400, 960)},
     **{f"r2cmix{n}full": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_MIX_R2C_FULL", "1") for n in (400, 1000)},
     "stft480": lambda: case_stft_n(32, 600, 480, 120, sr=48000),
-    **{f"mix{n}gen": with_env(lambda n=n: case_c2c(n, (1 << 26) // n), "VVHIP_STFT_SQ", "0") for n in (400, 480, 960)},
+    **{f"mix{n}gen": with_env(lambda n=n: case_c2c(n, (1 << 26) // n), "VVHIP_STFT_SQ", "0")
+       for n in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
+    **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (320, 441, 600, 640, 720, 800, 900)},
     "mix960": lambda: case_c2c(960, (1 << 26) // 960),
     "stft960": lambda: case_stft_n(32, 600, 960, 240, sr=48000),
     # *gen: the generic mixed-radix kernel instead of the two-pass register one

@@ -218,7 +218,10 @@ def test_round2_golden_gpu(amd, golden):
     assert np.array_equal(amd.filtfilt(g["h257"], g["xg"])[1], g["yg_kiss"])
 
 
-@pytest.mark.parametrize("nfft,hop,nch,n", [(400, 160, 4, 48000), (480, 160, 3, 20011), (960, 320, 2, 30001)])
+@pytest.mark.parametrize("nfft,hop,nch,n", [(400, 160, 4, 48000), (480, 160, 3, 20011), (960, 320, 2, 30001),
+                                           (320, 160, 2, 16000), (441, 220, 2, 44100), (600, 240, 3, 9999),
+                                           (640, 320, 1, 32000), (720, 360, 2, 14401), (800, 200, 2, 8000),
+                                           (900, 450, 2, 27000)])
 def test_stft_speech_register_kernel_vs_generic(vdev, monkeypatch, nfft, hop, nch, n):
     """The two-pass register kernel for 400 / 480 / 960-point frames
     (k_stft_sq) against the generic mixed-radix kernel (VVHIP_STFT_SQ=0, read
@@ -242,7 +245,8 @@ def test_stft_speech_register_kernel_vs_generic(vdev, monkeypatch, nfft, hop, nc
         assert np.abs(f - g).max() <= 2e-6 * scale
 
 
-@pytest.mark.parametrize("n,b", [(400, 1001), (480, 7), (960, 130)])
+@pytest.mark.parametrize("n,b", [(400, 1001), (480, 7), (960, 130), (320, 33), (441, 65), (600, 9), (640, 64),
+                                 (720, 5), (800, 100), (900, 17)])
 @pytest.mark.parametrize("fwd", [True, False])
 def test_c2c_register_kernel_vs_generic(vdev, monkeypatch, n, b, fwd):
     """c2c rows at 400 / 480 / 960 through the register kernel against the
@@ -265,7 +269,8 @@ def test_c2c_register_kernel_vs_generic(vdev, monkeypatch, n, b, fwd):
     np.testing.assert_array_equal(inplace.cpu().numpy(), fast)
 
 
-@pytest.mark.parametrize("n,b", [(400, 1001), (480, 3), (960, 77)])
+@pytest.mark.parametrize("n,b", [(400, 1001), (480, 3), (960, 77), (640, 12), (882, 31), (1200, 8), (1600, 40),
+                                 (1800, 3), (1920, 5)])
 def test_r2c_register_kernel_vs_generic(vdev, monkeypatch, n, b):
     """Real rows of 400 / 480 / 960 (the n/2-point transform of even/odd pairs
     plus the split step) through the register kernel against the generic

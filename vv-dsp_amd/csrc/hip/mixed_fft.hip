@@ -686,26 +686,39 @@ hipError_t run_stft_sq(const MixIO& io, long long pairs, hipStream_t s) {
     return hipGetLastError();
 }
 
-// c2c rows of n = N1 * N2 through the register kernel (400, 480, 960)
-bool sq_c2c(long long n, const MixIO& io, long long batch, hipStream_t s, hipError_t* e) {
+// Lengths the register kernel takes (n, N1, N2; N1, N2 <= 32): speech and
+// audio frames of 20 / 25 / 30 / 60 ms at 16, 32, 44.1 and 48 kHz
+#define VVH_SQ_LENGTHS(X) \
+    X(320, 16, 20) X(400, 20, 20) X(441, 21, 21) X(480, 20, 24) X(600, 20, 30) X(640, 20, 32) \
+    X(720, 24, 30) X(800, 25, 32) X(900, 30, 30) X(960, 30, 32)
+// half lengths of the real (R2C) rows: the list plus 200 and 240 (R2C at 400 / 480)
+#define VVH_SQ_HALF_LENGTHS(X) X(200, 10, 20) X(240, 12, 20) VVH_SQ_LENGTHS(X)
+
+bool sq_enabled() {
     const char* esq = getenv("VVHIP_STFT_SQ");   // 0: the generic kernel (A/B)
-    if (esq && *esq == '0') return false;
+    return !(esq && *esq == '0');
+}
+
+// c2c rows of n = N1 * N2 through the register kernel
+bool sq_c2c(long long n, const MixIO& io, long long batch, hipStream_t s, hipError_t* e) {
+    if (!sq_enabled()) return false;
     switch (n) {
-        case 400: *e = run_stft_sq<20, 20, 0>(io, batch, s); return true;
-        case 480: *e = run_stft_sq<20, 24, 0>(io, batch, s); return true;
-        case 960: *e = run_stft_sq<30, 32, 0>(io, batch, s); return true;
+#define VVH_SQ_C2C(L, A, B) \
+    case L: *e = run_stft_sq<A, B, 0>(io, batch, s); return true;
+        VVH_SQ_LENGTHS(VVH_SQ_C2C)
+#undef VVH_SQ_C2C
         default: return false;
     }
 }
 
-// real rows of 2n (n = 200, 240, 480: R2C at 400, 480, 960) through the register kernel
+// real rows of n2 = 2 x (N1 * N2) through the register kernel (MODE 5)
 bool sq_r2c(long long n2, const MixIO& io, long long batch, hipStream_t s, hipError_t* e) {
-    const char* esq = getenv("VVHIP_STFT_SQ");   // 0: the generic kernel (A/B)
-    if (esq && *esq == '0') return false;
-    switch (n2) {
-        case 400: *e = run_stft_sq<10, 20, 5>(io, batch, s); return true;
-        case 480: *e = run_stft_sq<12, 20, 5>(io, batch, s); return true;
-        case 960: *e = run_stft_sq<20, 24, 5>(io, batch, s); return true;
+    if (!sq_enabled() || n2 % 2) return false;
+    switch (n2 / 2) {
+#define VVH_SQ_R2C(L, A, B) \
+    case L: *e = run_stft_sq<A, B, 5>(io, batch, s); return true;
+        VVH_SQ_HALF_LENGTHS(VVH_SQ_R2C)
+#undef VVH_SQ_R2C
         default: return false;
     }
 }
@@ -918,11 +931,14 @@ hipError_t launch_stft_mixed(long long nfft, long long hop, int kind, const floa
     io.out_ch_stride = out_ch_stride;
     io.win = win;
     // speech lengths: the two-pass register kernel (VVHIP_STFT_SQ=0: the generic one, A/B)
-    const char* esq = getenv("VVHIP_STFT_SQ");
-    if (!(esq && *esq == '0')) {
-        if (nfft == 400) return run_stft_sq_kind<20, 20>(kind, io, batch, s);
-        if (nfft == 480) return run_stft_sq_kind<20, 24>(kind, io, batch, s);
-        if (nfft == 960) return run_stft_sq_kind<30, 32>(kind, io, batch, s);
+    if (sq_enabled()) {
+        switch (nfft) {
+#define VVH_SQ_STFT(L, A, B) \
+    case L: return run_stft_sq_kind<A, B>(kind, io, batch, s);
+            VVH_SQ_LENGTHS(VVH_SQ_STFT)
+#undef VVH_SQ_STFT
+            default: break;
+        }
     }
     switch (kind) {
         case 0: return run_mixed<1>(pl, io, batch, s);
