@@ -13,7 +13,7 @@ import sys
 
 
 def short(name):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
     return name.replace("void ", "")[:60]
 
 

@@ -649,24 +649,52 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, lon
             const long long q = g + s;
             if (q >= pairs) break;   // wave-uniform
             const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
-            const int lim = fra + 1 < io.frames ? 2 * W : W;
-            const long long bs = c * io.out_ch_stride + fra * W;
-            const float2* X = wbuf + s * LT;
+            if constexpr (n >= 900) {   // both rows per read of Z[e], Z[n-e]: 960-pt 5.83 -> 4.57 ms;
+                                        // 400 / 480 measured 1.3-1.4x slower that way (profiles/r02_ab_sq_emit.jsonl)
+                const bool hbq = fra + 1 < io.frames;
+                const long long bs = c * io.out_ch_stride + fra * W;
+                const float2* X = wbuf + s * LT;
+                // bin e of both rows from one read of Z[e] and Z[n - e]
 #pragma unroll 4
-            for (int o = lane; o < 2 * W; o += 64) {
-                if (o < lim) {
-                    const bool isb = o >= W;
-                    const int e = isb ? o - W : o;
+                for (int e = lane; e < W; e += 64) {
                     const float2 z = X[e], m = X[e == 0 ? 0 : n - e];
                     const float h = 0.5f;
-                    const float2 x = isb ? make_float2((z.y + m.y) * h, (m.x - z.x) * h)
-                                         : make_float2((z.x + m.x) * h, (z.y - m.y) * h);
+                    const float2 xa = make_float2((z.x + m.x) * h, (z.y - m.y) * h);
+                    const float2 xb = make_float2((z.y + m.y) * h, (m.x - z.x) * h);
                     if constexpr (MODE == 2) {
-                        io.out[bs + o] = x;
+                        io.out[bs + e] = xa;
+                        if (hbq) io.out[bs + W + e] = xb;
                     } else {
-                        float* fo = reinterpret_cast<float*>(io.out) + bs + o;
-                        if constexpr (MODE == 1) *fo = __builtin_amdgcn_sqrtf(__builtin_fmaf(x.x, x.x, x.y * x.y));
-                        else *fo = __builtin_fmaf(x.x, x.x, x.y * x.y);
+                        float* fo = reinterpret_cast<float*>(io.out) + bs + e;
+                        if constexpr (MODE == 1) {
+                            fo[0] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xa.x, xa.x, xa.y * xa.y));
+                            if (hbq) fo[W] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xb.x, xb.x, xb.y * xb.y));
+                        } else {
+                            fo[0] = __builtin_fmaf(xa.x, xa.x, xa.y * xa.y);
+                            if (hbq) fo[W] = __builtin_fmaf(xb.x, xb.x, xb.y * xb.y);
+                        }
+                    }
+                }
+            } else {
+                const int lim = fra + 1 < io.frames ? 2 * W : W;
+                const long long bs = c * io.out_ch_stride + fra * W;
+                const float2* X = wbuf + s * LT;
+#pragma unroll 4
+                for (int o = lane; o < 2 * W; o += 64) {
+                    if (o < lim) {
+                        const bool isb = o >= W;
+                        const int e = isb ? o - W : o;
+                        const float2 z = X[e], m = X[e == 0 ? 0 : n - e];
+                        const float h = 0.5f;
+                        const float2 x = isb ? make_float2((z.y + m.y) * h, (m.x - z.x) * h)
+                                             : make_float2((z.x + m.x) * h, (z.y - m.y) * h);
+                        if constexpr (MODE == 2) {
+                            io.out[bs + o] = x;
+                        } else {
+                            float* fo = reinterpret_cast<float*>(io.out) + bs + o;
+                            if constexpr (MODE == 1) *fo = __builtin_amdgcn_sqrtf(__builtin_fmaf(x.x, x.x, x.y * x.y));
+                            else *fo = __builtin_fmaf(x.x, x.x, x.y * x.y);
+                        }
                     }
                 }
             }
