@@ -62,3 +62,30 @@ def test_fir_fft_long_multichannel_device(vdev):
     for c in range(3):
         ref = fftconvolve(x[c].astype(np.float64), h.astype(np.float64))[:x.shape[1]]
         np.testing.assert_allclose(y[c], ref, rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("taps", [300, 10000])
+def test_fir_fft_mode_honours_prefix(amd, taps):
+    """vvhip_fir_apply_host(mode 0) with a caller history (vv_dsp_hip.h: taps-1
+    samples before x[0], oldest first): the long-filter overlap-save path has no
+    history input, so a prefix must route to a path that reads it."""
+    L = amd.lib
+    rng = np.random.default_rng(taps + 5)
+    h = (rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)
+    pre = rng.standard_normal(taps - 1).astype(np.float32)
+    x = rng.standard_normal(3 * taps + 11).astype(np.float32)
+    f = C.c_void_p()
+    fp = C.POINTER(C.c_float)
+    L.vvhip_fir_create.argtypes = [fp, C.c_size_t, C.POINTER(C.c_void_p)]
+    L.vvhip_fir_apply_host.argtypes = [C.c_void_p, fp, fp, C.c_size_t, fp, C.c_int]
+    L.vvhip_fir_destroy.argtypes = [C.c_void_p]
+    assert L.vvhip_fir_create(h.ctypes.data_as(fp), taps, C.byref(f)) == OK
+    try:
+        y = np.zeros_like(x)
+        assert L.vvhip_fir_apply_host(f, x.ctypes.data_as(fp), y.ctypes.data_as(fp), len(x),
+                                      pre.ctypes.data_as(fp), 0) == OK
+    finally:
+        L.vvhip_fir_destroy(f)
+    full = np.concatenate([pre, x]).astype(np.float64)
+    ref = fftconvolve(full, h.astype(np.float64))[taps - 1: taps - 1 + len(x)]
+    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=2e-5)

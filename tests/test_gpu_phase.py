@@ -77,3 +77,19 @@ def test_inst_phase_arguments(amd):
     assert L.vv_dsp_instantaneous_phase(fp, 0, fp) == 2
     assert L.vv_dsp_instantaneous_frequency(None, 4, 1.0, fp) == 1
     assert L.vv_dsp_instantaneous_frequency(fp, 0, 1.0, fp) == 2
+
+
+def test_inst_freq_in_place_device(vdev):
+    """d_phase == d_freq: the shim reads from a copy (f[i] needs p[i-1])."""
+    import ctypes as C
+    import torch
+    rng = np.random.default_rng(8)
+    p = torch.from_numpy(np.cumsum(rng.uniform(-1, 1, (5, 70001)), axis=1).astype(np.float32)).cuda()
+    want = vdev.instantaneous_frequency(p, 8000.0)
+    L = vdev.lib()
+    ip = p.clone()
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert L.vv_dsp_instantaneous_frequency_device(C.c_void_p(ip.data_ptr()), 70001, 5, 8000.0,
+                                                   C.c_void_p(ip.data_ptr()), s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(ip, want)

@@ -858,6 +858,14 @@ bool mixed_supported(long long n) {
     return make_plan(n, &pl) || fs_split(n, &n1, &n2);
 }
 
+// the fused STFT (launch_stft_mixed) needs a single-pass plan: n <= MIX_MAXN.
+// Larger smooth nfft take the generic gather + FFT path (which uses the four-step).
+bool stft_mixed_supported(long long n) {
+    if ((n & (n - 1)) == 0) return false;
+    MixedPlan pl;
+    return make_plan(n, &pl);
+}
+
 // four-step over an intermediate of at most VVHIP_MIX_CHUNK_MB (default: the
 // whole batch) per chunk of transforms
 static hipError_t launch_fft_mixed_fs(long long n, int fwd, const void* in, int real_in, float2* out,

@@ -438,7 +438,7 @@ static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch
                ST_INTERNAL);
         return ST_OK;
     }
-    if (use_mixed(NF)) {   // 7-smooth nfft <= 4096: frames, FFT and |X| in one kernel
+    if (!env_flag("VVHIP_NO_MIXED") && stft_mixed_supported(NF)) {   // 7-smooth nfft <= 4096: one kernel
         HIPCHK(launch_stft_mixed(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch,
                                  (long long)ch_stride, (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
                ST_INTERNAL);
@@ -830,7 +830,8 @@ int vvhip_fir_apply_device(vvhip_fir* f, const float* d_x, float* d_y, size_t n,
                ST_INTERNAL);
         return ST_OK;
     }
-    if (mode == 0) {   // long filters: overlap-save over the four-step FFTs
+    if (mode == 0 && !d_prefix) {   // long zero-state filters: overlap-save over the four-step FFTs
+        // (a caller-supplied history takes the direct form below, which reads it)
         const size_t nl = fir_long_block(f->taps);
         if (nl) return fir_ols_long(f, nl, d_x, d_y, n, nch, x_stride, y_stride, s);
     }
@@ -954,8 +955,15 @@ int vvhip_inst_phase_device(const float* d_z, size_t n, size_t batch, float* d_p
 int vvhip_inst_freq_device(const float* d_phase, size_t n, size_t batch, double fs, float* d_freq, void* stream) {
     if (!d_phase || !d_freq) return ST_NULL;
     if (n == 0) return ST_SIZE;
-    HIPCHK(launch_inst_freq(d_phase, (long long)n, (long long)batch, fs / kTwoPiD, d_freq, (hipStream_t)stream),
-           ST_INTERNAL);
+    if (batch == 0) return ST_OK;
+    hipStream_t s = (hipStream_t)stream;
+    Scratch tmp(s);
+    if (d_phase == d_freq) {   // f[i] needs p[i-1], which a neighbouring thread overwrites: read a copy
+        HIPCHK(tmp.alloc(4 * n * batch), ST_INTERNAL);
+        HIPCHK(hipMemcpyAsync(tmp.p, d_phase, 4 * n * batch, hipMemcpyDeviceToDevice, s), ST_INTERNAL);
+        d_phase = (const float*)tmp.p;
+    }
+    HIPCHK(launch_inst_freq(d_phase, (long long)n, (long long)batch, fs / kTwoPiD, d_freq, s), ST_INTERNAL);
     return ST_OK;
 }
 

@@ -32,6 +32,7 @@ hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, f
 // Mixed-radix Stockham FFT (mixed_fft.hip) for 7-smooth non-power-of-two n
 // <= 4096; same contract as launch_dft_naive, and in == out is allowed.
 bool mixed_supported(long long n);
+bool stft_mixed_supported(long long n);
 hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
                             long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s);
 // STFT rows through the mixed-radix kernel (frames gathered and windowed on

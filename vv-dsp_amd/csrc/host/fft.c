@@ -30,6 +30,14 @@ const vv_dsp_fft_backend_vtable* g_fft_backends[VV_DSP_FFT_NUM_BACKENDS];
 static vv_dsp_fft_backend g_current = VV_DSP_FFT_BACKEND_HIP;
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 
+/* make_plan_many -> vtable->make_plan hand-off of the batch count (fft_backend.h) */
+static __thread const struct vv_dsp_fft_plan* t_pending_spec;
+static __thread size_t t_pending_batch;
+
+size_t vv_amd_fft_pending_batch(const struct vv_dsp_fft_plan* spec) {
+    return (spec && spec == t_pending_spec) ? t_pending_batch : 1;
+}
+
 static int slot_ok(int b) {
     return b >= 0 && b < VV_DSP_FFT_NUM_BACKENDS && g_fft_backends[b] && g_fft_backends[b]->is_available();
 }
@@ -91,16 +99,21 @@ vv_dsp_status vv_dsp_fft_make_plan_many(size_t n, vv_dsp_fft_type type, vv_dsp_f
     if (dir != VV_DSP_FFT_FORWARD && dir != VV_DSP_FFT_BACKWARD) return VV_DSP_ERROR_OUT_OF_RANGE;
     ensure_init();
     if (!slot_ok(g_current)) return VV_DSP_ERROR_UNSUPPORTED;
-    vv_dsp_fft_plan* p = (vv_dsp_fft_plan*)calloc(1, sizeof(*p));
-    if (!p) return VV_DSP_ERROR_INTERNAL;
+    vv_amd_fft_plan* w = (vv_amd_fft_plan*)calloc(1, sizeof(*w));
+    if (!w) return VV_DSP_ERROR_INTERNAL;
+    vv_dsp_fft_plan* p = &w->pub;
     p->n = n;
     p->type = type;
     p->dir = dir;
     p->backend = g_current;
-    p->batch = batch;
+    w->batch = batch;
+    t_pending_spec = p;
+    t_pending_batch = batch;
     vv_dsp_status st = g_fft_backends[p->backend]->make_plan(p, &p->backend_plan.generic);
+    t_pending_spec = NULL;
+    t_pending_batch = 1;
     if (st != VV_DSP_OK) {
-        free(p);
+        free(w);
         return st;
     }
     *out_plan = p;
@@ -122,10 +135,10 @@ vv_dsp_status vv_dsp_fft_execute(const vv_dsp_fft_plan* plan, const void* in, vo
     if (!plan || !in || !out) return VV_DSP_ERROR_NULL_POINTER;
     const vv_dsp_fft_backend_vtable* vt = g_fft_backends[plan->backend];
     if (!vt || !vt->is_available()) return VV_DSP_ERROR_UNSUPPORTED;
-    if (plan->backend == VV_DSP_FFT_BACKEND_HIP || plan->batch == 1)
+    if (plan->backend == VV_DSP_FFT_BACKEND_HIP || vv_amd_plan_batch(plan) == 1)
         return vt->execute(plan, plan->backend_plan.generic, in, out);
     /* CPU backends have no batch notion: one call per transform */
-    for (size_t b = 0; b < plan->batch; ++b) {
+    for (size_t b = 0; b < vv_amd_plan_batch(plan); ++b) {
         vv_dsp_status st = vt->execute(plan, plan->backend_plan.generic,
                                        (const char*)in + b * in_stride_bytes(plan),
                                        (char*)out + b * out_stride_bytes(plan));
@@ -137,7 +150,7 @@ vv_dsp_status vv_dsp_fft_execute(const vv_dsp_fft_plan* plan, const void* in, vo
 vv_dsp_status vv_dsp_fft_execute_device(const vv_dsp_fft_plan* plan, const void* d_in, void* d_out, void* stream) {
     if (!plan || !d_in || !d_out) return VV_DSP_ERROR_NULL_POINTER;
     if (plan->backend != VV_DSP_FFT_BACKEND_HIP) return VV_DSP_ERROR_UNSUPPORTED;
-    return (vv_dsp_status)vvhip_fft_exec_device((vvhip_fft*)plan->backend_plan.generic, d_in, d_out, plan->batch,
+    return (vv_dsp_status)vvhip_fft_exec_device((vvhip_fft*)plan->backend_plan.generic, d_in, d_out, vv_amd_plan_batch(plan),
                                                 stream);
 }
 
@@ -146,7 +159,7 @@ vv_dsp_status vv_dsp_fft_destroy(vv_dsp_fft_plan* plan) {
     const vv_dsp_fft_backend_vtable* vt =
         ((int)plan->backend >= 0 && (int)plan->backend < VV_DSP_FFT_NUM_BACKENDS) ? g_fft_backends[plan->backend] : NULL;
     if (vt && vt->free_plan) vt->free_plan(plan->backend_plan.generic);
-    free(plan);
+    free((vv_amd_fft_plan*)plan);
     return VV_DSP_OK;
 }
 

@@ -16,8 +16,27 @@ struct vv_dsp_fft_plan {
     union {
         void* generic;
     } backend_plan;
-    size_t batch; /* appended field: transforms per execute (1 for the reference API) */
 };
+
+/* Plans made by THIS library's dispatcher carry a batch count.  It lives in a
+ * wrapper around the reference-sized plan, never inside it: a backend vtable
+ * must not read past struct vv_dsp_fft_plan, because the reference's
+ * dispatcher mallocs exactly that struct (src/spectral/fft.c:76) before it
+ * calls make_plan.  The HIP vtable learns the batch through
+ * vv_amd_fft_pending_batch(), which answers 1 for any plan it did not
+ * allocate itself (e.g. one made by the reference's own fft.c). */
+typedef struct vv_amd_fft_plan {
+    struct vv_dsp_fft_plan pub; /* first member: the opaque user handle points here */
+    size_t batch;               /* transforms per execute (1 for the reference API) */
+} vv_amd_fft_plan;
+
+static inline size_t vv_amd_plan_batch(const struct vv_dsp_fft_plan* p) {
+    return ((const vv_amd_fft_plan*)p)->batch;
+}
+
+/* Batch of the plan currently inside this thread's make_plan_many (fft.c), or 1
+ * when `spec` is not that plan. */
+__attribute__((visibility("hidden"))) size_t vv_amd_fft_pending_batch(const struct vv_dsp_fft_plan* spec);
 
 typedef struct vv_dsp_fft_backend_vtable {
     vv_dsp_status (*make_plan)(const struct vv_dsp_fft_plan* spec, void** backend_data);
