@@ -99,6 +99,8 @@ def fft_c2c_roofline(reps=50):
             "achieved_GBs": round(byts / (avg * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
             "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ffts_per_s": round(B / (avg * 1e-3), 1),
+            "kernel": "vvh::k_c2c<1024, true, 0> (one launch)",
+            **dict(zip(("traffic", "traffic_source"), kernel_traffic(["vvh::k_c2c<1024, true,"]))),
             "backward": {"ms_avg": round(bavg, 4), "ms_min": round(bbest, 4),
                          "frac": round(byts / (bavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
@@ -152,73 +154,183 @@ def fir_roofline(reps=50):
             "ms_avg": round(avg, 4), "ms_min": round(best, 4),
             "achieved_GBs": round(byts / (avg * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
             "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "samples_per_s": round(nch * n / (avg * 1e-3), 1)}
+            "samples_per_s": round(nch * n / (avg * 1e-3), 1),
+            "kernel": "vvh::k_fir_bulk_reg<1024, 0> (bulk pairs) + vvh::k_fir_pair<1024, false> (first/last pair of "
+                      "each channel), one step",
+            **dict(zip(("traffic", "traffic_source"), kernel_traffic(["vvh::k_fir_bulk_reg<1024", "vvh::k_fir_pair<1024"])))}
+
+
+def host_cpu_share():
+    """Threads for the CPU baseline: this process's CPU affinity, capped by the
+    cgroup CPU quota and by OMP_NUM_THREADS when either is set (the GPU box
+    exposes every core of the host but grants one GPU's job a share of them),
+    and the CPU model from /proc/cpuinfo."""
+    cands = {"affinity": len(os.sched_getaffinity(0))}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            cands["cgroup_quota"] = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        cands["OMP_NUM_THREADS"] = max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        pass
+    model = "?"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return min(cands.values()), cands, model, os.cpu_count()
+
+
+def _threaded(threads, seconds, work):
+    """Run work(i, t_end) on `threads` threads until `seconds` pass; ctypes
+    releases the GIL inside the reference's C calls."""
+    t_end = time.perf_counter() + seconds
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        done = sum(ex.map(lambda i: work(i, t_end), range(threads)))
+    return done, time.perf_counter() - t0
 
 
 def cpu_baseline(threads=None, seconds=15.0):
-    """The reference's own vv_dsp_stft_spectrogram (KissFFT, oracle/_ref = the
-    reference sources compiled in the build container) on this host's cores:
-    `threads` workers each run whole 60 s mono spectrograms back to back until
-    `seconds` have passed (a bounded sample of the same per-channel workload)."""
-    from vvapi import VvDsp
+    """The reference's own code (oracle/_ref = the reference sources compiled in
+    the build container, KissFFT backend) on this host's CPU share, on bounded
+    samples of three BASELINE workloads:
+      * headline: vv_dsp_stft_spectrogram of 60 s mono (stft.c:112-144) back to
+        back on every thread (frames/s; the bench line's cpu_baseline value);
+      * config 2: 1024-pt C2C transforms through vv_dsp_fft_execute
+        (fft_kiss.c:27-74), whole 65,536-transform batches per thread;
+      * config 4: vv_dsp_fir_apply direct form (fir.c:160-196), 257 taps, one
+        2^22-sample quarter channel per thread (the reference's fir_apply_fft
+        is O(n^2) there)."""
+    from vvapi import VvDsp, FirState
     path = os.path.join(ROOT, "oracle", "_ref", "libvvref.so")
+    bpath = os.path.join(ROOT, "oracle", "_ref", "librefbench.so")
     if not os.path.exists(path):
         return {"value": None, "unit": "frames/s", "cores": 0, "kind": "reference",
                 "sample": "oracle/_ref/libvvref.so missing"}
     ref = VvDsp(path)
-    threads = threads or max(1, min(16, len(os.sched_getaffinity(0))))
+    share, cands, model, ncpu = host_cpu_share()
+    threads = threads or share
     n = 60 * FS
     rng = np.random.default_rng(3)
     sigs = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(threads)]
-    t_end = time.perf_counter() + seconds
 
-    def work(i):
+    def stft_work(i, t_end):
         done = 0
         while time.perf_counter() < t_end:
-            ref.spectrogram(sigs[i], NFFT, HOP)   # ctypes releases the GIL
+            ref.spectrogram(sigs[i], NFFT, HOP)
             done += 1
         return done
 
-    t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex:
-        runs = sum(ex.map(work, range(threads)))
-    dt = time.perf_counter() - t0
+    runs, dt = _threaded(threads, seconds, stft_work)
     frames = runs * frames_of(n)
     t1 = time.perf_counter()
     ref.spectrogram(sigs[0], NFFT, HOP)
     d1 = time.perf_counter() - t1
-    return {"value": round(frames / dt, 1), "unit": "frames/s", "cores": threads, "kind": "reference",
-            "sample": f"{threads} threads x vv_dsp_stft_spectrogram(60 s @ 48 kHz mono, 1024 Hann, hop 256) "
-                      f"back to back for {seconds:.0f} s: {runs} runs = {frames} frames in {dt:.2f} s",
-            "single_thread_frames_per_s": round(frames_of(n) / d1, 1)}
+    del sigs
+    res = {"value": round(frames / dt, 1), "unit": "frames/s", "cores": threads, "kind": "reference",
+           "sample": f"{threads} threads x vv_dsp_stft_spectrogram(60 s @ 48 kHz mono, 1024 Hann, hop 256) "
+                     f"back to back for {seconds:.0f} s: {runs} runs = {frames} frames in {dt:.2f} s",
+           "single_thread_frames_per_s": round(frames_of(n) / d1, 1),
+           "cpu_model": model, "host_cpus": ncpu, "thread_caps": cands}
+
+    if os.path.exists(bpath):      # config 2
+        rb = C.CDLL(bpath)
+        rb.refbench_fft_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_int]
+        B, N, chunk = 65536, 1024, 4096
+        x = np.random.default_rng(1).uniform(-0.5, 0.5, (B, 2 * N)).astype(np.float32)
+        ys = [np.empty((chunk, 2 * N), np.float32) for _ in range(threads)]
+
+        def fft_work(i, t_end):
+            done = 0
+            while time.perf_counter() < t_end:
+                r0 = (done * chunk + i * 977 * chunk) % B
+                r0 -= r0 % chunk
+                assert rb.refbench_fft_rows(x[r0:].ctypes.data, ys[i].ctypes.data, N, chunk, 1) == 0
+                done += chunk
+            return done
+
+        cnt, dt2 = _threaded(threads, 5.0, fft_work)
+        res["config2_fft_c2c_1024"] = {
+            "value": round(cnt / dt2, 1), "unit": "transforms/s", "cores": threads,
+            "batch_65536_s": round(B / (cnt / dt2), 4),
+            "sample": f"{threads} threads x vv_dsp_fft_execute (Kiss radix-2, one plan per thread) over rows of a "
+                      f"65536 x 1024 uniform[-0.5,0.5) batch for 5 s: {cnt} transforms in {dt2:.2f} s"}
+        del x, ys
+
+    h = np.zeros(257, np.float32)          # config 4
+    ref.lib.vv_dsp_fir_design_lowpass(h.ctypes.data_as(C.POINTER(C.c_float)), 257, 0.25, 2)
+    ns = 1 << 22
+    xs = [np.random.default_rng(4 + i).uniform(-1, 1, ns).astype(np.float32) for i in range(threads)]
+    ys = [np.empty(ns, np.float32) for _ in range(threads)]
+
+    def fir_work(i, t_end):
+        st = FirState()
+        assert ref.lib.vv_dsp_fir_state_init(C.byref(st), 257) == 0
+        fp = C.POINTER(C.c_float)
+        r = ref.lib.vv_dsp_fir_apply(C.byref(st), h.ctypes.data_as(fp), xs[i].ctypes.data_as(fp),
+                                     ys[i].ctypes.data_as(fp), ns)
+        ref.lib.vv_dsp_fir_state_free(C.byref(st))
+        assert r == 0
+        return ns
+
+    cnt, dt4 = _threaded(threads, 0.0, fir_work)
+    res["config4_fir_direct_257"] = {
+        "value": round(cnt / dt4, 1), "unit": "samples/s", "cores": threads,
+        "config4_s": round(8 * (1 << 24) / (cnt / dt4), 3),
+        "sample": f"{threads} threads x vv_dsp_fir_apply (direct form, fresh state) on 2^22 uniform[-1,1) "
+                  f"samples each: {cnt} samples in {dt4:.2f} s"}
+    return res
 
 
-def hbm_traffic(channels):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
-    command (scripts/gpu_prof.sh + scripts/pmc_summary.py --json): FETCH_SIZE x 2
-    (gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md §HBM) + WRITE_SIZE,
-    both in KiB, summed over the bulk and tail STFT launches of one step."""
+def _load_pmc():
     try:
         with open(TRAFFIC_JSON) as f:
-            prof = json.load(f)
+            return json.load(f)
     except (OSError, ValueError):
+        return None
+
+
+def kernel_traffic(prefixes, per_step_calls=None, channels=None):
+    """HBM bytes per launch of one leg from the committed rocprofv3 PMC summary
+    of this command (scripts/gpu_bench_prof.sh + scripts/pmc_summary.py --json):
+    FETCH_SIZE x 2 (gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md
+    §HBM) + WRITE_SIZE, both in KiB, per dispatch, summed over the kernels of
+    one launch (names starting with one of `prefixes`)."""
+    prof = _load_pmc()
+    if prof is None:
         return None, "no PMC summary committed"
-    if prof.get("channels_per_gpu") != channels:
+    if channels is not None and prof.get("channels_per_gpu") != channels:
         return None, f"PMC summary is for {prof.get('channels_per_gpu')} channels per GPU"
     tot, names = 0.0, []
     for k, c in prof["kernels"].items():
-        if k.startswith("vvh::k_stft_pair<1024, 0"):
+        if k.startswith(tuple(prefixes)) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             tot += (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
-            names.append(k)
+            names.append(f"{k} ({c.get('avg_us')} us avg)")
     if not names:
-        return None, "PMC summary has no k_stft_pair<1024,0,*> entries"
+        return None, f"PMC summary has no {'/'.join(prefixes)} entries"
     return round(tot), f"{os.path.relpath(TRAFFIC_JSON, ROOT)} ({prof.get('box', '?')}): " \
                        f"(2*FETCH_SIZE + WRITE_SIZE) KiB x 1024 per dispatch over {', '.join(names)}"
 
 
-def gather_leg(out, total_ch, compute_s, frames_per_step, rank):
+def hbm_traffic(channels):
+    return kernel_traffic(["vvh::k_stft_pair<1024, 0"], channels=channels)
+
+
+def gather_leg(out, total_ch, compute_s, frames_per_step, rank, half=True):
     """One timed RCCL gather (torch.distributed nccl backend = RCCL, point to
-    point over xGMI) of every rank's [ch][frame][1024] rows to rank 0."""
+    point over xGMI) of every rank's [ch][frame][1024] rows to rank 0.  With
+    `half` (default) each rank sends bins 0..512 only (vv_dsp_spectrogram_pack_
+    half_device) and rank 0 expands them by mirror symmetry
+    (vv_dsp_spectrogram_unpack_half_device) -- bit-identical rows for half the
+    xGMI bytes (SURVEY 8e row note 1); the timed region covers pack, gather
+    and expand."""
     try:
         full = None
         if rank == 0:
@@ -226,21 +338,67 @@ def gather_leg(out, total_ch, compute_s, frames_per_step, rank):
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        vvdsp_dist.gather_rows(out, total_ch, dst=0, out=full)
+        if half:
+            vvdsp_dist.gather_rows_half(out, total_ch, NFFT, dst=0, out=full)
+        else:
+            vvdsp_dist.gather_rows(out, total_ch, dst=0, out=full)
         torch.cuda.synchronize()
         dist.barrier()
         g = time.perf_counter() - t0
         t = torch.tensor([g], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         g = float(t.item())
-        gathered = (total_ch - out.shape[0]) * out[0].numel() * out.element_size()
+        row_bins = NFFT // 2 + 1 if half else NFFT
+        gathered = (total_ch - out.shape[0]) * out.shape[1] * row_bins * out.element_size()
         del full
-        return {"gather_s": round(g, 4), "bytes_into_rank0": gathered,
+        return {"gather_s": round(g, 4), "bins_sent": row_bins, "bytes_into_rank0": gathered,
                 "xgmi_GBs_into_rank0": round(gathered / g / 1e9, 1),
                 "frames_per_s_with_gather": round(frames_per_step / (compute_s + g), 1),
-                "note": "one step of compute + one gather of the full magnitude rows to rank 0"}
+                "note": "one step of compute + one gather of every rank's magnitude rows to rank 0 "
+                        + ("(bins 0..512 packed on each rank, expanded to 1024 on rank 0, bit-identical)"
+                           if half else "(all 1024 bins)")}
     except Exception as e:  # report, do not lose the bench line
         return {"error": repr(e)[:300]}
+
+
+def full_job_leg(steps=3):
+    """Config 5's whole job -- 256 ch x 10 min @ 48 kHz, 147.5 GB in + out --
+    on ONE GPU (it fits the 288 GB of HBM): the strong-scaling anchor for the
+    driver's 1/2/4/8-GPU runs.  Same kernel and output layout as the headline."""
+    ch = 256
+    nfr = frames_of(SAMPLES)
+    try:
+        sig = torch.empty(ch, SAMPLES, device="cuda")
+        for c in range(ch):
+            g = torch.Generator(device="cuda").manual_seed(c)
+            sig[c].uniform_(-1.0, 1.0, generator=g)
+        out = torch.empty(ch, nfr, NFFT, device="cuda")
+    except torch.OutOfMemoryError as e:
+        return {"error": repr(e)[:200]}
+    st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
+    st.spectrogram(sig, out=out)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(steps):
+        st.spectrogram(sig, out=out)
+    b.record(s)
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / steps
+    fr = 12345
+    x0 = sig[255, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
+    w = np.array([0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(NFFT - 1) * np.float32(i))
+                  for i in range(NFFT)], np.float64)
+    ok = np.allclose(out[255, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * w)), rtol=5e-5, atol=5e-5)
+    byts = ch * SAMPLES * 4 + ch * nfr * NFFT * 4 + NFFT * 4
+    del sig, out, st
+    torch.cuda.empty_cache()
+    return {"workload": "config5 whole job on one GPU: 256 ch x 10 min @ 48 kHz, 1024 Hann, hop 256 "
+                        "(28,799,488 frames; 29.5 GB in, 118 GB out)",
+            "steps": steps, "ms_per_step": round(ms, 3), "frames_per_s": round(ch * nfr / (ms * 1e-3), 1),
+            "bytes_per_step": byts, "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "check_row_vs_numpy_f64": bool(ok)}
 
 
 def main():
@@ -249,7 +407,15 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=25)
     ap.add_argument("--channels", type=int, default=CH_PER_GPU, help="channels per GPU")
-    ap.add_argument("--no-extras", action="store_true", help="skip config 2/4 and CPU baseline legs")
+    ap.add_argument("--no-extras", action="store_true", help="skip config 2/3/4 and CPU baseline legs")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
+    ap.add_argument("--legs", default="c2c,fir,config3",
+                    help="extra GPU legs: c2c (config 2), fir (config 4), config3 (profiling runs leave config3 "
+                         "out so the headline kernel's PMC average covers the headline launches only)")
+    ap.add_argument("--full-job", choices=["auto", "on", "off"], default="auto",
+                    help="config 5's whole 256-channel job on one GPU as an extra leg (auto: on at N = 1 with extras)")
+    ap.add_argument("--gather-bins", choices=["half", "full"], default="half",
+                    help="gather bins 0..512 and expand on rank 0 (half, default) or all 1024 bins (full)")
     ap.add_argument("--gather", choices=["auto", "on", "off"], default="auto",
                     help="after the timed steps, time one RCCL gather of all spectrogram rows to rank 0 "
                          "(config 5 'with gather'; auto = on when N > 1)")
@@ -316,7 +482,8 @@ def main():
     ok = np.allclose(out[0, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * w)), rtol=5e-5, atol=5e-5)
     gather = None
     if world > 1 and (args.gather == "on" or args.gather == "auto"):
-        gather = gather_leg(out, C_ * world, elapsed / args.steps, frames_total / args.steps, rank)
+        gather = gather_leg(out, C_ * world, elapsed / args.steps, frames_total / args.steps, rank,
+                            half=args.gather_bins == "half")
     del sig, out, st
     torch.cuda.empty_cache()
 
@@ -355,14 +522,21 @@ def main():
     }
     if gather is not None:
         res["with_gather"] = gather
+    legs = set(args.legs.split(","))
     if rank == 0 and not args.no_extras and world == 1:
-        res["fft_c2c_1024"] = fft_c2c_roofline()
+        if "c2c" in legs:
+            res["fft_c2c_1024"] = fft_c2c_roofline()
+            torch.cuda.empty_cache()
+        if "fir" in legs:
+            res["fir_ols_257"] = fir_roofline()
+            torch.cuda.empty_cache()
+        if "config3" in legs:
+            res["stft_config3"] = stft_config3()
+            torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and (args.full_job == "on" or (args.full_job == "auto" and not args.no_extras)):
+        res["config5_full_job_1gpu"] = full_job_leg()
         torch.cuda.empty_cache()
-        res["fir_ols_257"] = fir_roofline()
-        torch.cuda.empty_cache()
-        res["stft_config3"] = stft_config3()
-        torch.cuda.empty_cache()
-    if rank == 0 and not args.no_extras and world == 1:
+    if rank == 0 and not args.no_extras and not args.no_cpu and world == 1:
         res["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -23,6 +23,11 @@ extern "C" {
 /* number of usable HIP devices */
 int vv_dsp_amd_device_count(void);
 const char* vv_dsp_amd_last_error(void);
+/* The calling thread's device for the device-pointer calls below (hipSetDevice):
+ * one process per GPU sets it once; one process driving several GPUs switches it
+ * per shard.  OUT_OF_RANGE for a bad index, UNSUPPORTED with no device. */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_amd_set_device(int device);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_amd_get_device(int* device);
 
 /* FFT: `batch` contiguous transforms per execute (host or device pointers). */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_fft_make_plan_many(size_t n, vv_dsp_fft_type type, vv_dsp_fft_dir dir,
@@ -57,6 +62,36 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_frames_range_device(vv_dsp_stft* h, c
                                                                size_t n, size_t nch, size_t ch_stride,
                                                                size_t frame0, size_t nframes, void* d_out,
                                                                size_t out_ch_stride, int out_kind, void* stream);
+/* ---- Multi-GPU layout of config 5: channels shard with no
+ * exchange; the only collective is the caller's gather of the rows. ----
+ * The contiguous block split rank `rank` of `world` owns: channels
+ * [*first, *first + *count), rank order = channel order, sizes differ by at most
+ * one (the same split as vv-dsp_amd/vvdsp_dist.py channel_shard). */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_shard_range(size_t total, size_t world, size_t rank, size_t* first,
+                                                  size_t* count);
+/* One rank's share of a multi-channel spectrogram on `device`: the rows of
+ * channels [first, first + count) of a [total][n] job (d_signal points at the
+ * shard's first channel, on that device) into d_out [count][frames][row].
+ * out_kind as vv_dsp_stft_frames_range_device (0 magnitude, 1 complex, 2 power
+ * n/2+1).  The handle may be shared by all devices: its window is copied to
+ * each device once.  The thread's current device is restored on return. */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_channel_shard_device(vv_dsp_stft* h, int device,
+                                                                const vv_dsp_real* d_signal, size_t n, size_t count,
+                                                                size_t ch_stride, int out_kind, void* d_out,
+                                                                size_t out_ch_stride, void* stream, size_t* out_frames);
+/* Half-spectrum rows for the gather: magnitude (or power) rows of real frames
+ * are mirror-symmetric, |X[n-k]| = |X[k]|, so a rank can send bins 0..n/2 only
+ * (half the xGMI bytes of config 5's gather) and the root expands them.
+ * pack: [rows][fft_size] -> [rows][fft_size/2+1]; unpack: the reverse, bin k
+ * above fft_size/2 taken from bin fft_size-k.  For rows of the fused STFT
+ * kernels (power-of-two fft_size <= 8192, 7-smooth <= 4096) the mirror bins
+ * are computed from the same conjugate pair, so unpack(pack(rows)) == rows bit
+ * for bit. */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_spectrogram_pack_half_device(const vv_dsp_real* d_rows, size_t rows,
+                                                                   size_t fft_size, vv_dsp_real* d_half, void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_spectrogram_unpack_half_device(const vv_dsp_real* d_half, size_t rows,
+                                                                     size_t fft_size, vv_dsp_real* d_rows,
+                                                                     void* stream);
 /* Batched framing (vv_dsp_fetch_frame / vv_dsp_overlap_add, framing.c:71-146):
  * frames [frame0, frame0 + count) into d_frames[count][frame_len]; and count
  * frames added into d_out[output_len] at (frame0 + f) * hop_len, every output

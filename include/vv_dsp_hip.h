@@ -59,6 +59,9 @@ int vvhip_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int vvhip_memset(void* dst, int value, size_t bytes);
 int vvhip_stream_sync(void* stream);
 int vvhip_device_sync(void);
+/* the calling thread's current HIP device (hipSetDevice / hipGetDevice) */
+int vvhip_set_device(int device);
+int vvhip_get_device(int* device);
 
 /* ---- FFT: replaces the backend vtable slot (fft_backend.h:32-38) ----
  * type: 0 C2C, 1 R2C, 2 C2R (fft.h:152-156); dir: +1 forward, -1 backward.
@@ -90,6 +93,10 @@ int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n
 int vvhip_stft_spectrogram_range_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
                                         size_t ch_stride, size_t frame0, size_t nframes, void* d_out,
                                         size_t out_ch_stride, int out_kind, void* stream);
+/* Half-spectrum rows for the config-5 gather: pack [rows][n] -> [rows][n/2+1]
+ * (unpack 0), or expand [rows][n/2+1] -> [rows][n] by out[k] = in[n-k] above
+ * n/2 (unpack 1; magnitude rows of real frames are mirror-symmetric). */
+int vvhip_rows_half_device(const float* d_in, float* d_out, size_t rows, size_t n, int unpack, void* stream);
 int vvhip_stft_process_host(vvhip_stft* h, const float* frame, float* spec_out);
 int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count, float* d_spec,
                               void* stream);

@@ -146,6 +146,7 @@ def main():
          minph_kiss=ref.minphase_from_cepstrum(c), minph_np64=H)
 
     round2_sets(ref, man)
+    round3_sets(ref, man)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
     print("wrote", len(man), "golden sets")
@@ -200,8 +201,65 @@ def round2_sets(ref, man):
          x=xs, kiss=mag, np64=np_mag.astype(np.float64))
 
 
+REGISTER_LENGTHS = (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)
+# real rows whose n/2-point transform is a register length (vv-dsp_amd mixed_fft.hip VVH_SQ_HALF_LENGTHS)
+REGISTER_R2C_LENGTHS = (400, 480) + tuple(2 * n for n in REGISTER_LENGTHS)
+
+
+def round3_sets(ref, man):
+    """Round-3 fixtures: every length of the two-pass register kernel
+    (k_stft_sq), pinned to the reference's own non-power-of-two path
+    (fft_kiss.c:76-92 via :114-116; R2C :120-147; STFT stft.c:74-92,112-144)
+    and NumPy f64.  One set per length: c2c forward and backward of one complex
+    row, and an STFT of 3*n+13 samples at hop n/2 (6 frames, the last one
+    zero-padded): the reference's magnitude rows (vv_dsp_stft_spectrogram) and
+    complex rows (vv_dsp_stft_process per frame), with f64 complex rows
+    (magnitude and power rows follow from them)."""
+    for n in REGISTER_LENGTHS:
+        rng = np.random.default_rng(30000 + n)
+        x = (rng.random(n) - 0.5 + 1j * (rng.random(n) - 0.5)).astype(np.complex64)
+        hop = n // 2
+        sig = rng.uniform(-1, 1, 3 * n + 13).astype(np.float32)
+        mag = ref.spectrogram(sig, n, hop)
+        nfr = mag.shape[0]
+        win = ref.window(1, n)[1]
+        pad = np.concatenate([sig, np.zeros(n, np.float32)])
+        frames = np.stack([pad[f * hop: f * hop + n] for f in range(nfr)])
+        st, h = ref.stft_create(n, hop)
+        assert st == 0
+        try:
+            cpx = np.stack([ref.stft_process(h, fr.copy(), n) for fr in frames])
+        finally:
+            ref.lib.vv_dsp_stft_destroy(h)
+        X64 = np.fft.fft(frames.astype(np.float64) * win.astype(np.float64), axis=1)
+        save(f"register_n{n}", man, f"register-kernel length {n}: c2c fwd/bwd of one uniform[-0.5,0.5) complex "
+             f"row (seed {30000 + n}); STFT of {3 * n + 13} uniform[-1,1) samples, nfft {n}, hop {hop}, Hann: "
+             "reference magnitude rows, reference complex rows (stft_process), f64 complex rows",
+             x=x, c2c_fwd_kiss=ref.fft(x, C2C, FWD), c2c_fwd_np64=np.fft.fft(x.astype(np.complex128)),
+             c2c_bwd_kiss=ref.fft(x, C2C, BWD), c2c_bwd_np64=np.fft.ifft(x.astype(np.complex128)),
+             sig=sig, hop=np.array([hop], np.int64), stft_mag_kiss=mag.astype(np.float32),
+             stft_cpx_kiss=cpx.astype(np.complex64), stft_cpx_np64=X64)
+    rows, kiss, np64 = {}, {}, {}
+    for n in REGISTER_R2C_LENGTHS:
+        rng = np.random.default_rng(31000 + n)
+        xr = (rng.random(n) - 0.5).astype(np.float32)
+        rows[f"x{n}"] = xr
+        kiss[f"kiss{n}"] = ref.fft(xr, R2C)
+        np64[f"np64_{n}"] = np.fft.rfft(xr.astype(np.float64))
+    save("register_r2c", man, "R2C rows at every length whose half is a register-kernel length "
+         f"{REGISTER_R2C_LENGTHS}: uniform[-0.5,0.5) seed 31000+n; the reference's R2C (its O(n^2) DFT) and "
+         "NumPy f64", **rows, **kiss, **np64)
+
+
 if __name__ == "__main__":
-    if "--round2-only" in sys.argv:   # add the round-2 sets without rewriting the others
+    if "--round3-only" in sys.argv:   # add the round-3 sets without rewriting the others
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            m = json.load(f)
+        round3_sets(VvDsp(REF), m)
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(m, f, indent=1, sort_keys=True)
+        print("manifest now", len(m), "sets")
+    elif "--round2-only" in sys.argv:   # add the round-2 sets without rewriting the others
         with open(os.path.join(HERE, "manifest.json")) as f:
             m = json.load(f)
         round2_sets(VvDsp(REF), m)

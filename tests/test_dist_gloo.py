@@ -52,6 +52,39 @@ def _worker(rank, world, nch, port, q, slab=None):
         dist.destroy_process_group()
 
 
+def _half_worker(rank, world, nch, port, q):
+    """gather_rows_half: ranks send bins 0..NFFT/2 of their rows; rank 0
+    expands by mirror symmetry.  pack / unpack here are torch slices on CPU
+    tensors (the layout under test); on the GPU they are the library kernels
+    (tests/test_gpu_shard.py pins those)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vvapi import Oracle
+        orc = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
+        x = _signals(nch)
+        lo, hi = vvdsp_dist.channel_shard(nch, world, rank)
+        local = torch.from_numpy(np.stack([orc.spectrogram(x[c], NFFT, HOP) for c in range(lo, hi)]))
+        h = NFFT // 2 + 1
+        mirror = torch.tensor([k if k < h else NFFT - k for k in range(NFFT)])
+
+        def unpack(t, o):
+            o.copy_(t[..., mirror])
+
+        full = vvdsp_dist.gather_rows_half(local, nch, NFFT, dst=0, pack=lambda t: t[..., :h].contiguous(),
+                                           unpack=unpack)
+        if rank == 0:
+            ref = np.stack([orc.spectrogram(x[c], NFFT, HOP) for c in range(nch)])
+            ref = ref[..., mirror.numpy()]
+            q.put(bool(np.array_equal(full.numpy(), ref)) and tuple(full.shape) == ref.shape)
+        else:
+            q.put(full is None)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
 def _frame_worker(rank, world, port, q):
     """One long signal split by frame ranges (config 3 sharded): each rank
     transforms its input slice (frame0's first sample on, as
@@ -115,6 +148,40 @@ def test_frame_sharded_spectrogram_gather_gloo(world):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+@pytest.mark.parametrize("world,nch", [(2, 4), (3, 6)])
+def test_half_bin_gather_gloo(world, nch):
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        pytest.skip("oracle not built (make -C oracle)")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_half_worker, args=(r, world, nch, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert all(q.get(timeout=5) is True for _ in range(world))
+
+
+def test_shard_range_c_matches_python():
+    """vv_dsp_shard_range (vv_dsp_amd.h, pure host arithmetic) is the same split
+    as vvdsp_dist.channel_shard."""
+    import ctypes as C
+    L = C.CDLL(os.path.join(ROOT, "vv-dsp_amd", "lib", "libvvdsp_amd.so"))
+    L.vv_dsp_shard_range.argtypes = [C.c_size_t] * 3 + [C.POINTER(C.c_size_t)] * 2
+    for total in (0, 1, 7, 256, 1001):
+        for world in (1, 2, 3, 8):
+            for r in range(world):
+                a, b = C.c_size_t(), C.c_size_t()
+                assert L.vv_dsp_shard_range(total, world, r, C.byref(a), C.byref(b)) == 0
+                assert (a.value, a.value + b.value) == vvdsp_dist.channel_shard(total, world, r)
+    a, b = C.c_size_t(), C.c_size_t()
+    assert L.vv_dsp_shard_range(4, 2, 2, C.byref(a), C.byref(b)) == 3        # OUT_OF_RANGE
+    assert L.vv_dsp_shard_range(4, 0, 0, C.byref(a), C.byref(b)) == 3
+    assert L.vv_dsp_shard_range(4, 2, 0, None, C.byref(b)) == 1              # NULL_POINTER
 
 
 def test_frame_shard_layout():

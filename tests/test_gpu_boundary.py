@@ -157,20 +157,22 @@ def test_dispatcher_destroy_frees_device_memory(amd):
     import torch
     L = amd.lib
     L.vv_dsp_fft_make_plan_many.argtypes = [C.c_size_t, C.c_int, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]
-    for _ in range(3):
+    x = np.zeros(2 * 1024 * 4096, np.float32)
+    x[0::2048] = 1.0
+    y = np.empty_like(x)
+
+    def cycle():
         p = C.c_void_p()
         assert L.vv_dsp_fft_make_plan_many(1024, C2C, FWD, 4096, C.byref(p)) == OK
-        assert L.vv_dsp_fft_destroy(p) == OK
-    torch.cuda.synchronize()
-    free0 = torch.cuda.mem_get_info()[0]
-    for _ in range(200):
-        p = C.c_void_p()
-        assert L.vv_dsp_fft_make_plan_many(1024, C2C, FWD, 4096, C.byref(p)) == OK
-        x = np.zeros(2 * 1024 * 4096, np.float32)
-        x[0::2048] = 1.0
-        y = np.empty_like(x)
         assert L.vv_dsp_fft_execute(p, x.ctypes.data, y.ctypes.data) == OK
         assert L.vv_dsp_fft_destroy(p) == OK
+
+    for _ in range(3):
+        cycle()                   # per-device tables and the host-path staging pool are cached once
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(200):          # a 32 MiB batch per plan: a per-plan leak would show as >= 6 GiB
+        cycle()
     assert np.allclose(y.view(np.complex64).reshape(4096, 1024), 1.0)
     torch.cuda.synchronize()
     assert free0 - torch.cuda.mem_get_info()[0] < (4 << 20)

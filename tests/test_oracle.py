@@ -312,3 +312,31 @@ def test_oracle_round2_golden(orc, golden):
     g = golden("stft_16000_n400_h160")
     assert np.array_equal(orc.spectrogram(g["x"], 400, 160), g["kiss"])
     np.testing.assert_allclose(g["kiss"], g["np64"], atol=2e-3)
+
+
+REGISTER_LENGTHS = (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)
+
+
+def test_oracle_register_golden(orc, golden):
+    """The restatement reproduces the reference's outputs in the round-3
+    fixtures bit for bit: c2c and R2C at every register-kernel length (the
+    reference's O(n^2) DFT, fft_kiss.c:76-92 via :114-116, R2C :120-147), the
+    spectrogram rows (stft.c:112-144) and the complex rows of
+    vv_dsp_stft_process (stft.c:74-92: window, then C2C)."""
+    for n in REGISTER_LENGTHS:
+        g = golden(f"register_n{n}")
+        assert np.array_equal(orc.fft(g["x"], C2C, FWD), g["c2c_fwd_kiss"]), n
+        assert np.array_equal(orc.fft(g["x"], C2C, BWD), g["c2c_bwd_kiss"]), n
+        hop = int(g["hop"][0])
+        assert np.array_equal(orc.spectrogram(g["sig"], n, hop), g["stft_mag_kiss"]), n
+        w = orc.window(1, n)
+        pad = np.concatenate([g["sig"], np.zeros(n, np.float32)])
+        for f in range(g["stft_cpx_kiss"].shape[0]):
+            fr = (pad[f * hop: f * hop + n] * w).astype(np.complex64)
+            assert np.array_equal(orc.fft(fr, C2C, FWD), g["stft_cpx_kiss"][f]), (n, f)
+        # the reference's f32 O(n^2) DFT is itself ~1e-4 relative off f64 here
+        np.testing.assert_allclose(g["c2c_fwd_kiss"], g["c2c_fwd_np64"], rtol=1e-3, atol=5e-3)
+    g = golden("register_r2c")
+    for key in (k for k in g if k.startswith("x")):
+        n = int(key[1:])
+        assert np.array_equal(orc.fft(g[key], R2C), g[f"kiss{n}"]), n

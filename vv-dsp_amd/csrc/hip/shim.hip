@@ -326,6 +326,30 @@ int vvhip_device_sync(void) {
     return ST_OK;
 }
 
+int vvhip_set_device(int device) {
+    const int nd = device_count();
+    if (nd <= 0) return fail(ST_UNSUP, "no HIP device");
+    if (device < 0 || device >= nd) return fail(ST_RANGE, "device index");
+    HIPCHK(hipSetDevice(device), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_get_device(int* device) {
+    if (!device) return ST_NULL;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    HIPCHK(hipGetDevice(device), ST_INTERNAL);
+    return ST_OK;
+}
+
+int vvhip_rows_half_device(const float* d_in, float* d_out, size_t rows, size_t n, int unpack, void* stream) {
+    if (!d_in || !d_out) return ST_NULL;
+    if (n == 0) return ST_SIZE;
+    if (d_in == d_out) return fail(ST_RANGE, "half-row pack/unpack: in and out must not alias");
+    HIPCHK(launch_rows_half(d_in, d_out, (long long)rows, (long long)n, unpack ? 1 : 0, (hipStream_t)stream),
+           ST_INTERNAL);
+    return ST_OK;
+}
+
 int vvhip_fft_plan_create(size_t n, int type, int dir, size_t batch, vvhip_fft** out) {
     if (!out) return ST_NULL;
     *out = nullptr;
@@ -402,8 +426,11 @@ void vvhip_fft_plan_destroy(vvhip_fft* p) {
 // ---------------------------------------------------------------------------
 struct vvhip_stft {
     size_t nfft = 0, hop = 0;
-    float* d_win = nullptr;
+    float* d_win = nullptr;   // on device `dev` (current at create)
+    int dev = 0;
     std::vector<float> h_win;
+    std::mutex win_mu;        // per-device window copies for device-pointer calls on other GPUs
+    std::vector<std::pair<int, float*>> other_wins;
     hipStream_t stream = nullptr;
     DevBuf b0, b1, b2;
     HostLane lanes[2];
@@ -416,10 +443,32 @@ struct vvhip_stft {
 // SIZE_MAX: all).  The signal is viewed from frame0's first sample on: frame
 // f >= frame0 of the whole signal is frame f - frame0 of that view, and the
 // zero padding past n is the same.
+// The handle's window on the calling thread's current device: a device-pointer
+// call may run on any GPU of the node (one handle, several shards), so the
+// window is copied once to each device that uses it.
+static const float* stft_window_here(vvhip_stft* h) {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return nullptr;
+    if (d == h->dev) return h->d_win;
+    std::lock_guard<std::mutex> lk(h->win_mu);
+    for (auto& w : h->other_wins)
+        if (w.first == d) return w.second;
+    float* p = nullptr;
+    if (hipMalloc(&p, sizeof(float) * (h->nfft + 2)) != hipSuccess) return nullptr;
+    if (hipMemcpy(p, h->h_win.data(), sizeof(float) * h->nfft, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    h->other_wins.push_back({d, p});
+    return p;
+}
+
 static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch, size_t ch_stride,
                            void* out, size_t out_ch_stride, int out_kind, hipStream_t s, size_t frame0 = 0,
                            size_t nframes = SIZE_MAX) {
     size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    const float* win = stft_window_here(h);
+    if (!win) return fail(ST_INTERNAL, "stft window on the current device");
     if (out_kind < 0 || out_kind > 2) return fail(ST_RANGE, "stft output kind");
     if (frame0 != 0 || nframes != SIZE_MAX) {
         if (frame0 > frames || (nframes != SIZE_MAX && nframes > frames - frame0))
@@ -434,13 +483,13 @@ static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch
     const long long NF = (long long)h->nfft;
     if (stft_fused_supported(NF)) {
         HIPCHK(launch_stft(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch, (long long)ch_stride,
-                           (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
+                           (long long)frames, win, out, (long long)out_ch_stride, s),
                ST_INTERNAL);
         return ST_OK;
     }
     if (!env_flag("VVHIP_NO_MIXED") && stft_mixed_supported(NF)) {   // 7-smooth nfft <= 4096: one kernel
         HIPCHK(launch_stft_mixed(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch,
-                                 (long long)ch_stride, (long long)frames, h->d_win, out, (long long)out_ch_stride, s),
+                                 (long long)ch_stride, (long long)frames, win, out, (long long)out_ch_stride, s),
                ST_INTERNAL);
         return ST_OK;
     }
@@ -451,7 +500,7 @@ static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch
         const size_t cnt = frames * h->nfft;
         HIPCHK(fr.alloc(8 * cnt), ST_INTERNAL);
         HIPCHK(launch_frame_gather(NF, (long long)h->hop, sig + c * ch_stride, (long long)n, 1, 0,
-                                   (long long)frames, h->d_win, (float2*)fr.p, s),
+                                   (long long)frames, win, (float2*)fr.p, s),
                ST_INTERNAL);
         if (complex_out) {
             int st = fft_run(h->nfft, 0, 1, fr.p, (float2*)out + c * out_ch_stride, frames, s);
@@ -488,6 +537,7 @@ int vvhip_stft_create(size_t nfft, size_t hop, const float* window, vvhip_stft**
     h->nfft = nfft;
     h->hop = hop;
     h->h_win.assign(window, window + nfft);
+    if (hipGetDevice(&h->dev) != hipSuccess) h->dev = 0;
     if (hipMalloc(&h->d_win, sizeof(float) * (nfft + 2)) != hipSuccess ||
         hipMemcpy(h->d_win, window, sizeof(float) * nfft, hipMemcpyHostToDevice) != hipSuccess) {
         vvhip_stft_destroy(h);
@@ -504,6 +554,7 @@ void vvhip_stft_destroy(vvhip_stft* h) {
         (void)hipStreamDestroy(h->stream);
     }
     if (h->d_win) (void)hipFree(h->d_win);
+    for (auto& w : h->other_wins) (void)hipFree(w.second);
     h->b0.release();
     h->b1.release();
     h->b2.release();
@@ -582,14 +633,16 @@ int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count
     const size_t n = count * h->nfft;
     const long long NF = (long long)h->nfft;
     hipStream_t s = (hipStream_t)stream;
+    const float* win = stft_window_here(h);
+    if (!win) return fail(ST_INTERNAL, "stft window on the current device");
     if (stft_fused_supported(NF)) {
-        HIPCHK(launch_stft(NF, NF, 1, d_frames, (long long)n, 1, 0, (long long)count, h->d_win, d_spec, 0, s),
+        HIPCHK(launch_stft(NF, NF, 1, d_frames, (long long)n, 1, 0, (long long)count, win, d_spec, 0, s),
                ST_INTERNAL);
         return ST_OK;
     }
     Scratch fr(s);
     HIPCHK(fr.alloc(8 * n), ST_INTERNAL);
-    HIPCHK(launch_frame_gather(NF, NF, d_frames, (long long)n, 1, 0, (long long)count, h->d_win,
+    HIPCHK(launch_frame_gather(NF, NF, d_frames, (long long)n, 1, 0, (long long)count, win,
                                (float2*)fr.p, s),
            ST_INTERNAL);
     return fft_run(h->nfft, 0, 1, fr.p, d_spec, count, s);
@@ -615,10 +668,12 @@ int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t cou
     if (!h || !d_spec || !d_out_add) return ST_NULL;
     if (hop == 0) return ST_SIZE;
     hipStream_t s = (hipStream_t)stream;
+    const float* win = stft_window_here(h);
+    if (!win) return fail(ST_INTERNAL, "stft window on the current device");
     const char* eo = getenv("VVHIP_ISTFT_OLD");   // A/B switch (scripts/kbench.py): IFFT to scratch + k_ola
     if (istft_fused_supported((long long)h->nfft, (long long)hop) && !(eo && *eo == '1')) {
         HIPCHK(launch_istft_fused((long long)h->nfft, (long long)hop, (const float2*)d_spec, (long long)count,
-                                  h->d_win, d_out_add, d_norm_add, s),
+                                  win, d_out_add, d_norm_add, s),
                ST_INTERNAL);
         return ST_OK;
     }
@@ -626,7 +681,7 @@ int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t cou
     HIPCHK(tf.alloc(8 * h->nfft * count), ST_INTERNAL);
     int st = fft_run(h->nfft, 0, -1, d_spec, tf.p, count, s);
     if (st) return st;
-    HIPCHK(launch_ola((long long)h->nfft, (long long)hop, (const float2*)tf.p, (long long)count, h->d_win,
+    HIPCHK(launch_ola((long long)h->nfft, (long long)hop, (const float2*)tf.p, (long long)count, win,
                       d_out_add, d_norm_add, s),
            ST_INTERNAL);
     return ST_OK;

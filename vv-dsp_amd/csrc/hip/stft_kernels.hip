@@ -80,7 +80,11 @@ __device__ __forceinline__ void pair_post(float2 Z, float2 Zm, float2* A, float2
     const vf2_t d = z - zm;   // (-Im Xb, Im Xa)
     if constexpr (MODE == 0 || MODE == 2) {
         const vf2_t dd = d * d;
-        const vf2_t m2 = s * s + dd.yx;   // (|Xa|^2, |Xb|^2)
+        // an explicit fused multiply-add: every call site rounds the same way, so
+        // bins k and N-k (the same conjugate pair) get bit-identical values
+        // wherever they are computed (lane 0's partner bins, tail pairs) -- the
+        // half-spectrum gather relies on it (vv_dsp_spectrogram_unpack_half_device)
+        const vf2_t m2 = __builtin_elementwise_fma(s, s, dd.yx);   // (|Xa|^2, |Xb|^2)
         A->x = MODE == 0 ? __builtin_amdgcn_sqrtf(m2.x) : m2.x;
         B->x = MODE == 0 ? __builtin_amdgcn_sqrtf(m2.y) : m2.y;
         A->y = B->y = 0.0f;
@@ -939,6 +943,36 @@ hipError_t launch_magnitude(const float2* in, float* out, long long count, hipSt
     long long blocks = (count + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(k_magnitude, dim3((unsigned)blocks), dim3(256), 0, s, in, out, count);
+    return hipGetLastError();
+}
+
+// Half-spectrum packing for the config-5 gather (SURVEY 8e row note 1): the
+// magnitude rows of real frames are mirror-symmetric, |X[n-k]| = |X[k]|, so
+// bins 0..n/2 carry the whole row.  Pack: [rows][n] -> [rows][n/2+1]; unpack:
+// out[k] = in[k <= n/2 ? k : n-k].  One workgroup per row (grid-stride over rows).
+__global__ void __launch_bounds__(256) k_rows_half_pack(const float* in, float* out, long long rows, long long n) {
+    const long long h = n / 2 + 1;
+    for (long long r = blockIdx.x; r < rows; r += gridDim.x) {
+        const float* src = in + r * n;
+        float* dst = out + r * h;
+        for (long long k = threadIdx.x; k < h; k += 256) dst[k] = src[k];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_rows_half_unpack(const float* in, float* out, long long rows, long long n) {
+    const long long h = n / 2 + 1;
+    for (long long r = blockIdx.x; r < rows; r += gridDim.x) {
+        const float* src = in + r * h;
+        float* dst = out + r * n;
+        for (long long k = threadIdx.x; k < n; k += 256) dst[k] = src[k < h ? k : n - k];
+    }
+}
+
+hipError_t launch_rows_half(const float* in, float* out, long long rows, long long n, int unpack, hipStream_t s) {
+    if (rows <= 0 || n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)(rows < 262144 ? rows : 262144);
+    if (unpack) hipLaunchKernelGGL(k_rows_half_unpack, dim3(grid), dim3(256), 0, s, in, out, rows, n);
+    else hipLaunchKernelGGL(k_rows_half_pack, dim3(grid), dim3(256), 0, s, in, out, rows, n);
     return hipGetLastError();
 }
 

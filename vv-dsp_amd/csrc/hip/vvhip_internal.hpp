@@ -124,6 +124,7 @@ hipError_t launch_frame_gather(long long nfft, long long hop, const float* sig, 
                                long long nch, long long ch_stride, long long frames,
                                const float* win, float2* out, hipStream_t s);
 hipError_t launch_magnitude(const float2* in, float* out, long long count, hipStream_t s);
+hipError_t launch_rows_half(const float* in, float* out, long long rows, long long n, int unpack, hipStream_t s);
 hipError_t launch_power_half(const float2* in, float* out, long long nfft, long long rows, hipStream_t s);
 // ISTFT accumulate (stft_reconstruct batch): out_add[i] += Re(t[f][i])*w[i] for frames at hop
 hipError_t launch_ola(long long nfft, long long hop, const float2* time_frames, long long count,

@@ -164,4 +164,9 @@ vv_dsp_status vv_dsp_fft_destroy(vv_dsp_fft_plan* plan) {
 }
 
 int vv_dsp_amd_device_count(void) { return vvhip_available(); }
+vv_dsp_status vv_dsp_amd_set_device(int device) { return (vv_dsp_status)vvhip_set_device(device); }
+vv_dsp_status vv_dsp_amd_get_device(int* device) {
+    if (!device) return VV_DSP_ERROR_NULL_POINTER;
+    return (vv_dsp_status)vvhip_get_device(device);
+}
 const char* vv_dsp_amd_last_error(void) { return vvhip_last_error(); }

@@ -79,6 +79,13 @@ def lib():
         getattr(L, f"vv_dsp_{f}_device").argtypes = [_vp, _sz, _sz, _vp, _vp]
     L.vvhip_fir_block_size.argtypes = [_vp, _sz]
     L.vvhip_fir_block_size.restype = _sz
+    L.vv_dsp_amd_set_device.argtypes = [C.c_int]
+    L.vv_dsp_amd_get_device.argtypes = [C.POINTER(C.c_int)]
+    L.vv_dsp_shard_range.argtypes = [_sz, _sz, _sz, C.POINTER(_sz), C.POINTER(_sz)]
+    L.vv_dsp_stft_channel_shard_device.argtypes = [_vp, C.c_int, _vp, _sz, _sz, _sz, C.c_int, _vp, _sz, _vp,
+                                                   C.POINTER(_sz)]
+    L.vv_dsp_spectrogram_pack_half_device.argtypes = [_vp, _sz, _sz, _vp, _vp]
+    L.vv_dsp_spectrogram_unpack_half_device.argtypes = [_vp, _sz, _sz, _vp, _vp]
     _lib = L
     return L
 
@@ -302,6 +309,41 @@ class FirPlan:
         if getattr(self, "h", None) and _lib is not None:
             _lib.vv_dsp_fir_plan_destroy(self.h)
             self.h = None
+
+
+def shard_range(total, world, rank):
+    """vv_dsp_shard_range: rank's contiguous channel block (first, count)."""
+    a, b = _sz(), _sz()
+    _check(lib().vv_dsp_shard_range(total, world, rank, C.byref(a), C.byref(b)), "shard_range")
+    return a.value, b.value
+
+
+def pack_half(rows, nfft, out=None, stream=None):
+    """[..., nfft] float32 device rows -> [..., nfft/2+1] (vv_dsp_spectrogram_pack_half_device)."""
+    if rows.shape[-1] != nfft:
+        raise VvError(f"pack_half: rows of {rows.shape[-1]} bins, expected {nfft}")
+    nrows = rows.numel() // nfft
+    if out is None:
+        out = torch.empty(tuple(rows.shape[:-1]) + (nfft // 2 + 1,), dtype=torch.float32, device=rows.device)
+    _expect(rows, torch.float32, nrows * nfft, "pack_half input")
+    _expect(out, torch.float32, nrows * (nfft // 2 + 1), "pack_half output")
+    _check(lib().vv_dsp_spectrogram_pack_half_device(_ptr(rows), nrows, nfft, _ptr(out), _stream(stream)),
+           "spectrogram_pack_half_device")
+    return out
+
+
+def unpack_half(half, nfft, out=None, stream=None):
+    """[..., nfft/2+1] -> [..., nfft], bin k > nfft/2 from bin nfft-k (vv_dsp_spectrogram_unpack_half_device)."""
+    if half.shape[-1] != nfft // 2 + 1:
+        raise VvError(f"unpack_half: rows of {half.shape[-1]} bins, expected {nfft // 2 + 1}")
+    nrows = half.numel() // (nfft // 2 + 1)
+    if out is None:
+        out = torch.empty(tuple(half.shape[:-1]) + (nfft,), dtype=torch.float32, device=half.device)
+    _expect(half, torch.float32, nrows * (nfft // 2 + 1), "unpack_half input")
+    _expect(out, torch.float32, nrows * nfft, "unpack_half output")
+    _check(lib().vv_dsp_spectrogram_unpack_half_device(_ptr(half), nrows, nfft, _ptr(out), _stream(stream)),
+           "spectrogram_unpack_half_device")
+    return out
 
 
 def hilbert(x, stream=None):

@@ -87,6 +87,28 @@ def gather_rows(local, total, dst=0, group=None, out=None, sizes=None):
     return None
 
 
+def gather_rows_half(local, total, nfft, dst=0, group=None, out=None, pack=None, unpack=None):
+    """gather_rows for magnitude / power rows [ch, frames, nfft] of real frames,
+    sending bins 0..nfft/2 only (SURVEY 8e row note 1: half the xGMI bytes of
+    config 5's gather).  Each rank packs its rows, the packed rows are gathered,
+    and rank `dst` expands them by mirror symmetry.  pack / unpack default to
+    the library's device kernels (vv_dsp_spectrogram_{pack,unpack}_half_device);
+    for fused-kernel rows the result equals gather_rows bit for bit."""
+    if pack is None or unpack is None:
+        import vvdsp_amd as vv
+        pack = pack or (lambda t: vv.pack_half(t, nfft))
+        unpack = unpack or (lambda t, o: vv.unpack_half(t, nfft, out=o))
+    half = pack(local)
+    got = gather_rows(half, total, dst=dst, group=group)
+    del half
+    if got is None:
+        return None
+    if out is None:
+        out = torch.empty(tuple(got.shape[:-1]) + (nfft,), dtype=got.dtype, device=got.device)
+    unpack(got, out)
+    return out
+
+
 def gather_frames(local, frames, dst=0, group=None):
     """Gather a single signal's frame shards ([f_r, width] per rank, frame_shard
     layout) into the whole [frames, width] spectrogram on rank `dst`."""
