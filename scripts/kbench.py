@@ -393,6 +393,8 @@ CASES = {
     "r2c1024": lambda: case_r2c(1024, 131072),
     "c2r1024": lambda: case_c2r(1024, 131072),
     "stft": lambda: case_stft(32, 600),
+    "stft_b": lambda: case_stft(32, 600), "stft_c": lambda: case_stft(32, 600),
+    "stft256ch": lambda: case_stft(256, 600),
     **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130)},

@@ -64,7 +64,7 @@ static hipError_t lab_firreg(const float2* H, const float* x, float* y, long lon
     const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
     const int grid = (EXP & 64) ? (int)((nch * cnt + 31) / 32) : (EXP & 128) ? capv / 8 * 8 : (int)(need < capv ? need : capv);
     hipLaunchKernelGGL((k_fir_bulk_reg<N, EXP>), dim3(grid), dim3(256), 0, s, H, x, y, nch, n, n, cnt, qf,
-                       pass_twiddles(N));
+                       pass_twiddles(N), n, (const float*)nullptr, le, qf, ql);
     return hipGetLastError();
 }
 template <int EXP>

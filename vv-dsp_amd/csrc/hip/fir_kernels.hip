@@ -329,7 +329,8 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
 template <int N, int EXP = 0>
 __global__ void __launch_bounds__(256, 4)
 k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
-               long long cnt, long long q0, const float2* gpass) {
+               long long cnt, long long q0, const float2* gpass, long long n, const float* prefix, long long lm1,
+               long long qf, long long ql) {
     using G = Geo<N>;
     static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
     constexpr int F = 4, RL = G::RL;
@@ -374,16 +375,51 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 #pragma unroll
         for (int r = 0; r < G::P; ++r) xb[r] = b[t + 64 * r];   // overlaps the next pair's block a: cached
     };
+    // Edge pairs (pair index < qf: the span starts before sample 0; >= ql: it
+    // reaches past n) take bounds-checked loads (history prefix or zeros before
+    // 0, zeros past n) and predicated stores in the same launch -- a wave-
+    // uniform branch, so the bulk pairs pay two scalar compares.
+    // An edge pair is loaded at the top of its own iteration (nothing else live
+    // then); a bulk pair is prefetched during the previous pair's stores.
+    auto is_edge = [&](long long jj) { return (jj >> 1) < qf || (jj >> 1) >= ql; };
     if constexpr (EXP & 8) {
 #pragma unroll
         for (int r = 0; r < G::P; ++r) xa[r] = xb[r] = (float)(t + r);
     }
-    load_a(c, j);
-    load_b(c, j);
+    if (!is_edge(j)) {
+        load_a(c, j);
+        load_b(c, j);
+    }
     for (; p < p_end; p += p_step) {
         const bool more = p + p_step < p_end;
         long long cn = c, jn = j;
         if (more) locate(p + p_step, &cn, &jn);
+        if (is_edge(j)) {
+            // staged through the (idle) exchange buffer with a rolled loop, so the
+            // bounds checks need no per-register address state
+            const float* xs = x + c * x_stride;
+            const float* pre = prefix ? prefix + c * lm1 : nullptr;
+            float* sf = reinterpret_cast<float*>(my);
+            auto stage = [&](long long s0, float* dst) {
+#pragma unroll 1
+                for (int k = t; k < N; k += 64) {
+                    const long long i = s0 + k;
+                    float v = 0.0f;
+                    if (i < 0) {
+                        if (pre && i >= -lm1) v = pre[lm1 + i];
+                    } else if (i < n) {
+                        v = xs[i];
+                    }
+                    sf[k] = v;
+                }
+                xsync<64>();
+#pragma unroll
+                for (int r = 0; r < G::P; ++r) dst[r] = sf[t + 64 * r];
+                xsync<64>();
+            };
+            stage(j * LOUT - LE, xa);
+            stage((j + 1) * LOUT - LE, xb);
+        }
         float2 v[G::P];
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
@@ -398,11 +434,26 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
         }
         tw.opaque();
         if constexpr (!(EXP & 2)) fft_regs<N, false, false, true, TwLastReg<N>>(u, t, my, tw);
-        if (more) {   // ahead of this pair's stores: in flight across them
+        if (more && !is_edge(jn)) {   // ahead of this pair's stores: in flight across them
             load_a(cn, jn);
             load_b(cn, jn);
         }
         float* ya = y + c * y_stride + j * LOUT - LE;   // + e: block j output (e >= LE)
+        if (is_edge(j)) {   // outputs past n are not stored
+            long long rem = n - (j * LOUT - LE + t);   // this lane's outputs below n: e < rem
+            const int rm = (int)(rem < (1 << 30) ? rem : (1 << 30));
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                const int m = q / RL + G::NPT * (q % RL);
+                if (q % RL != 0) {
+                    if (64 * m < rm) ya[t + 64 * m] = u[q].x;
+                    if (64 * m + LOUT < rm) ya[LOUT + t + 64 * m] = u[q].y;
+                }
+            }
+            c = cn;
+            j = jn;
+            continue;
+        }
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
             if constexpr (EXP & 4) {
@@ -482,14 +533,18 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     const char* er = getenv("VVHIP_FIR_REG");   // A/B switch (scripts/kbench.py): 0 = LDS-span k_fir_bulk
     const bool reg = !(er && *er == '0');
     if (ql > qf && le == N / 4 && !old && reg) {
+        // every pair of every channel in one launch: the edge pairs [0, qf) and
+        // [ql, ppc) take the kernel's bounds-checked branch (round 2 ran them as a
+        // second, latency-bound launch: 11 us of config 4's 237)
         if constexpr (FIR_BULK<N>) {
             static std::atomic<int> capc_r;
             const int cap_r = cached_grid(capc_r, (const void*)k_fir_bulk_reg<N>, 256, 0, 1LL << 40);
-            const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
+            const long long need = (nch * ppc + 3) / 4;
             const int grid = (int)(need < cap_r ? need : cap_r);
-            hipLaunchKernelGGL((k_fir_bulk_reg<N>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, cnt,
-                               qf, pN);
+            hipLaunchKernelGGL((k_fir_bulk_reg<N>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, ppc,
+                               0LL, pN, n, prefix, lm1, qf, ql);
         }
+        return hipGetLastError();
     } else if (ql > qf && le == N / 4 && !old) {
         if constexpr (FIR_BULK<N>) {
             const int cap_v2 = cached_grid(capc_v2, (const void*)k_fir_bulk<N, true>, 256, 0, 1LL << 40);

@@ -200,7 +200,9 @@ struct Row {
             const float sx = io.scale, sy = io.scale * io.isign;
             for (int e = t; e < io.nout; e += T) {
                 const float2 x = buf[e];
-                ca[e] = make_float2(x.x * sx, x.y * sy);
+                // R2C (MODE 4): Im X[n/2] = 0 exactly, as the reference's R2C (fft_kiss.c:140-145)
+                const bool nyq = MODE == 4 && 2 * e == n;
+                ca[e] = make_float2(x.x * sx, nyq ? 0.0f : x.y * sy);
             }
         } else if constexpr (MODE == 5) {
             // real length 2n from the n-point transform of its even/odd pairs:
@@ -208,7 +210,9 @@ struct Row {
             for (int e = t; e < io.nout; e += T) {
                 const float2 A = buf[e < n ? e : 0], B = cconj(buf[e == 0 || e == n ? 0 : n - e]);
                 const float2 X = split_fwd(A, B, io.twn[e]);
-                ca[e] = make_float2(X.x * io.scale, X.y * io.scale);
+                // Im X[n] (the row's Nyquist bin) = 0 exactly, as the reference (fft_kiss.c:140-145);
+                // W_2n^n rounded from double is not exactly -1 + 0i
+                ca[e] = make_float2(X.x * io.scale, e == n ? 0.0f : X.y * io.scale);
             }
         } else {
             const int lim = MODE == 3 ? n / 2 + 1 : n;
@@ -625,7 +629,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, lon
                 for (int e = lane; e < io.nout; e += 64) {
                     const float2 A = X[e < n ? e : 0], B = cconj(X[e == 0 || e == n ? 0 : n - e]);
                     const float2 Y = split_fwd(A, B, io.twn[e]);
-                    y[e] = make_float2(Y.x * io.scale, Y.y * io.scale);
+                    y[e] = make_float2(Y.x * io.scale, e == n ? 0.0f : Y.y * io.scale);   // Im Nyquist = 0
                 }
             }
         }

@@ -259,7 +259,10 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
             return ST_OK;
         }
         HIPCHK(dft_any(N, 1, in, 1, (float2*)out, NH, B, N, NH, 1.0f, s), ST_INTERNAL);
-        HIPCHK(launch_zero_nyquist_imag((float2*)out, N, B, NH, s), ST_INTERNAL);
+        // the single-pass mixed-radix kernels store Im X[n/2] = 0 themselves;
+        // the f64 DFT, Bluestein and four-step paths get it here
+        if (!(use_mixed(N) && stft_mixed_supported(N)))
+            HIPCHK(launch_zero_nyquist_imag((float2*)out, N, B, NH, s), ST_INTERNAL);
         return ST_OK;
     }
     // C2R: cpx[n/2+1] -> real[n]
