@@ -429,7 +429,9 @@ CASES = {
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152,
-                                                                         2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194]},
+                                                                         2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194,
+                                                                         16384, 16448]},
+    **{f"stftcps{c}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_CPS", str(c)) for c in (1, 2, 4, 8)},
     "stftspan": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RING", "0"),
     "stftpowspan": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RING", "0"),
     "stftcspan": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_RING", "0"),

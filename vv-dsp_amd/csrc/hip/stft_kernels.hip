@@ -300,6 +300,10 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // neighbouring pairs share an L2, while waves balance dynamically.  The
     // counter atomics are hand-counted VMEM ops like the spans and stores.
     constexpr bool DYN = (EXP & 8192) != 0;
+    // EXP bit 14 (probe): two span buffers per transform slot, the span of pair
+    // i+2 DMA'd while pair i is transformed, pair i+1's waited for before pair
+    // i's stores (LDS: 2 workgroups per CU instead of 3)
+    constexpr bool D2V = (EXP & 16384) != 0;
     constexpr bool STAGE = BULK && MODE == 0 && G::NPASS > 1 && G::T > 1;
     // power rows (N = 1024): the DIRECT stores below, keeping only the
     // 64-bin blocks under N/2 plus one lane for bin N/2
@@ -307,6 +311,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // complex rows (N = 1024): DIRECT with 8 B/lane stores, conj() for the mirror blocks
     constexpr bool CPXD = BULK && MODE == 1 && G::T == 64 && G::NPASS > 1;
     constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
+    constexpr bool D2 = D2V && GLDS && !RING && !DYN;
     constexpr int SPAN = GLDS ? ((EXP & 2048) ? N + 256 : N + N / 2) : 1;   // floats per transform: hop <= N/2
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
@@ -326,7 +331,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // N + 256 float spans, so 4 workgroups fit per CU
     constexpr int TWE = (EXP & 2048) ? 128 : TwLayout<N>::ENTRIES;
     __shared__ float2 ltab[TWE];
-    __shared__ float span_all[GLDS ? F * SPAN : 1];
+    __shared__ float span_all[GLDS ? F * SPAN * (D2 ? 2 : 1) : 1];
     using TWT = std::conditional_t<(EXP & 2048) != 0, TwMask<N>, TwTab<N>>;
     const TWT tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
@@ -443,7 +448,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // GLDS: the pair's span [fa*hop, fa*hop + hop + N) goes HBM/L2 -> LDS by
     // 16 B/lane LDS-DMA, issued right after the previous span was read, so it
     // lands while that pair is transformed -- no VGPRs held across iterations.
-    float* span = span_all + (GLDS ? slot * SPAN : 0);
+    float* span = span_all + (GLDS ? slot * SPAN * (D2 ? 2 : 1) : 0);
+    float* span_dst = span;   // where issue_span puts the next span (D2: alternates)
     // Pairs that reach past the end of the signal (the zero-padded tail, at
     // most a few per channel) fill the span with ordinary bounds-checked loads
     // and LDS stores instead: the compiler waits on those itself, and being
@@ -454,9 +460,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         if (ff * hop + len <= n) {
             for (int u = t >> 6; u * 256 < ((EXP & 64) ? 2 * (int)hop : len); u += G::T / 64) {
                 const int e = u * 256 + lane * 4;
-                if constexpr (EXP & 128) glds16_pol<1>(s0 + (e < len ? e : 0), span + u * 256);
-                else if constexpr (EXP & 256) glds16_pol<2>(s0 + (e < len ? e : 0), span + u * 256);
-                else glds16(s0 + (e < len ? e : 0), span + u * 256);
+                if constexpr (EXP & 128) glds16_pol<1>(s0 + (e < len ? e : 0), span_dst + u * 256);
+                else if constexpr (EXP & 256) glds16_pol<2>(s0 + (e < len ? e : 0), span_dst + u * 256);
+                else glds16(s0 + (e < len ? e : 0), span_dst + u * 256);
             }
         } else {
             const long long left = n - ff * hop;   // samples of this span inside the signal
@@ -465,7 +471,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 vf4_t q;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) q[k] = e + k < left ? s0[e + k] : 0.0f;
-                *reinterpret_cast<vf4_t*>(span + u * 256 + lane * 4) = q;
+                *reinterpret_cast<vf4_t*>(span_dst + u * 256 + lane * 4) = q;
             }
         }
     };
@@ -505,6 +511,18 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     };
     // the first span's DMA is in flight while the block stages its twiddles
     if (any) load_pair(c, fa);
+    if constexpr (D2) {   // and the second pair's, into the other buffer
+        if (any && p + p_step < p_end) {
+            long long c1, f1;
+            locate(p + p_step, &c1, &f1);
+            span_dst = span + SPAN;
+            issue_span(c1, f1);
+        }
+    }
+    // D2: LDS-DMA ops of one full span (hop <= N/2), and whether the span issued
+    // this iteration is in flight (a tail span is filled synchronously)
+    const int nd = D2 ? (int)((N + hop + 255) >> 8) : 0;
+    bool d2_async = false;
     if constexpr (DYN) {
         if (any && pn < pairs) grab();   // -> the pair after pn
     }
@@ -572,6 +590,26 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 if (pnn < pairs) grab();
             }
             pn = pnn;
+        } else if constexpr (D2) {
+            // this pair's span is complete (waited for before the previous
+            // pair's stores, or by the prologue); after reading it, its buffer
+            // takes the span of the pair two ahead
+            float* cur = span + (kk & 1) * SPAN;
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = cur[t + r * G::T];
+                xb[r] = cur[hop + t + r * G::T];
+            }
+            lgkm_wait0();   // span read before it is refilled
+            d2_async = false;
+            const long long p2 = p + 2 * p_step;
+            if (p2 < p_end) {
+                long long c2, f2;
+                locate(p2, &c2, &f2);
+                span_dst = cur;
+                issue_span(c2, f2);
+                d2_async = f2 * hop + N + hop <= n;
+            }
         } else if constexpr (GLDS) {
             // younger than this span's DMA: only the previous pair's NST stores
             vm_wait<NST>();
@@ -598,6 +636,16 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
         if constexpr (!(EXP & 2)) fft_regs<N, true, true, RI, TWT, (EXP & 1) != 0>(v, t, my, tw);
+        if constexpr (D2) {
+            // the next pair's span: younger than it are the previous pair's NST
+            // stores and, when in flight, the span just issued
+            if (more) {
+                if (!d2_async) vm_wait<NST>();
+                else if (nd == 5) vm_wait<NST + 5>();
+                else if (nd == 6) vm_wait<NST + 6>();
+                else vm_wait<NST>();
+            }
+        }
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
         char* rowb = rowa + ROW * ES;
         const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
@@ -653,6 +701,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             rs = rsn;
             ++kk;
         }
+        if constexpr (D2) ++kk;
     }
     if constexpr (DYN) {   // the XCD's last wave out resets its counters for the next launch
         vm_wait<0>();
@@ -803,6 +852,11 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const int cap0 = cached_grid(capc[0], (const void*)k_stft_pair<N, MODE, 0>, WG, 0, 1LL << 40);
         long long cps = (bulk_pairs + (long long)F * cap0 - 1) / ((long long)F * cap0);
         cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
+        {   // A/B switch (scripts/kbench.py stftcps*): an upper bound on the pairs per slot
+            const char* ec = getenv("VVHIP_STFT_CPS");
+            const long long cmax = ec && *ec ? atoll(ec) : 0;
+            if (cmax > 0 && cps > cmax) cps = cmax;
+        }
         float* sink = store_sink();
         if (!sink) return hipErrorOutOfMemory;
         auto launch = [&](auto kern, int var, long long pair0, long long cnt) {
