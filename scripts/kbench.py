@@ -135,8 +135,9 @@ def lowpass(taps=257, fc=0.25):
 
 def case_fir(nch, n, taps=257):
     h = lowpass(taps)
-    x = torch.rand(nch, n, device="cuda") * 2 - 1
-    y = torch.empty_like(x)
+    if ("fir", nch, n) not in _SHARED:   # shared by the A/B cases (same placement)
+        _SHARED[("fir", nch, n)] = (torch.rand(nch, n, device="cuda") * 2 - 1, torch.empty(nch, n, device="cuda"))
+    x, y = _SHARED[("fir", nch, n)]
     p = vv.FirPlan(h)
     return (lambda: p(x, out=y)), 2 * nch * n * 4, (x, y, p)
 
@@ -268,11 +269,12 @@ def case_firlab(e, nch=8, n=1 << 24, fn="firlab_run"):
     run = getattr(lib, fn)
     run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                ctypes.c_longlong, ctypes.c_void_p]
-    x = torch.rand(nch, n, device="cuda") * 2 - 1
-    y = torch.empty_like(x)
-    hp = torch.zeros(1024)
-    hp[:257] = lowpass(257)
-    H = (torch.fft.fft(hp.double()) / 1024).to(torch.complex64).cuda()   # config 4's spectrum
+    if ("firlab", nch, n) not in _SHARED:   # one buffer set for every FIR lab case (same placement)
+        hp = torch.zeros(1024)
+        hp[:257] = lowpass(257)
+        _SHARED[("firlab", nch, n)] = (torch.rand(nch, n, device="cuda") * 2 - 1, torch.empty(nch, n, device="cuda"),
+                                       (torch.fft.fft(hp.double()) / 1024).to(torch.complex64).cuda())
+    x, y, H = _SHARED[("firlab", nch, n)]   # H: config 4's spectrum
     s = torch.cuda.current_stream().cuda_stream
     return (lambda: run(e, H.data_ptr(), x.data_ptr(), y.data_ptr(), n, nch, s)), 2 * nch * n * 4, \
         (x, y, H, lib)
@@ -426,7 +428,8 @@ CASES = {
        for i in (0, 4, 64, 1024, 2052) for o in (0, 4, 8, 64, 1024, 2052, 4100)},
     **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
-    **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130)},
+    **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
+                                                                          256, 320)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152,
                                                                          2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194,

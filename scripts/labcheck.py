@@ -12,6 +12,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vv-dsp_amd"))
 import vvdsp_amd as vv  # noqa: E402
 
+if sys.argv[1] == "fir":   # python scripts/labcheck.py fir <EXP>: k_fir_bulk_reg variant vs EXP 0
+    e = int(sys.argv[2])
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
+    lib.firreglab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_longlong, ctypes.c_longlong, ctypes.c_void_p]
+    nch, n = 3, (1 << 20) + 12345
+    x = torch.rand(nch, n, device="cuda") * 2 - 1
+    H = torch.complex(torch.rand(1024, device="cuda"), torch.rand(1024, device="cuda"))
+    s = torch.cuda.current_stream().cuda_stream
+    ref = torch.full_like(x, -2.0)
+    assert lib.firreglab_run(0, H.data_ptr(), x.data_ptr(), ref.data_ptr(), n, nch, s) == 0
+    for rep in range(2):
+        out = torch.full_like(x, -1.0)
+        assert lib.firreglab_run(e, H.data_ptr(), x.data_ptr(), out.data_ptr(), n, nch, s) == 0
+        torch.cuda.synchronize()
+        # the lab launch covers the bulk pairs only (the edge pairs' outputs stay -2 / -1)
+        ref_w = ref != -2.0
+        out = torch.where(ref_w, out, ref)
+        ne = out != ref
+        bad = ne.sum().item()
+        d = (out - ref).abs().max().item()
+        idx = ne.nonzero()[:5].tolist()
+        print(f"firreglab{e} launch {rep}: {bad} of {out.numel()} values differ, max |diff| {d:.3g} "
+              f"(max |y| {ref.abs().max().item():.3g}), first at {idx}")
+        assert d <= 1e-5 * ref.abs().max().item()   # same arithmetic, possibly other contractions
+    sys.exit(0)
 e = int(sys.argv[1])
 nch = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 sec = int(sys.argv[3]) if len(sys.argv) > 3 else 60
