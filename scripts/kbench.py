@@ -104,10 +104,12 @@ def case_stft_place(in_kb, out_kb, nch=32, seconds=600):
 def case_stft_n(nch, seconds, nfft, hop, sr=16000):
     """magnitude rows at any nfft (non-power-of-two: frame gather + mixed-radix FFT + |X|)"""
     n = seconds * sr
-    sig = torch.rand(nch, n, device="cuda") * 2 - 1
     st = vv.Stft(nfft, hop)
     fr = st.frames(n)
-    out = torch.empty(nch, fr, nfft, device="cuda")
+    key = ("stftn", nch, n, nfft, hop)
+    if key not in _SHARED:   # shared by the A/B cases of one shape (same placement)
+        _SHARED[key] = (torch.rand(nch, n, device="cuda") * 2 - 1, torch.empty(nch, fr, nfft, device="cuda"))
+    sig, out = _SHARED[key]
     return (lambda: st.spectrogram(sig, out=out)), nch * n * 4 + nch * fr * nfft * 4, (sig, out, st)
 
 
@@ -405,6 +407,12 @@ CASES = {
     **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
     **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
     "stft400": lambda: case_stft_n(32, 600, 400, 160),
+    # speech lengths at 48 kHz (hop = nfft / 4), and VVHIP_MIX_VAR=1 (the conjugate-symmetric row emit)
+    **{f"sq{nf}": (lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000))
+       for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
+    **{f"sq{nf}v1": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_MIX_VAR", "1")
+       for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
+    "stft400v1": with_env(lambda: case_stft_n(32, 600, 400, 160), "VVHIP_MIX_VAR", "1"),
     **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 960, 1000)},
     **{f"r2cmix{n}gen": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_STFT_SQ", "0") for n in (400, 960)},
     **{f"r2cmix{n}full": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_MIX_R2C_FULL", "1") for n in (400, 1000)},
