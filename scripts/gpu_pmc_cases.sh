@@ -18,5 +18,5 @@ for grp in "$@"; do
   if [ $rc -ne 0 ]; then echo "pass $i rc=$rc"; tail -5 $O/p$i.log; exit $rc; fi
   echo "== pass $i: $grp"
   grep '^{' $O/p$i.log
-  python3 scripts/pmc_cases.py $O/p$i --cases "$cases"
+  python3 scripts/pmc_cases.py $O/p$i --cases "$cases" --kernel "${KERNEL:-vvh::k_stft_pair}"
 done

@@ -412,7 +412,9 @@ CASES = {
        for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
     **{f"sq{nf}v1": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_MIX_VAR", "1")
        for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
-    "stft400v1": with_env(lambda: case_stft_n(32, 600, 400, 160), "VVHIP_MIX_VAR", "1"),
+    **{f"sq{nf}lb4": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_SQ_LB4", "1")
+       for nf in (320, 480)},
+    **{f"mix{n}lb4": with_env(lambda n=n: case_c2c(n, (1 << 26) // n), "VVHIP_SQ_LB4", "1") for n in (320, 480)},
     **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 960, 1000)},
     **{f"r2cmix{n}gen": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_STFT_SQ", "0") for n in (400, 960)},
     **{f"r2cmix{n}full": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_MIX_R2C_FULL", "1") for n in (400, 1000)},
@@ -444,6 +446,8 @@ CASES = {
                                                                          16384, 16448]},
     **{f"stftcps{c}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_CPS", str(c)) for c in (1, 2, 4, 8)},
     "stftspan": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RING", "0"),
+    "stftchunk": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DYN", "0"),
+    "stftchunk256ch": with_env(lambda: case_stft(256, 600), "VVHIP_STFT_DYN", "0"),
     "stftpowspan": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RING", "0"),
     "stftcspan": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_RING", "0"),
     "stft60span": with_env(lambda: case_stft(1, 60), "VVHIP_STFT_RING", "0"),

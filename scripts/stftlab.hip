@@ -23,16 +23,9 @@ static hipError_t lab_launch(const float* sig, long long n, long long nch, const
     const long long chunk = cps * F;
     const long long grid = (EXP & (4096 | 8192)) ? (cap0 / 8) * 8 : (pairs + chunk - 1) / chunk;
     float* sink = store_sink();
-    if constexpr ((EXP & 8192) != 0) {   // XCD counters (zero once; the kernel's last waves reset them)
-        static unsigned* ctr = nullptr;
-        if (!ctr) {
-            if (hipMalloc(&ctr, 32 * 32 * sizeof(unsigned)) != hipSuccess) return hipErrorOutOfMemory;
-            (void)hipMemset(ctr, 0, 32 * 32 * sizeof(unsigned));
-        }
-        sink = reinterpret_cast<float*>(ctr);
-    }
+    unsigned* ctr = (EXP & 8192) ? stream_counters(s) : nullptr;   // XCD counters (the kernel's last waves reset them)
     hipLaunchKernelGGL((k_stft_pair<N, 0, 0, EXP>), dim3((unsigned)grid), dim3(256), 0, s, sig, n, nch, n, frames, hop,
-                       0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, sink);
+                       0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, sink, ctr);
     return hipGetLastError();
 }
 // config 4's bulk launch (8 ch x 2^24, 257 taps: N 1024, le 256) of k_fir_bulk<1024, true, EXP>

@@ -1,0 +1,70 @@
+"""The dynamically scheduled STFT walk (k_stft_pair VAR 4: persistent grid,
+per-(device, stream) work counters that the kernel's last waves reset) against
+the chunked launch it replaces for large magnitude jobs (VVHIP_STFT_DYN=0):
+bit-identical rows, repeated launches (the counters must come back to zero),
+two streams at once (each its own counter block), the zero-padded tail and a
+missing second frame (odd frame count), and sampled rows against NumPy f64 at
+the harness tolerance (stft.c:112-144, python/test_fft.py:37-38)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NCH = 7
+N = 7 * 60 * 48000 + 333   # 78,749 frames per channel (1 + (n - 1024 + 256) // 256): odd, zero-padded tail
+
+
+@pytest.fixture(scope="module")
+def job(vdev):
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(11)
+    sig = torch.rand(NCH, N, device="cuda", generator=g) * 2 - 1
+    st = vdev.Stft(1024, 256)
+    os.environ["VVHIP_STFT_DYN"] = "0"
+    try:
+        ref = st.spectrogram(sig).clone()
+    finally:
+        os.environ["VVHIP_STFT_DYN"] = ""
+    torch.cuda.synchronize()
+    return sig, st, ref
+
+
+def test_dynamic_walk_equals_chunked(job):
+    import torch
+    sig, st, ref = job
+    assert ref.shape == (NCH, 78749, 1024) and st.frames(N) == 78749
+    out = torch.full_like(ref, -1.0)
+    for _ in range(3):   # the counters are reset by each launch's last waves
+        out.fill_(-1.0)
+        st.spectrogram(sig, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+
+
+def test_dynamic_walk_two_streams(job):
+    import torch
+    sig, st, ref = job
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    o1, o2 = torch.full_like(ref, -1.0), torch.full_like(ref, -1.0)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        st.spectrogram(sig, out=o1, stream=s1)
+        st.spectrogram(sig, out=o2, stream=s2)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, ref)
+    assert torch.equal(o2, ref)
+
+
+def test_dynamic_walk_rows_vs_numpy(job, orc):
+    sig, st, ref = job
+    out = st.spectrogram(sig)
+    w = orc.window(1, 1024).astype(np.float64)
+    for c in (0, NCH - 1):
+        x = sig[c].cpu().numpy().astype(np.float64)
+        pad = np.concatenate([x, np.zeros(1024)])
+        frames = [0, 1, 4097, 39374, 78744, 78747, 78748]   # the last ones run past the end
+        X = np.abs(np.fft.fft(np.stack([pad[f * 256:f * 256 + 1024] for f in frames]) * w, axis=1))
+        np.testing.assert_allclose(out[c][frames].cpu().numpy(), X, rtol=5e-5, atol=5e-5)

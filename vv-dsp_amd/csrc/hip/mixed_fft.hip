@@ -518,18 +518,23 @@ __device__ __forceinline__ void reg_dft(float2* v) {
     }
 }
 
-template <int N1, int N2>
+template <int N1, int N2, int MODE = 0>
 struct Sq {
     static constexpr int N = N1 * N2;
     static constexpr int TT = N1 > N2 ? N1 : N2;   // lanes per transform
     static constexpr int TPW = 64 / TT;            // transforms per wave
     static constexpr int P2 = N2 + 1;              // padded pass-1 row (k1 rows of N2)
     static constexpr int LT = N1 * P2 > N ? N1 * P2 : N;   // float2 per transform
-    static constexpr int LDS = 4 * TPW * LT + N + N / 2;   // + the W_n table and the window
-    // workgroups per CU the LDS allows, at most 3 (<= 168 VGPRs without spills;
-    // 4 would need <= 128 and spills): latency-bound, so occupancy matters
+    // + the W_n table and the window (MODE 5: W_2n^k, k <= n, for the split step)
+    static constexpr int LDS = 4 * TPW * LT + N + (MODE == 5 ? N + 1 : N / 2);
+    // workgroups per CU the LDS allows, at most 3 (<= 168 VGPRs), or 4 when
+    // both factors are <= 20 (the transform's registers then fit 128 VGPRs
+    // without spills: 320 = 16 x 20 measured 3.4 % faster at 4 than at 3; 480 =
+    // 20 x 24 spills at 128 and measured 21 % slower, profiles/r03_kbench_sq_lb4.jsonl).
+    // Latency-bound, so occupancy matters.
     static constexpr int FIT = (160 * 1024) / (8 * LDS);
-    static constexpr int LB = FIT < 3 ? (FIT < 1 ? 1 : FIT) : 3;
+    static constexpr int CAP = (N1 <= 20 && N2 <= 20) ? 4 : 3;
+    static constexpr int LB = FIT < CAP ? (FIT < 1 ? 1 : FIT) : CAP;
 };
 
 // MODE 0 c2c rows (`pairs` = rows), MODE 5 real rows of 2n (even/odd pairs
@@ -537,16 +542,20 @@ struct Sq {
 // rows, 3 |X|^2 for bins 0..n/2 (as k_fft_mixed).  A wave reads its rows whole
 // before it writes them, so in == out is safe.
 template <int N1, int N2, int MODE>
-__global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, long long pairs, const float2* __restrict__ gtab) {
-    using S = Sq<N1, N2>;
+__global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO io, long long pairs, const float2* __restrict__ gtab) {
+    using S = Sq<N1, N2, MODE>;
     constexpr int n = S::N, TT = S::TT, TPW = S::TPW, P2 = S::P2, LT = S::LT;
     constexpr int W = MODE == 3 ? n / 2 + 1 : n;   // bins per row
     __shared__ float2 sm[S::LDS];
     float2* const tab = sm + 4 * TPW * LT;
     float* const lwin = reinterpret_cast<float*>(tab + n);
+    float2* const ltw = tab + n;   // MODE 5 (in the window's place)
     for (int i = threadIdx.x; i < n; i += 256) {
         tab[i] = gtab[i];
         if constexpr (MODE != 0 && MODE != 5) lwin[i] = io.win[i];
+    }
+    if constexpr (MODE == 5) {   // the split step's W_2n^k from LDS, not a dependent global load per bin
+        for (int i = threadIdx.x; i <= n; i += 256) ltw[i] = io.twn[i];
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / TT, t = lane - slot * TT;
@@ -628,7 +637,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2>::LB)) k_stft_sq(MixIO io, lon
                 float2* y = io.out + q * io.out_dist;
                 for (int e = lane; e < io.nout; e += 64) {
                     const float2 A = X[e < n ? e : 0], B = cconj(X[e == 0 || e == n ? 0 : n - e]);
-                    const float2 Y = split_fwd(A, B, io.twn[e]);
+                    const float2 Y = split_fwd(A, B, ltw[e]);
                     y[e] = make_float2(Y.x * io.scale, e == n ? 0.0f : Y.y * io.scale);   // Im Nyquist = 0
                 }
             }
@@ -756,7 +765,7 @@ template <int N1, int N2, int MODE>
 hipError_t run_stft_sq(const MixIO& io, long long pairs, hipStream_t s) {
     const float2* tab = twiddle_table(N1 * N2);
     if (!tab) return hipErrorOutOfMemory;
-    constexpr int TPW = Sq<N1, N2>::TPW;
+    constexpr int TPW = Sq<N1, N2, MODE>::TPW;
     const long long work = (pairs + 4 * TPW - 1) / (4 * TPW);
     const int grid = persistent_grid((const void*)k_stft_sq<N1, N2, MODE>, 256, 0, work);
     hipLaunchKernelGGL((k_stft_sq<N1, N2, MODE>), dim3(grid), dim3(256), 0, s, io, pairs, tab);

@@ -282,14 +282,15 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
 // with nt / sc1, bits 9/10 row stores with sc1 / nt (default sc0 sc1 nt).  Results are
 // wrong under bits 0-4 and 6.
 template <int N, int MODE, int VAR, int EXP = 0>
-__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3)) ? ((EXP & 2048) ? 4 : 3) : 1)
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4)) ? ((EXP & 2048) ? 4 : 3) : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
-            long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink) {
+            long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink,
+            unsigned* ctrs) {
     using G = Geo<N>;
     using Mi = Mirror<N>;
     constexpr bool TAIL = VAR == 2;
-    constexpr bool BULK = VAR == 0 || VAR == 3;
+    constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4;
     // VAR 3: VAR 0 with each wave walking a contiguous run of pairs and its
     // span kept as a ring of 256-float chunks (hop % 256 == 0): a pair DMAs only
     // its 2*hop new samples instead of the whole N + hop span
@@ -299,7 +300,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // (k / DB) * 8 DB + xcd * DB + k % DB, so the chip works on one moving band and
     // neighbouring pairs share an L2, while waves balance dynamically.  The
     // counter atomics are hand-counted VMEM ops like the spans and stores.
-    constexpr bool DYN = (EXP & 8192) != 0;
+    // VAR 4 (the library's bulk launch for magnitude rows of large jobs) is
+    // this walk: a persistent grid, counters from stream_counters()
+    constexpr bool DYN = (EXP & 8192) != 0 || VAR == 4;
     // EXP bit 14 (probe): two span buffers per transform slot, the span of pair
     // i+2 DMA'd while pair i is transformed, pair i+1's waited for before pair
     // i's stores (LDS: 2 workgroups per CU instead of 3)
@@ -415,7 +418,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // one counter per (XCD, slot): 32 streams, so no address takes more than one
     // atomic per workgroup of its XCD per pair
     const int stream = __builtin_amdgcn_readfirstlane((int)(blockIdx.x & 7) * F + slot);
-    unsigned* const ctr = DYN ? reinterpret_cast<unsigned*>(sink) + 32 * stream : nullptr;
+    unsigned* const ctr = DYN ? ctrs + 32 * stream : nullptr;
     constexpr long long DB = 64;
     auto band_pair = [&](unsigned k) -> long long {
         return (long long)(k / DB) * (8 * F * DB) + (long long)stream * DB + (long long)(k % DB);
@@ -840,7 +843,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         long long mpc = (nfull < frames ? nfull : frames) / 2;
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
-        static std::atomic<int> capc[4];   // zero-initialised (static storage)
+        static std::atomic<int> capc[5];   // zero-initialised (static storage)
         // The bulk launch is NOT persistent: one workgroup per `cps` pairs per
         // transform slot, so the hardware dispatcher balances the CUs and the
         // launch has no straggler tail (measured 8-13 % faster than the
@@ -859,6 +862,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         }
         float* sink = store_sink();
         if (!sink) return hipErrorOutOfMemory;
+        unsigned* ctrs = nullptr;
         auto launch = [&](auto kern, int var, long long pair0, long long cnt) {
             const int capv = cached_grid(capc[var], (const void*)kern, WG, 0, 1LL << 40);
             const long long need = (nch * cnt + F - 1) / F;
@@ -868,6 +872,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 chunk = cps * F;
                 grid = (nch * cnt + chunk - 1) / chunk;
             }
+            if (var == 4) grid = capv / 8 * 8;   // persistent, the same number of blocks per XCD group
             if (var == 3) {   // run length (pairs), a divisor of cps; VVHIP_STFT_RUN overrides (A/B)
                 long long rl = cps;
                 const char* eru = getenv("VVHIP_STFT_RUN");
@@ -876,7 +881,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 chunk |= rl << 40;
             }
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0,
-                               cnt, win, out, out_ch_stride, pN, tN, chunk, sink);
+                               cnt, win, out, out_ch_stride, pN, tN, chunk, sink, ctrs);
         };
         // 16 B aligned output rows allow the staged 16 B/lane stores
         // (power rows are n/2+1 floats: their direct stores are dwords, 4 B suffice;
@@ -901,7 +906,26 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const char* er = getenv("VVHIP_STFT_RING");
         const bool ring = Geo<N>::T == 64 && hop % 256 == 0 &&
                           (er && *er ? *er == '1' : MODE == 2);
-        if (aligned && FUSE_TAIL && ring) {
+        // Magnitude rows of large jobs: the persistent dynamic walk (VAR 4) --
+        // each wave takes its next pair from a per-(XCD group, slot) counter, so
+        // the chip sweeps one moving band of pairs with the load balanced on the
+        // fly (-1.6 % against the chunked launch in two same-buffer measurements,
+        // profiles/r03_kbench_ablation_samebuf.jsonl lab8192; bit-identical rows).
+        // VVHIP_STFT_DYN = 0 keeps the chunked VAR 0 (A/B switch, read per call).
+        const char* ed = getenv("VVHIP_STFT_DYN");
+        bool dyn = false;
+        if constexpr (MODE == 0 && Geo<N>::T == 64) {
+            const int capd = cached_grid(capc[4], (const void*)k_stft_pair<N, MODE, 4>, WG, 0, 1LL << 40);
+            dyn = aligned && FUSE_TAIL && !ring && !(ed && *ed == '0') && capd >= 8 &&
+                  bulk_pairs >= 16LL * F * capd;   // >= 16 pairs per wave: the band walk pays off
+            if (dyn) {
+                ctrs = stream_counters(s);
+                if (!ctrs) return hipErrorOutOfMemory;
+            }
+        }
+        if (dyn) {
+            if constexpr (MODE == 0 && Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 4>, 4, 0LL, ppc);
+        } else if (aligned && FUSE_TAIL && ring) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 3>, 3, 0LL, ppc);
         } else if (aligned && FUSE_TAIL) {
             launch(k_stft_pair<N, MODE, 0>, 0, 0LL, ppc);

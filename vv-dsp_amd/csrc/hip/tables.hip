@@ -17,7 +17,7 @@ namespace {
 std::mutex g_mu;
 std::map<std::tuple<int, int, long long>, void*> g_cache;   // (device, kind, n) -> device buffer
 
-enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2, KIND_SINK = 3, KIND_SPLIT = 4 };
+enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2, KIND_SINK = 3, KIND_SPLIT = 4, KIND_CTR = 5 };
 
 int current_device() {
     int dev = 0;
@@ -106,6 +106,17 @@ const float2* twiddle_split(long long n, int* lo_bits) {
 
 // Write sink for lanes whose store has no destination in a kernel that keeps
 // its count of memory instructions fixed (SINK_FLOATS floats, never read).
+// Work counters of the dynamically scheduled STFT launch (k_stft_pair VAR 4),
+// one zeroed block per (device, stream): the kernel's last wave of each counter
+// stream resets it, so launches ordered on one stream find it zero, and launches
+// on different streams never share one.
+unsigned* stream_counters(hipStream_t s) {
+    return (unsigned*)cached(KIND_CTR, (long long)(uintptr_t)s, sizeof(unsigned) * STFT_CTR_WORDS,
+                             [](unsigned char* b) {
+                                 for (size_t i = 0; i < sizeof(unsigned) * STFT_CTR_WORDS; ++i) b[i] = 0;
+                             });
+}
+
 float* store_sink() {
     return (float*)cached(KIND_SINK, 0, sizeof(float) * SINK_FLOATS, [](unsigned char* b) {
         for (size_t i = 0; i < sizeof(float) * SINK_FLOATS; ++i) b[i] = 0;

@@ -64,6 +64,9 @@ int mel_chunk_schedule(const int* meta, int n_mels, std::vector<int>* chunks, st
 // with nothing to write, in kernels that hand-count their memory operations.
 constexpr size_t SINK_FLOATS = 1u << 18;   // 1 MiB = 4096 waves x 64 lanes
 float* store_sink();
+// per-(device, stream) zeroed work counters of the dynamic STFT walk (32 streams x 32 words)
+constexpr size_t STFT_CTR_WORDS = 32 * 32;
+unsigned* stream_counters(hipStream_t s);
 // ---- batched framing (framing_kernels.hip), framing.c:58-146 semantics
 long long reflect_sample(long long idx, long long n);   // framing.c:21-56, host side (span bounds)
 hipError_t launch_fetch_frames(const float* sig, long long base, long long n, float* out, long long len,
