@@ -320,7 +320,7 @@ def kernel_traffic(prefixes, per_step_calls=None, channels=None):
 
 
 def hbm_traffic(channels):
-    return kernel_traffic(["vvh::k_stft_pair<1024, 0"], channels=channels)
+    return kernel_traffic(["vvh::k_stft_pair<1024, 0, 4"], channels=channels)
 
 
 def gather_leg(out, total_ch, compute_s, frames_per_step, rank, half=True):
@@ -510,10 +510,10 @@ def main():
             "nfft": NFFT, "hop": HOP, "window": "hann (symmetric, window.c:25-36)",
             "output": "[ch][frame][1024] f32 magnitudes (stft.c:133-139)",
             "parallelism": f"dp{world} (channel shards, no data-path collective)"},
-        "roofline": {"kernel": "vvh::k_stft_pair<1024,0,0> (LDS-DMA frame spans + Hann + two frames per "
-                               "1024-pt complex FFT + |X| rows as full-line streaming stores; the zero-padded "
-                               "tail pairs run in the same launch); kernel_ms = HIP events around the launch on "
-                               "the launch stream",
+        "roofline": {"kernel": "vvh::k_stft_pair<1024,0,4> (persistent dynamic band walk; LDS-DMA frame spans + "
+                               "Hann + two frames per 1024-pt complex FFT + |X| rows as full-line streaming stores; "
+                               "the zero-padded tail pairs run in the same launch); kernel_ms = HIP events around "
+                               "the launch on the launch stream",
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
