@@ -410,8 +410,8 @@ CASES = {
     # speech lengths at 48 kHz (hop = nfft / 4), and VVHIP_MIX_VAR=1 (the conjugate-symmetric row emit)
     **{f"sq{nf}": (lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000))
        for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
-    **{f"sq{nf}v1": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_MIX_VAR", "1")
-       for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
+    **{f"sq{nf}v{v}": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_MIX_VAR", str(v))
+       for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960) for v in (1, 3, 4, 5, 6)},
     **{f"sq{nf}lb4": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_SQ_LB4", "1")
        for nf in (320, 480)},
     **{f"mix{n}lb4": with_env(lambda n=n: case_c2c(n, (1 << 26) // n), "VVHIP_SQ_LB4", "1") for n in (320, 480)},

@@ -140,6 +140,7 @@ struct MixIO {
     const float* win;
     const float2* twn;   // MODE 5: W_n^k, k < n (n = 2 * the transform length)
     int var;   // A/B switch (VVHIP_MIX_VAR)
+    int a16;   // STFT: output rows 16 B aligned (base and channel stride), for 16 B/lane row stores
 };
 
 template <int MODE>
@@ -525,6 +526,8 @@ struct Sq {
     static constexpr int TPW = 64 / TT;            // transforms per wave
     static constexpr int P2 = N2 + 1;              // padded pass-1 row (k1 rows of N2)
     static constexpr int LT = N1 * P2 > N ? N1 * P2 : N;   // float2 per transform
+    // magnitude rows (MODE 1) staged for 16 B/lane stores: whole float4s per row, 16 B aligned buffers
+    static constexpr bool STG = MODE == 1 && N % 4 == 0 && LT % 2 == 0;
     // + the W_n table and the window (MODE 5: W_2n^k, k <= n, for the split step)
     static constexpr int LDS = 4 * TPW * LT + N + (MODE == 5 ? N + 1 : N / 2);
     // workgroups per CU the LDS allows, at most 3 (<= 168 VGPRs), or 4 when
@@ -546,7 +549,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
     using S = Sq<N1, N2, MODE>;
     constexpr int n = S::N, TT = S::TT, TPW = S::TPW, P2 = S::P2, LT = S::LT;
     constexpr int W = MODE == 3 ? n / 2 + 1 : n;   // bins per row
-    __shared__ float2 sm[S::LDS];
+    __shared__ __attribute__((aligned(16))) float2 sm[S::LDS];
     float2* const tab = sm + 4 * TPW * LT;
     float* const lwin = reinterpret_cast<float*>(tab + n);
     float2* const ltw = tab + n;   // MODE 5 (in the window's place)
@@ -663,7 +666,56 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
         // emitting each row bin by bin (480-point rows 6.00 -> 4.92 ms for 32 ch x
         // 10 min at 48 kHz, profiles/r03_kbench_sq_sym.jsonl); n >= 900 keeps the
         // per-bin emit of both rows below (2 % faster there).
-        if constexpr ((MODE == 1 || MODE == 2) && n < 900) {
+        if constexpr (S::STG) {
+            // Magnitude rows staged in the transform's own (now consumed) LDS
+            // buffer and written as 16 B/lane stores of the pair's 2W-float run:
+            // |X| of bins e and n - e of both rows from one read of Z[e], Z[n-e]
+            // (conjugate symmetry), held in registers until every read is done.
+            // 12-18 % faster than the 4 B/lane stores of the symmetric emit below
+            // at 400 / 480 / 720 / 900 / 960 (profiles/r03_kbench_sq_stage.jsonl);
+            // the launcher takes the generic kernel for rows that are not 16 B aligned.
+            constexpr int IT = (n / 2 + 1 + 63) / 64;
+#pragma unroll
+            for (int s = 0; s < TPW; ++s) {
+                const long long q = g + s;
+                if (q >= pairs) break;   // wave-uniform
+                float* const X = reinterpret_cast<float*>(wbuf + s * LT);
+                const float2* const Z = wbuf + s * LT;
+                float ma[IT], mb[IT];
+#pragma unroll
+                for (int i = 0; i < IT; ++i) {
+                    const int e = lane + 64 * i;
+                    const int ec = 2 * e <= n ? e : 0;
+                    const float2 z = Z[ec], m = Z[ec == 0 ? 0 : n - ec];
+                    const float h = 0.5f;
+                    const float2 xa = make_float2((z.x + m.x) * h, (z.y - m.y) * h);
+                    const float2 xb = make_float2((z.y + m.y) * h, (m.x - z.x) * h);
+                    ma[i] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xa.x, xa.x, xa.y * xa.y));
+                    mb[i] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xb.x, xb.x, xb.y * xb.y));
+                }
+                xsync<64>();   // every read of Z before the rows overwrite it
+#pragma unroll
+                for (int i = 0; i < IT; ++i) {
+                    const int e = lane + 64 * i;
+                    if (2 * e <= n) {
+                        X[e] = ma[i];
+                        X[W + e] = mb[i];
+                        if (e != 0 && 2 * e != n) {
+                            X[n - e] = ma[i];
+                            X[W + n - e] = mb[i];
+                        }
+                    }
+                }
+                xsync<64>();
+                const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
+                const int lim = fra + 1 < io.frames ? 2 * W : W;   // floats of the run (row b may not exist)
+                vf4_t* const fo = reinterpret_cast<vf4_t*>(reinterpret_cast<float*>(io.out) + c * io.out_ch_stride + fra * W);
+                const vf4_t* const X4 = reinterpret_cast<const vf4_t*>(X);
+#pragma unroll
+                for (int o = lane; o < (2 * W) / 4; o += 64)
+                    if (4 * o < lim) __builtin_nontemporal_store(X4[o], fo + o);
+            }
+        } else if constexpr ((MODE == 1 || MODE == 2) && n < 900) {
 #pragma unroll
             for (int s = 0; s < TPW; ++s) {
                 const long long q = g + s;
@@ -1024,11 +1076,14 @@ hipError_t launch_stft_mixed(long long nfft, long long hop, int kind, const floa
     io.hop = hop;
     io.out_ch_stride = out_ch_stride;
     io.win = win;
+    io.a16 = ((uintptr_t)out & 15) == 0 && (out_ch_stride & 3) == 0;
     // speech lengths: the two-pass register kernel (VVHIP_STFT_SQ=0: the generic one, A/B)
     if (sq_enabled()) {
         switch (nfft) {
 #define VVH_SQ_STFT(L, A, B) \
-    case L: return run_stft_sq_kind<A, B>(kind, io, batch, s);
+    case L:                                                                  \
+        if (kind == 0 && Sq<A, B, 1>::STG && !io.a16) break; /* unaligned rows: generic */ \
+        return run_stft_sq_kind<A, B>(kind, io, batch, s);
             VVH_SQ_LENGTHS(VVH_SQ_STFT)
 #undef VVH_SQ_STFT
             default: break;
