@@ -113,6 +113,18 @@ def case_stft_n(nch, seconds, nfft, hop, sr=16000):
     return (lambda: st.spectrogram(sig, out=out)), nch * n * 4 + nch * fr * nfft * 4, (sig, out, st)
 
 
+def case_stft_pow_n(nch, seconds, nfft, hop, sr=16000):
+    """power rows [ch][frame][nfft/2+1] at any nfft (register kernel MODE 3 at the speech lengths)"""
+    n = seconds * sr
+    st = vv.Stft(nfft, hop)
+    fr = st.frames(n)
+    key = ("stftpown", nch, n, nfft, hop)
+    if key not in _SHARED:
+        _SHARED[key] = (torch.rand(nch, n, device="cuda") * 2 - 1, torch.empty(nch, fr, nfft // 2 + 1, device="cuda"))
+    sig, out = _SHARED[key]
+    return (lambda: st.power(sig, out=out)), nch * n * 4 + nch * fr * (nfft // 2 + 1) * 4, (sig, out, st)
+
+
 def case_stft_power(nch, seconds):
     """power rows [ch][frame][513] (STFT mode 2, the mel kernel's input)"""
     n = seconds * 48000
@@ -407,6 +419,8 @@ CASES = {
     **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
     **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
     "stft400": lambda: case_stft_n(32, 600, 400, 160),
+    **{f"sqpow{nf}": (lambda nf=nf: case_stft_pow_n(32, 600, nf, nf // 4, sr=48000)) for nf in (400, 480, 960)},
+    "sqpow400k16": lambda: case_stft_pow_n(32, 600, 400, 160, sr=16000),
     # speech lengths at 48 kHz (hop = nfft / 4), and VVHIP_MIX_VAR=1 (the conjugate-symmetric row emit)
     **{f"sq{nf}": (lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000))
        for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},

@@ -525,9 +525,8 @@ struct Sq {
     static constexpr int TT = N1 > N2 ? N1 : N2;   // lanes per transform
     static constexpr int TPW = 64 / TT;            // transforms per wave
     static constexpr int P2 = N2 + 1;              // padded pass-1 row (k1 rows of N2)
-    static constexpr int LT = N1 * P2 > N ? N1 * P2 : N;   // float2 per transform
-    // magnitude rows (MODE 1) staged for 16 B/lane stores: whole float4s per row, 16 B aligned buffers
-    static constexpr bool STG = MODE == 1 && N % 4 == 0 && LT % 2 == 0;
+    // float2 per transform, even: 16 B aligned transform buffers (the staged row flush reads float4s)
+    static constexpr int LT = ((N1 * P2 > N ? N1 * P2 : N) + 1) / 2 * 2;
     // + the W_n table and the window (MODE 5: W_2n^k, k <= n, for the split step)
     static constexpr int LDS = 4 * TPW * LT + N + (MODE == 5 ? N + 1 : N / 2);
     // workgroups per CU the LDS allows, at most 3 (<= 168 VGPRs), or 4 when
@@ -538,6 +537,14 @@ struct Sq {
     static constexpr int FIT = (160 * 1024) / (8 * LDS);
     static constexpr int CAP = (N1 <= 20 && N2 <= 20) ? 4 : 3;
     static constexpr int LB = FIT < CAP ? (FIT < 1 ? 1 : FIT) : CAP;
+    // magnitude rows (MODE 1) are staged in LDS and flushed as one contiguous
+    // run per pair: 16 B/lane when the row length is a multiple of 4 floats
+    // (and the output 16 B aligned), 4 B/lane otherwise
+    // (not for magnitude rows of 600 = 20 x 30 / 640 = 20 x 32: at 3 waves per
+    // SIMD the held magnitudes make the 30/32-point pass spill, 1.16-1.34x
+    // slower, profiles/r03_ab_sq_stage_pow.jsonl -- those keep the symmetric emit)
+    static constexpr bool STG = MODE == 3 || (MODE == 1 && !(LB == 3 && (N1 > 24 || N2 > 24)));
+    static constexpr bool ST16 = STG && MODE == 1 && N % 4 == 0;
 };
 
 // MODE 0 c2c rows (`pairs` = rows), MODE 5 real rows of 2n (even/odd pairs
@@ -667,13 +674,14 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
         // 10 min at 48 kHz, profiles/r03_kbench_sq_sym.jsonl); n >= 900 keeps the
         // per-bin emit of both rows below (2 % faster there).
         if constexpr (S::STG) {
-            // Magnitude rows staged in the transform's own (now consumed) LDS
-            // buffer and written as 16 B/lane stores of the pair's 2W-float run:
+            // Magnitude (and power) rows staged in the transform's own (now consumed) LDS
+            // buffer and written as 16 B/lane stores of the pair's 2W-float run
+            // (4 B/lane plain stores for power rows and rows not a multiple of 4 floats):
             // |X| of bins e and n - e of both rows from one read of Z[e], Z[n-e]
             // (conjugate symmetry), held in registers until every read is done.
             // 12-18 % faster than the 4 B/lane stores of the symmetric emit below
-            // at 400 / 480 / 720 / 900 / 960 (profiles/r03_kbench_sq_stage.jsonl);
-            // the launcher takes the generic kernel for rows that are not 16 B aligned.
+            // at 400 / 480 / 720 / 900 / 960 (profiles/r03_kbench_sq_stage.jsonl,
+            // r03_ab_sq_stage_all.jsonl).
             constexpr int IT = (n / 2 + 1 + 63) / 64;
 #pragma unroll
             for (int s = 0; s < TPW; ++s) {
@@ -690,8 +698,12 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
                     const float h = 0.5f;
                     const float2 xa = make_float2((z.x + m.x) * h, (z.y - m.y) * h);
                     const float2 xb = make_float2((z.y + m.y) * h, (m.x - z.x) * h);
-                    ma[i] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xa.x, xa.x, xa.y * xa.y));
-                    mb[i] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xb.x, xb.x, xb.y * xb.y));
+                    ma[i] = __builtin_fmaf(xa.x, xa.x, xa.y * xa.y);
+                    mb[i] = __builtin_fmaf(xb.x, xb.x, xb.y * xb.y);
+                    if constexpr (MODE == 1) {
+                        ma[i] = __builtin_amdgcn_sqrtf(ma[i]);
+                        mb[i] = __builtin_amdgcn_sqrtf(mb[i]);
+                    }
                 }
                 xsync<64>();   // every read of Z before the rows overwrite it
 #pragma unroll
@@ -700,7 +712,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
                     if (2 * e <= n) {
                         X[e] = ma[i];
                         X[W + e] = mb[i];
-                        if (e != 0 && 2 * e != n) {
+                        if (MODE == 1 && e != 0 && 2 * e != n) {   // power rows (MODE 3) end at bin n/2
                             X[n - e] = ma[i];
                             X[W + n - e] = mb[i];
                         }
@@ -709,11 +721,15 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
                 xsync<64>();
                 const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
                 const int lim = fra + 1 < io.frames ? 2 * W : W;   // floats of the run (row b may not exist)
-                vf4_t* const fo = reinterpret_cast<vf4_t*>(reinterpret_cast<float*>(io.out) + c * io.out_ch_stride + fra * W);
-                const vf4_t* const X4 = reinterpret_cast<const vf4_t*>(X);
+                float* const fo = reinterpret_cast<float*>(io.out) + c * io.out_ch_stride + fra * W;
+                if (S::ST16 && io.a16) {
+                    const vf4_t* const X4 = reinterpret_cast<const vf4_t*>(X);
 #pragma unroll
-                for (int o = lane; o < (2 * W) / 4; o += 64)
-                    if (4 * o < lim) __builtin_nontemporal_store(X4[o], fo + o);
+                    for (int o = lane; o < (2 * W) / 4; o += 64)
+                        if (4 * o < lim) __builtin_nontemporal_store(X4[o], reinterpret_cast<vf4_t*>(fo) + o);
+                } else {   // plain stores: runs that are not whole lines merge in L2
+                    for (int o = lane; o < lim; o += 64) fo[o] = X[o];
+                }
             }
         } else if constexpr ((MODE == 1 || MODE == 2) && n < 900) {
 #pragma unroll
@@ -1081,9 +1097,7 @@ hipError_t launch_stft_mixed(long long nfft, long long hop, int kind, const floa
     if (sq_enabled()) {
         switch (nfft) {
 #define VVH_SQ_STFT(L, A, B) \
-    case L:                                                                  \
-        if (kind == 0 && Sq<A, B, 1>::STG && !io.a16) break; /* unaligned rows: generic */ \
-        return run_stft_sq_kind<A, B>(kind, io, batch, s);
+    case L: return run_stft_sq_kind<A, B>(kind, io, batch, s);
             VVH_SQ_LENGTHS(VVH_SQ_STFT)
 #undef VVH_SQ_STFT
             default: break;
