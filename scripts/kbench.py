@@ -299,8 +299,10 @@ def case_c2clab(e, batch=65536):
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
     lib.c2clab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
-    x = torch.rand(batch, 1024, dtype=torch.complex64, device="cuda")
-    y = torch.empty_like(x)
+    if ("c2clab", batch) not in _SHARED:   # one buffer pair for every c2c lab case (same placement)
+        x = torch.rand(batch, 1024, dtype=torch.complex64, device="cuda")
+        _SHARED[("c2clab", batch)] = (x, torch.empty_like(x))
+    x, y = _SHARED[("c2clab", batch)]
     s = torch.cuda.current_stream().cuda_stream
     return (lambda: lib.c2clab_run(e, x.data_ptr(), y.data_ptr(), batch, s)), 2 * batch * 1024 * 8, (x, y, lib)
 
@@ -450,7 +452,7 @@ CASES = {
     "stft256ch": lambda: case_stft(256, 600),
     **{f"place_i{i}_o{o}": (lambda i=i, o=o: case_stft_place(i, o))
        for i in (0, 4, 64, 1024, 2052) for o in (0, 4, 8, 64, 1024, 2052, 4100)},
-    **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2)},
+    **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2, 4, 6)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
                                                                           256, 320)},

@@ -79,6 +79,8 @@ extern "C" int c2clab_run(int exp, const void* in, void* out, long long batch, v
         case 0: return (int)vvh::lab_c2c<0>((const float2*)in, (float2*)out, batch, s);
         case 1: return (int)vvh::lab_c2c<1>((const float2*)in, (float2*)out, batch, s);
         case 2: return (int)vvh::lab_c2c<2>((const float2*)in, (float2*)out, batch, s);
+        case 4: return (int)vvh::lab_c2c<4>((const float2*)in, (float2*)out, batch, s);
+        case 6: return (int)vvh::lab_c2c<6>((const float2*)in, (float2*)out, batch, s);
         default: return -1;
     }
 }

@@ -30,7 +30,7 @@ namespace vvh {
 // (pass_exchange_ri): 26 KB of LDS per workgroup instead of 43 KB, so four
 // workgroups (16 waves) fit per CU and keep more transforms' loads in flight.
 template <int N, bool FWD, int EXP = 0>
-__global__ void __launch_bounds__(Wg<N>::value, N == 1024 ? 4 : 1)
+__global__ void __launch_bounds__(Wg<N>::value, N == 1024 ? ((EXP & 4) ? 5 : 4) : 1)
 k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
       const float2* gpass, const float2* gtab, float scale) {
     using G = Geo<N>;
