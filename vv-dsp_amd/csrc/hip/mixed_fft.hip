@@ -560,8 +560,11 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
     float2* const tab = sm + 4 * TPW * LT;
     float* const lwin = reinterpret_cast<float*>(tab + n);
     float2* const ltw = tab + n;   // MODE 5 (in the window's place)
+    // pass 1's twiddles W_n^(k1 t) stored [k1][t] (t < N2): for one k1 the lanes
+    // read consecutive entries (tab[k1 t] had k1-strided, bank-conflicting reads)
     for (int i = threadIdx.x; i < n; i += 256) {
-        tab[i] = gtab[i];
+        const int k1 = i / N2, tt = i - k1 * N2;
+        tab[i] = gtab[k1 * tt];
         if constexpr (MODE != 0 && MODE != 5) lwin[i] = io.win[i];
     }
     if constexpr (MODE == 5) {   // the split step's W_2n^k from LDS, not a dependent global load per bin
@@ -594,7 +597,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
                 }
                 reg_dft<N1>(v);
 #pragma unroll
-                for (int k1 = 0; k1 < N1; ++k1) L[k1 * P2 + t] = k1 == 0 ? v[0] : cmul(v[k1], tab[k1 * t]);
+                for (int k1 = 0; k1 < N1; ++k1) L[k1 * P2 + t] = k1 == 0 ? v[0] : cmul(v[k1], tab[k1 * N2 + t]);
             } else if (MODE != 0 && MODE != 5 && lane_ok && q < pairs && t < N2) {
                 const long long c = q / io.ppc, fra = 2 * (q - c * io.ppc);
                 const long long st = fra * io.hop;
@@ -624,7 +627,7 @@ __global__ void __launch_bounds__(256, (Sq<N1, N2, MODE>::LB)) k_stft_sq(MixIO i
                 }
                 reg_dft<N1>(v);
 #pragma unroll
-                for (int k1 = 0; k1 < N1; ++k1) L[k1 * P2 + t] = k1 == 0 ? v[0] : cmul(v[k1], tab[k1 * t]);
+                for (int k1 = 0; k1 < N1; ++k1) L[k1 * P2 + t] = k1 == 0 ? v[0] : cmul(v[k1], tab[k1 * N2 + t]);
             }
         }
         xsync<64>();
