@@ -111,6 +111,38 @@ def _frame_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _stream_worker(rank, world, nch, port, q, slab):
+    """gather_rows_stream: rank 0 never allocates the [nch, ...] result on the
+    device; slabs of `slab` bytes per rank go through one staging buffer into a
+    host tensor (host_sink), uneven shards included."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vvapi import Oracle
+        orc = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
+        x = _signals(nch)
+        lo, hi = vvdsp_dist.channel_shard(nch, world, rank)
+        shape = orc.spectrogram(x[0], NFFT, HOP).shape
+        local = torch.from_numpy(np.stack([orc.spectrogram(x[c], NFFT, HOP) for c in range(lo, hi)])) \
+            if hi > lo else torch.zeros((0,) + shape)
+        out = torch.full((nch,) + shape, -1.0) if rank == 0 else None
+        seen = []
+
+        def sink(first, block):
+            seen.append((first, block.shape[0]))
+            vvdsp_dist.host_sink(out)(first, block)
+
+        vvdsp_dist.gather_rows_stream(local, nch, sink if rank == 0 else None, dst=0, slab_bytes=slab)
+        if rank == 0:
+            ref = np.stack([orc.spectrogram(x[c], NFFT, HOP) for c in range(nch)])
+            rows = sorted(f + i for f, k in seen for i in range(k))
+            q.put(bool(np.array_equal(out.numpy(), ref)) and rows == list(range(nch)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -164,6 +196,22 @@ def test_half_bin_gather_gloo(world, nch):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert all(q.get(timeout=5) is True for _ in range(world))
+
+
+@pytest.mark.parametrize("world,nch,slab", [(2, 5, 1), (3, 7, 100000), (2, 6, 1 << 30)])
+def test_streaming_gather_gloo(world, nch, slab):
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        pytest.skip("oracle not built (make -C oracle)")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, nch, port, q, slab)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
 
 
 def test_shard_range_c_matches_python():

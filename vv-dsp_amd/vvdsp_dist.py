@@ -87,6 +87,55 @@ def gather_rows(local, total, dst=0, group=None, out=None, sizes=None):
     return None
 
 
+def gather_rows_stream(local, total, sink, dst=0, group=None, sizes=None, slab_bytes=GATHER_SLAB_BYTES):
+    """gather_rows without the [total, ...] destination: rank `dst` receives
+    slabs of at most ~slab_bytes per rank into one reusable staging buffer and
+    hands each rank's piece to sink(first_row, block) in row order (e.g.
+    host_sink: straight into a pinned host tensor, so config 5's 118 GB never
+    has to fit on one GPU next to its own shard).  Ranks with fewer rows pad
+    their slabs; only real rows reach the sink."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = shard_sizes(total, world) if sizes is None else list(sizes)
+    if len(sizes) != world or sum(sizes) != total:
+        raise ValueError(f"shard sizes {sizes} do not cover {total} rows on {world} ranks")
+    if local.shape[0] != sizes[rank]:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} channels, layout says {sizes[rank]}")
+    cmax = max(sizes)
+    if cmax == 0:
+        return
+    firsts = [sum(sizes[:r]) for r in range(world)]
+    tail = tuple(local.shape[1:])
+    row_bytes = max(1, int(torch.Size(tail).numel()) * local.element_size())
+    step = max(1, min(cmax, int(slab_bytes) // row_bytes))
+    loc = local.contiguous()
+    send = torch.empty((step,) + tail, dtype=local.dtype, device=local.device)
+    stage = torch.empty((world, step) + tail, dtype=local.dtype, device=local.device) if rank == dst else None
+    for i0 in range(0, cmax, step):
+        i1 = min(cmax, i0 + step)
+        mine = max(0, min(i1, sizes[rank]) - i0)   # real rows of this slab on this rank
+        if mine:
+            send[:mine].copy_(loc[i0:i0 + mine])
+        if mine < i1 - i0:
+            send[mine:i1 - i0].zero_()
+        if rank == dst:
+            dist.gather(send[:i1 - i0], gather_list=[stage[r, :i1 - i0] for r in range(world)], dst=dst, group=group)
+            for r in range(world):
+                real = max(0, min(i1, sizes[r]) - i0)
+                if real:
+                    sink(firsts[r] + i0, stage[r, :real])
+        else:
+            dist.gather(send[:i1 - i0], dst=dst, group=group)
+
+
+def host_sink(out):
+    """A gather_rows_stream sink that copies each block into the host tensor
+    `out` ([total, ...], ideally pinned) at its row position."""
+    def sink(first, block):
+        out[first:first + block.shape[0]].copy_(block)
+    return sink
+
+
 def gather_rows_half(local, total, nfft, dst=0, group=None, out=None, pack=None, unpack=None):
     """gather_rows for magnitude / power rows [ch, frames, nfft] of real frames,
     sending bins 0..nfft/2 only (SURVEY 8e row note 1: half the xGMI bytes of
