@@ -128,10 +128,11 @@ def case_stft_pow_n(nch, seconds, nfft, hop, sr=16000):
 def case_stft_power(nch, seconds):
     """power rows [ch][frame][513] (STFT mode 2, the mel kernel's input)"""
     n = seconds * 48000
-    sig = torch.rand(nch, n, device="cuda") * 2 - 1
     st = vv.Stft(1024, 256)
     fr = st.frames(n)
-    out = torch.empty(nch, fr, 513, device="cuda")
+    if ("pow", nch, n) not in _SHARED:   # shared by the A/B cases (same placement)
+        _SHARED[("pow", nch, n)] = (torch.rand(nch, n, device="cuda") * 2 - 1, torch.empty(nch, fr, 513, device="cuda"))
+    sig, out = _SHARED[("pow", nch, n)]
     return (lambda: st.power(sig, out=out)), nch * n * 4 + nch * fr * 513 * 4, (sig, out, st)
 
 
@@ -463,6 +464,8 @@ CASES = {
     **{f"stftcps{c}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_CPS", str(c)) for c in (1, 2, 4, 8)},
     "stftspan": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RING", "0"),
     "stftchunk": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DYN", "0"),
+    "stftpowdyn": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_DYN", "1"),
+    "stftcdyn": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_DYN", "1"),
     "stftchunk256ch": with_env(lambda: case_stft(256, 600), "VVHIP_STFT_DYN", "0"),
     "stftpowspan": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RING", "0"),
     "stftcspan": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_RING", "0"),

@@ -68,3 +68,25 @@ def test_dynamic_walk_rows_vs_numpy(job, orc):
         frames = [0, 1, 4097, 39374, 78744, 78747, 78748]   # the last ones run past the end
         X = np.abs(np.fft.fft(np.stack([pad[f * 256:f * 256 + 1024] for f in frames]) * w, axis=1))
         np.testing.assert_allclose(out[c][frames].cpu().numpy(), X, rtol=5e-5, atol=5e-5)
+
+
+@pytest.mark.parametrize("kind", ["power", "complex"])
+def test_dynamic_walk_other_rows(job, kind):
+    """VVHIP_STFT_DYN=1 runs power (n/2+1) and complex rows through the same
+    walk: rows equal to the default launch's, bit for bit."""
+    import torch
+    sig, st, _ = job
+    run = (lambda: st.power(sig)) if kind == "power" else (lambda: st.spectrogram(sig, complex_out=True))
+    os.environ["VVHIP_STFT_DYN"] = "0"
+    try:
+        ref = run().clone()
+    finally:
+        os.environ["VVHIP_STFT_DYN"] = ""
+    os.environ["VVHIP_STFT_DYN"] = "1"
+    try:
+        for _ in range(2):
+            got = run()
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref)
+    finally:
+        os.environ["VVHIP_STFT_DYN"] = ""

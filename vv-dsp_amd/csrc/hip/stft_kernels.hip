@@ -906,17 +906,22 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const char* er = getenv("VVHIP_STFT_RING");
         const bool ring = Geo<N>::T == 64 && hop % 256 == 0 &&
                           (er && *er ? *er == '1' : MODE == 2);
-        // Magnitude rows of large jobs: the persistent dynamic walk (VAR 4) --
+        // Magnitude and complex rows of large jobs: the persistent dynamic walk (VAR 4) --
         // each wave takes its next pair from a per-(XCD group, slot) counter, so
         // the chip sweeps one moving band of pairs with the load balanced on the
         // fly (-1.6 % against the chunked launch in two same-buffer measurements,
         // profiles/r03_kbench_ablation_samebuf.jsonl lab8192; bit-identical rows).
         // VVHIP_STFT_DYN = 0 keeps the chunked VAR 0 (A/B switch, read per call).
+        // Complex rows take it too (1.629 -> 1.579 ms for 8 ch x 10 min, -3.1 %);
+        // power rows keep the ring walk below (2.689 ring vs 2.730 dynamic vs
+        // 2.760 chunked, profiles/r03_kbench_dyn_modes.jsonl).  VVHIP_STFT_DYN =
+        // 1 forces it for every row kind (A/B).
         const char* ed = getenv("VVHIP_STFT_DYN");
         bool dyn = false;
-        if constexpr (MODE == 0 && Geo<N>::T == 64) {
+        if constexpr (Geo<N>::T == 64) {
             const int capd = cached_grid(capc[4], (const void*)k_stft_pair<N, MODE, 4>, WG, 0, 1LL << 40);
-            dyn = aligned && FUSE_TAIL && !ring && !(ed && *ed == '0') && capd >= 8 &&
+            const bool want = ed && *ed ? *ed == '1' : (MODE == 0 || MODE == 1);
+            dyn = aligned && FUSE_TAIL && want && capd >= 8 &&
                   bulk_pairs >= 16LL * F * capd;   // >= 16 pairs per wave: the band walk pays off
             if (dyn) {
                 ctrs = stream_counters(s);
@@ -924,7 +929,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             }
         }
         if (dyn) {
-            if constexpr (MODE == 0 && Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 4>, 4, 0LL, ppc);
+            if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 4>, 4, 0LL, ppc);
         } else if (aligned && FUSE_TAIL && ring) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 3>, 3, 0LL, ppc);
         } else if (aligned && FUSE_TAIL) {
