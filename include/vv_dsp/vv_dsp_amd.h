@@ -150,6 +150,23 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_mfcc_process_device(const vv_dsp_mfcc_plan
                                                           size_t num_frames, vv_dsp_real* d_out_mfcc, void* stream);
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_log_mel_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
                                                      size_t num_frames, vv_dsp_real* d_out_log_mel, void* stream);
+/* Signal -> log-mel / MFCC rows without the power spectrogram in HBM:
+ * d_signal [nch][n] (ch_stride floats apart) -> d_out [nch][frames][n_mels]
+ * (log-mel) or [nch][frames][num_mfcc_coeffs] (MFCC), out_ch_stride floats
+ * apart.  The values are those of vv_dsp_stft_power_device followed by
+ * vv_dsp_log_mel_device / vv_dsp_mfcc_process_device (the stft's window,
+ * nfft and hop; the plan's filterbank, log epsilon, DCT and lifter), bit for
+ * bit: for nfft = 1024 one kernel computes them with the power rows kept in
+ * LDS, otherwise the two steps run through a scratch buffer.  The plan's
+ * n_fft must equal the stft's nfft (VV_DSP_ERROR_INVALID_SIZE). */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_log_mel_device(vv_dsp_stft* h, const vv_dsp_mfcc_plan* plan,
+                                                          const vv_dsp_real* d_signal, size_t n, size_t nch,
+                                                          size_t ch_stride, vv_dsp_real* d_out, size_t out_ch_stride,
+                                                          void* stream, size_t* out_frames);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_mfcc_device(vv_dsp_stft* h, const vv_dsp_mfcc_plan* plan,
+                                                       const vv_dsp_real* d_signal, size_t n, size_t nch,
+                                                       size_t ch_stride, vv_dsp_real* d_out, size_t out_ch_stride,
+                                                       void* stream, size_t* out_frames);
 
 /* Chirp-z plan (vv_dsp_czt_exec_cpx / _real semantics, czt.c:44-178): chirps and
  * the chirp's spectrum resident on the device; `batch` contiguous rows

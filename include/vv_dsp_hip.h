@@ -144,6 +144,11 @@ void vvhip_mel_destroy(vvhip_mel* m);
  *      1: power rows -> MFCC [frames][n_coeffs]
  *      2: log-mel rows [frames][n_mels] -> MFCC [frames][n_coeffs] */
 int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_out, int kind, void* stream);
+/* signal [ch][n] (ch_stride floats apart) -> log-mel (kind 0) or MFCC (kind 1)
+ * rows [ch][frame][n_mels | n_coeffs]: the stft's power rows feed the mel plan
+ * in one kernel when nfft = 1024 (else two launches, same values) */
+int vvhip_stft_mel_device(vvhip_stft* h, vvhip_mel* m, const float* d_signal, size_t n, size_t nch, size_t ch_stride,
+                          float* d_out, size_t out_ch_stride, int kind, void* stream);
 int vvhip_mel_host(vvhip_mel* m, const float* in, size_t frames, float* out, int kind);
 
 /* Block length (real FFT size) the overlap-save path uses for a signal of n samples. */

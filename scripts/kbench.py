@@ -125,6 +125,22 @@ def case_stft_pow_n(nch, seconds, nfft, hop, sr=16000):
     return (lambda: st.power(sig, out=out)), nch * n * 4 + nch * fr * (nfft // 2 + 1) * 4, (sig, out, st)
 
 
+def case_stft_mel(log_mel, nch=32, seconds=600, n_mels=40, n_coeffs=13):
+    """signal -> log-mel / MFCC rows (vv_dsp_stft_log_mel_device / _mfcc_device; the
+    power rows stay in LDS); bytes = signal in + rows out"""
+    n = seconds * 48000
+    st = vv.Stft(1024, 256)
+    fr = st.frames(n)
+    mf = vv.Mfcc(1024, n_mels, n_coeffs, 48000.0, 20.0, 20000.0, lifter=22.0)
+    width = n_mels if log_mel else n_coeffs
+    if ("melsig", nch, n) not in _SHARED:
+        _SHARED[("melsig", nch, n)] = torch.rand(nch, n, device="cuda") * 2 - 1
+    sig = _SHARED[("melsig", nch, n)]
+    out = torch.empty(nch, fr, width, device="cuda")
+    return (lambda: mf.from_signal(st, sig, log_mel=log_mel, out=out)), nch * n * 4 + nch * fr * width * 4, \
+        (sig, out, st, mf)
+
+
 def case_stft_power(nch, seconds):
     """power rows [ch][frame][513] (STFT mode 2, the mel kernel's input)"""
     n = seconds * 48000
@@ -464,6 +480,9 @@ CASES = {
     **{f"stftcps{c}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_CPS", str(c)) for c in (1, 2, 4, 8)},
     "stftspan": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RING", "0"),
     "stftchunk": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DYN", "0"),
+    "melsig": lambda: case_stft_mel(True), "mfccsig": lambda: case_stft_mel(False),
+    "melsig2": with_env(lambda: case_stft_mel(True), "VVHIP_MEL_FUSED", "0"),
+    "mfccsig2": with_env(lambda: case_stft_mel(False), "VVHIP_MEL_FUSED", "0"),
     "stftpowdyn": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_DYN", "1"),
     "stftcdyn": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_DYN", "1"),
     "stftchunk256ch": with_env(lambda: case_stft(256, 600), "VVHIP_STFT_DYN", "0"),

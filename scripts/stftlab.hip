@@ -25,7 +25,7 @@ static hipError_t lab_launch(const float* sig, long long n, long long nch, const
     float* sink = store_sink();
     unsigned* ctr = (EXP & 8192) ? stream_counters(s) : nullptr;   // XCD counters (the kernel's last waves reset them)
     hipLaunchKernelGGL((k_stft_pair<N, 0, 0, EXP>), dim3((unsigned)grid), dim3(256), 0, s, sig, n, nch, n, frames, hop,
-                       0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, sink, ctr);
+                       0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, sink, ctr, MelArgs{});
     return hipGetLastError();
 }
 // config 4's bulk launch (8 ch x 2^24, 257 taps: N 1024, le 256) of k_fir_bulk<1024, true, EXP>

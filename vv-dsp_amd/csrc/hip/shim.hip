@@ -1399,6 +1399,51 @@ int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_ou
     return ST_OK;
 }
 
+// Signal -> log-mel (kind 0) / MFCC (kind 1) rows [ch][frame][n_mels or
+// n_coeffs]: one fused launch (launch_stft_mel) when the shape allows it, else
+// the power rows into scratch and the plan's mel kernel -- the same values.
+int vvhip_stft_mel_device(vvhip_stft* h, vvhip_mel* m, const float* d_signal, size_t n, size_t nch, size_t ch_stride,
+                          float* d_out, size_t out_ch_stride, int kind, void* stream) {
+    if (!h || !m || !d_signal || !d_out) return ST_NULL;
+    if (kind != 0 && kind != 1) return fail(ST_RANGE, "stft mel output kind");
+    if (m->nbins != (int)(h->nfft / 2 + 1)) return fail(ST_SIZE, "mfcc plan bins differ from the stft's nfft/2+1");
+    if (kind == 1 && m->n_coeffs == 0) return fail(ST_RANGE, "mfcc plan lacks the DCT");
+    if (nch == 0) return ST_OK;
+    const hipStream_t s = (hipStream_t)stream;
+    const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    const float* win = stft_window_here(h);
+    if (!win) return fail(ST_INTERNAL, "stft window on the current device");
+    const char* ef = getenv("VVHIP_MEL_FUSED");   // 0: the two launches (A/B), read per call
+    if (!(ef && *ef == '0')) {
+        MelArgs a;
+        a.W = m->W;
+        a.chunks = m->chunks;
+        a.cbeg = m->cbeg;
+        a.D = m->D;
+        a.lift = m->lift;
+        a.nnz = m->nnz;
+        a.nc = m->nc;
+        a.M = m->n_mels;
+        a.C = m->n_coeffs;
+        a.eps = m->eps;
+        const hipError_t e = launch_stft_mel(kind, (long long)h->nfft, (long long)h->hop, d_signal, (long long)n,
+                                             (long long)nch, (long long)ch_stride, (long long)frames, win, a, d_out,
+                                             (long long)out_ch_stride, s);
+        if (e == hipSuccess) return ST_OK;
+        if (e != hipErrorNotSupported) return fail(ST_INTERNAL, hipGetErrorString(e));
+        (void)hipGetLastError();
+    }
+    const size_t nb = h->nfft / 2 + 1, width = kind == 0 ? (size_t)m->n_mels : (size_t)m->n_coeffs;
+    Scratch pw(s);
+    HIPCHK(pw.alloc(sizeof(float) * nch * frames * nb), ST_INTERNAL);
+    int st = stft_frames_run(h, d_signal, n, nch, ch_stride, pw.p, frames * nb, 2, s);
+    if (st) return st;
+    if (out_ch_stride == frames * width) return vvhip_mel_device(m, (const float*)pw.p, nch * frames, d_out, kind, stream);
+    for (size_t c = 0; c < nch && !st; ++c)
+        st = vvhip_mel_device(m, (const float*)pw.p + c * frames * nb, frames, d_out + c * out_ch_stride, kind, stream);
+    return st;
+}
+
 int vvhip_mel_host(vvhip_mel* m, const float* in, size_t frames, float* out, int kind) {
     if (!m || !in || !out) return ST_NULL;
     std::lock_guard<std::mutex> host_lock(m->host_mu);

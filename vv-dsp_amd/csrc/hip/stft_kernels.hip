@@ -266,6 +266,187 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
     }
 }
 
+// Log-mel (MODE 3) or MFCC (MODE 4) rows of one frame pair from the FFT
+// registers (N = 1024, one wave per transform).  The power of bins 0..N/2 of
+// both frames (pair_post<2>: the power rows' arithmetic) goes to the
+// transform's idle exchange buffer P in natural order; then k_mel_grp's steps
+// with FR = 2 frames: chunk partials (FMA in bin order; lane c % 64 holds chunk
+// c in round c / 64), per-filter sums of the partials in chunk order (fetched
+// across lanes by ds_bpermute), logf(e + eps), and for MODE 4 the DCT-II and
+// lifter over the log-mel rows (kept in P's spare tail) -- the same operations
+// in the same order, so the rows equal launch_stft mode 2 followed by
+// launch_mel_grp bit for bit.  The plan's tables sit in dynamic LDS (about
+// 4-8 KB), paid for by spans of N + 256 floats (hop <= 256), so 3 workgroups
+// per CU still fit; no compiler-generated global load enters the hand-counted
+// pipeline.  Stores: MODE 3 four counted dword stores (rows a, b x filters
+// t, t + 64; M <= 128), MODE 4 two ((frame, coefficient) pairs t, t + 64;
+// C <= 64); lanes without a row element write to the sink.
+constexpr int MEL_MAX_ROUNDS = 4;   // chunks <= 256
+constexpr int MEL_LM_OFF = 1028;    // MODE 4: log-mel rows in P past the two power rows (16 B aligned)
+template <int N, int MODE>
+__device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, float* fb, bool has_b, float* sink,
+                                         float* P, const float* sW, const int* sCh, const int* sCb,
+                                         const float* sD, const float* sL, const MelArgs& mel) {
+    using G = Geo<N>;
+    using Mi = Mirror<N>;
+    constexpr int R = G::RL, J = G::NPT / 2, NB = G::NB, T = G::T, RW = N / 2 + 1;
+    static_assert(T == 64, "one wave per transform");
+    static_assert(2 * RW <= MEL_LM_OFF, "log-mel rows past the power rows");
+    float ea[J][R], eb[J][R], sa[R], sb[R];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int q = 2 * j * R + r;
+            float2 A, B;
+            pair_post<2>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+            ea[j][r] = A.x;
+            eb[j][r] = B.x;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int qm = Mi::normal(r);
+        float2 A2, B2;
+        pair_post<2>(v[qm], v[Mi::special(qm)], &A2, &B2);
+        sa[r] = A2.x;
+        sb[r] = B2.x;
+    }
+    // block m of 64 bins: an even block (lane t: bin 64 m + t) or the mirror
+    // block of slot (jm, rm) (lane t: bin 64 m + (64 - t) % 64), as direct_rows
+    static_for<0, N / T>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        if constexpr (T * m < N / 2) {
+            constexpr int je = m % (NB / T), re = m / (NB / T);
+            if constexpr (je < J) {
+                P[T * m + t] = ea[je][re];
+                P[RW + T * m + t] = eb[je][re];
+            } else {
+                constexpr int mm = (N / T - 1) - m, rm = mm / (NB / T), jm = mm % (NB / T);
+                float va, vb;
+                if constexpr (jm + 1 < J) {
+                    va = t == 0 ? ea[jm + 1][rm] : ea[jm][rm];
+                    vb = t == 0 ? eb[jm + 1][rm] : eb[jm][rm];
+                } else {
+                    va = t == 0 ? sa[rm] : ea[jm][rm];
+                    vb = t == 0 ? sb[rm] : eb[jm][rm];
+                }
+                const int bin = T * m + (t == 0 ? 0 : T - t);
+                P[bin] = va;
+                P[RW + bin] = vb;
+            }
+        }
+    });
+    if (t == 0) {
+        P[N / 2] = ea[0][R / 2];
+        P[RW + N / 2] = eb[0][R / 2];
+    }
+    xsync<T>();
+    const int nc = mel.nc, M = mel.M, C = mel.C;
+    float pa[MEL_MAX_ROUNDS], pb[MEL_MAX_ROUNDS];
+#pragma unroll
+    for (int u = 0; u < MEL_MAX_ROUNDS; ++u) {
+        pa[u] = pb[u] = 0.0f;
+        const int c = t + T * u;
+        if (c < nc) {
+            const int lo = sCh[3 * c], len = sCh[3 * c + 1], off = sCh[3 * c + 2];
+            float a0 = 0.0f, b0 = 0.0f;
+            for (int j = 0; j < len; ++j) {
+                const float w = sW[off + j];
+                a0 = __builtin_fmaf(P[lo + j], w, a0);
+                b0 = __builtin_fmaf(P[RW + lo + j], w, b0);
+            }
+            pa[u] = a0;
+            pb[u] = b0;
+        }
+    }
+    const int nr = (nc + T - 1) / T;   // rounds holding chunks (wave-uniform)
+    float la[2], lb[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int m = t + T * u;
+        const bool on = m < M;
+        const int cb = on ? sCb[m] : 0, ce = on ? sCb[m + 1] : 0;
+        int kmax = ce - cb;   // the wave's longest filter (in chunks) sets the trip count
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) {
+            const int o = __shfl_xor(kmax, sh, 64);
+            kmax = o > kmax ? o : kmax;
+        }
+        float e0 = 0.0f, e1 = 0.0f;
+        for (int k = 0; k < kmax; ++k) {   // chunk cb + k of this lane's filter, in order
+            const int c = cb + k < ce ? cb + k : 0;
+            const int addr = (c & (T - 1)) << 2, rd = c / T;
+            float ga = 0.0f, gb = 0.0f;
+#pragma unroll
+            for (int r = 0; r < MEL_MAX_ROUNDS; ++r) {
+                if (r < nr) {   // every lane joins each permute (wave-uniform condition)
+                    const float xa = __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(pa[r])));
+                    const float xb = __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(pb[r])));
+                    ga = rd == r ? xa : ga;
+                    gb = rd == r ? xb : gb;
+                }
+            }
+            if (cb + k < ce) {
+                e0 += ga;
+                e1 += gb;
+            }
+        }
+        la[u] = on ? logf(e0 + mel.eps) : 0.0f;
+        lb[u] = on ? logf(e1 + mel.eps) : 0.0f;
+    }
+    float* const snk = sink + t;
+    if constexpr (MODE == 3) {
+        st4_counted(t < M ? fa + t : snk, la[0]);
+        st4_counted(t + T < M ? fa + t + T : snk, la[1]);
+        st4_counted(has_b && t < M ? fb + t : snk, lb[0]);
+        st4_counted(has_b && t + T < M ? fb + t + T : snk, lb[1]);
+    } else {
+        float* const lm = P + MEL_LM_OFF;   // [2][M], M <= (ri_floats - MEL_LM_OFF) / 2
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int m = t + T * u;
+            if (m < M) {
+                lm[m] = la[u];
+                lm[M + m] = lb[u];
+            }
+        }
+        xsync<T>();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int idx = t + T * u;
+            float res = 0.0f;
+            float* dst = snk;
+            if (idx < 2 * C) {
+                const int f = idx / C, i = idx - f * C;
+                const float* l = lm + f * M;
+                const float* d = sD + i * M;
+                float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+                int m = 0;
+                if ((M & 3) == 0) {   // as k_mel_grp: four partial sums
+                    for (; m < M; m += 4) {
+                        const vf4_t a = *reinterpret_cast<const vf4_t*>(l + m);
+                        c0 = __builtin_fmaf(a[0], d[m], c0);
+                        c1 = __builtin_fmaf(a[1], d[m + 1], c1);
+                        c2 = __builtin_fmaf(a[2], d[m + 2], c2);
+                        c3 = __builtin_fmaf(a[3], d[m + 3], c3);
+                    }
+                } else {
+                    for (; m + 1 < M; m += 2) {
+                        c0 = __builtin_fmaf(l[m], d[m], c0);
+                        c1 = __builtin_fmaf(l[m + 1], d[m + 1], c1);
+                    }
+                    if (m < M) c0 = __builtin_fmaf(l[m], d[m], c0);
+                }
+                res = ((c0 + c1) + (c2 + c3)) * sL[i];
+                if (f == 0) dst = fa + i;
+                else if (has_b) dst = fb + i;
+            }
+            st4_counted(dst, res);
+        }
+    }
+}
+
 // Frame pairs (2j, 2j+1) of one channel, j in [pair0, pair0 + ppc): pairs never
 // span channels, so a channel's rows do not depend on how channels are grouped
 // into calls or shards.
@@ -286,9 +467,12 @@ __global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR =
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink,
-            unsigned* ctrs) {
+            unsigned* ctrs, MelArgs mel) {
     using G = Geo<N>;
     using Mi = Mirror<N>;
+    // MODE 3 / 4: log-mel / MFCC rows from the power rows, which stay in LDS
+    // (launch_stft_mel; the tables of the MFCC plan in dynamic LDS)
+    constexpr bool MEL = MODE == 3 || MODE == 4;
     constexpr bool TAIL = VAR == 2;
     constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4;
     // VAR 3: VAR 0 with each wave walking a contiguous run of pairs and its
@@ -310,19 +494,22 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr bool STAGE = BULK && MODE == 0 && G::NPASS > 1 && G::T > 1;
     // power rows (N = 1024): the DIRECT stores below, keeping only the
     // 64-bin blocks under N/2 plus one lane for bin N/2
-    constexpr bool POWD = BULK && MODE == 2 && G::T == 64 && G::NPASS > 1;
+    constexpr bool POWD = BULK && (MODE == 2 || MEL) && G::T == 64 && G::NPASS > 1;
+    static_assert(!MEL || POWD, "log-mel / MFCC rows: the one-wave-per-transform bulk kernel (N = 1024)");
     // complex rows (N = 1024): DIRECT with 8 B/lane stores, conj() for the mirror blocks
     constexpr bool CPXD = BULK && MODE == 1 && G::T == 64 && G::NPASS > 1;
     constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
     constexpr bool D2 = D2V && GLDS && !RING && !DYN;
-    constexpr int SPAN = GLDS ? ((EXP & 2048) ? N + 256 : N + N / 2) : 1;   // floats per transform: hop <= N/2
+    // floats per transform: hop <= N/2 (MEL and the EXP bit 11 probe: hop <= 256)
+    constexpr int SPAN = GLDS ? (((EXP & 2048) || MEL) ? N + 256 : N + N / 2) : 1;
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
     // written as 16 B/lane stores
     constexpr bool DIRECT = GLDS && G::T == 64;
     static_assert(!RING || DIRECT, "ring spans: one wave per transform on the LDS-DMA path");
     // stores per pair (both rows): power rows keep half the blocks + bin N/2
-    constexpr int NST = (EXP & 4) ? 0 : (EXP & 16) ? 8 : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
+    constexpr int NST = (EXP & 4) ? 0 : (EXP & 16) ? 8 : MEL ? (MODE == 3 ? 4 : 2)
+                                                       : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
@@ -353,6 +540,10 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
     constexpr long long ES = MODE == 1 ? 8 : 4;            // bytes per bin
     constexpr long long ROW = MODE == 2 ? N / 2 + 1 : N;   // bins per row
+    const long long ROWR = MODE == 3 ? (long long)mel.M : MODE == 4 ? (long long)mel.C : ROW;
+    // MEL: the plan's tables in dynamic LDS: W [nnz], chunks [3 nc], cbeg [M + 1], then (MODE 4) D [C M], lift [C]
+    extern __shared__ __attribute__((aligned(16))) float mel_lds[];
+    const int mel_dpos = MEL ? (mel.nnz + 3 * mel.nc + mel.M + 1 + 3) & ~3 : 0;
     // rows of one pair from the registers, plain stores (unaligned / tail pairs)
     auto store_generic = [&](float2* v, char* rowa, char* rowb, bool has_b) {
         if constexpr (G::T == 1) {
@@ -534,6 +725,16 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     } else {
         stage_twiddles<N, WG>(ltab, gpass, gtab);
     }
+    if constexpr (MEL) {
+        int* const mi = reinterpret_cast<int*>(mel_lds);
+        for (int i = threadIdx.x; i < mel.nnz; i += WG) mel_lds[i] = mel.W[i];
+        for (int i = threadIdx.x; i < 3 * mel.nc; i += WG) mi[mel.nnz + i] = mel.chunks[i];
+        for (int i = threadIdx.x; i <= mel.M; i += WG) mi[mel.nnz + 3 * mel.nc + i] = mel.cbeg[i];
+        if constexpr (MODE == 4) {
+            for (int i = threadIdx.x; i < mel.C * mel.M; i += WG) mel_lds[mel_dpos + i] = mel.D[i];
+            for (int i = threadIdx.x; i < mel.C; i += WG) mel_lds[mel_dpos + mel.C * mel.M + i] = mel.lift[i];
+        }
+    }
     __syncthreads();
     if (!any && !DYN) return;
     if constexpr (GLDS) vm_wait<0>();
@@ -649,10 +850,15 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 else vm_wait<NST>();
             }
         }
-        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
-        char* rowb = rowa + ROW * ES;
+        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROWR) * ES;
+        char* rowb = rowa + ROWR * ES;
         const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
-        if constexpr (DIRECT) {
+        if constexpr (MEL) {
+            const int* mi = reinterpret_cast<const int*>(mel_lds);
+            mel_rows<N, MODE>(v, t, reinterpret_cast<float*>(rowa), reinterpret_cast<float*>(rowb), has_b, sink,
+                              reinterpret_cast<float*>(my), mel_lds, mi + mel.nnz, mi + mel.nnz + 3 * mel.nc,
+                              mel_lds + mel_dpos, mel_lds + mel_dpos + mel.C * mel.M, mel);
+        } else if constexpr (DIRECT) {
             direct_rows<N, MODE, EXP>(v, t, rowa, rowb, has_b, sink);
         } else if constexpr (STAGE) {
             // both magnitude rows through the (now idle) exchange buffer, then
@@ -881,7 +1087,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 chunk |= rl << 40;
             }
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0,
-                               cnt, win, out, out_ch_stride, pN, tN, chunk, sink, ctrs);
+                               cnt, win, out, out_ch_stride, pN, tN, chunk, sink, ctrs, MelArgs{});
         };
         // 16 B aligned output rows allow the staged 16 B/lane stores
         // (power rows are n/2+1 floats: their direct stores are dwords, 4 B suffice;
@@ -961,6 +1167,66 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
 
 bool stft_fused_supported(long long nfft) {
     return nfft >= 2 && nfft <= 8192 && (nfft & (nfft - 1)) == 0;
+}
+
+// Signal -> log-mel (kind 0) / MFCC (kind 1) rows in one launch (k_stft_pair
+// MODE 3 / 4, N = 1024).  The launch follows run_stft's bulk path: the chunked
+// non-persistent grid, or the dynamic walk for large jobs; the plan's tables
+// ride in dynamic LDS, so the occupancy is computed per call.
+template <int MODE>
+static hipError_t run_stft_mel(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
+                               long long hop, const float* win, const MelArgs& mel, float* out, long long out_ch_stride,
+                               hipStream_t s) {
+    constexpr int N = 1024, WG = Wg<N>::value, F = Wg<N>::F;
+    const float2* tN = twiddle_table(N);
+    const float2* pN = pass_twiddles(N);
+    float* sink = store_sink();
+    if (!tN || !pN || !sink) return hipErrorOutOfMemory;
+    const long long ppc = (frames + 1) / 2, pairs = nch * ppc;
+    if (pairs <= 0) return hipSuccess;
+    // the plan's tables in dynamic LDS (the kernel's layout); occupancy per call
+    const long long dpos = (mel.nnz + 3LL * mel.nc + mel.M + 1 + 3) & ~3LL;
+    const size_t dyn = sizeof(float) * (size_t)(dpos + (MODE == 4 ? (long long)mel.C * mel.M + mel.C : 0));
+    const int cap = persistent_grid((const void*)k_stft_pair<N, MODE, 0>, WG, dyn, 1LL << 40);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_stft_pair<N, MODE, 0>, WG, dyn) !=
+            hipSuccess ||
+        per_cu < 1)
+        return hipErrorNotSupported;
+    unsigned* ctrs = nullptr;
+    const char* ed = getenv("VVHIP_STFT_DYN");
+    const bool dyn_walk = !(ed && *ed == '0') && cap >= 8 && pairs >= 16LL * F * cap;
+    long long grid, chunk = 0;
+    if (dyn_walk) {
+        ctrs = stream_counters(s);
+        if (!ctrs) return hipErrorOutOfMemory;
+        grid = cap / 8 * 8;
+    } else {
+        long long cps = (pairs + (long long)F * cap - 1) / ((long long)F * cap);
+        cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
+        chunk = cps * F;
+        grid = (pairs + chunk - 1) / chunk;
+    }
+    if (dyn_walk)
+        hipLaunchKernelGGL((k_stft_pair<N, MODE, 4>), dim3((unsigned)grid), dim3(WG), dyn, s, sig, n, nch, ch_stride,
+                           frames, hop, 0LL, ppc, win, (void*)out, out_ch_stride, pN, tN, chunk, sink, ctrs, mel);
+    else
+        hipLaunchKernelGGL((k_stft_pair<N, MODE, 0>), dim3((unsigned)grid), dim3(WG), dyn, s, sig, n, nch, ch_stride,
+                           frames, hop, 0LL, ppc, win, (void*)out, out_ch_stride, pN, tN, chunk, sink, ctrs, mel);
+    return hipGetLastError();
+}
+
+hipError_t launch_stft_mel(int kind, long long nfft, long long hop, const float* sig, long long n, long long nch,
+                           long long ch_stride, long long frames, const float* win, const MelArgs& mel, float* out,
+                           long long out_ch_stride, hipStream_t s) {
+    // the LDS-DMA span path's conditions (run_stft's `aligned`), one store
+    // instruction per 64 output values, and power rows of this nfft
+    const bool shape_ok = nfft == 1024 && hop % 4 == 0 && hop <= 256 && ((uintptr_t)sig & 15) == 0 &&
+                          (ch_stride & 3) == 0 && mel.M >= 1 && mel.M <= 128 && mel.nc <= 64 * MEL_MAX_ROUNDS &&
+                          (kind == 0 || (mel.C >= 1 && mel.C <= 64 && 2 * mel.M <= ri_floats<1024>() - MEL_LM_OFF));
+    if (!shape_ok || (kind != 0 && kind != 1)) return hipErrorNotSupported;
+    return kind == 0 ? run_stft_mel<3>(sig, n, nch, ch_stride, frames, hop, win, mel, out, out_ch_stride, s)
+                     : run_stft_mel<4>(sig, n, nch, ch_stride, frames, hop, win, mel, out, out_ch_stride, s);
 }
 
 hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,

@@ -119,6 +119,25 @@ bool stft_fused_supported(long long nfft);
 hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,
                        long long nch, long long ch_stride, long long frames, const float* win,
                        void* out, long long out_ch_stride, hipStream_t s);
+// Mel filterbank / log / DCT tables of an MFCC plan (vvhip_mel, device
+// pointers) for the fused signal -> log-mel / MFCC launch
+struct MelArgs {
+    const float* W = nullptr;      // non-zero filter weights, packed (nnz)
+    const int* chunks = nullptr;   // {lo, len, off} per chunk (mel_chunk_schedule)
+    const int* cbeg = nullptr;     // first chunk of each filter [M + 1]
+    const float* D = nullptr;      // DCT-II rows [C][M]
+    const float* lift = nullptr;   // lifter factors [C]
+    int nnz = 0, nc = 0, M = 0, C = 0;
+    float eps = 0.0f;
+};
+// Log-mel (kind 0) or MFCC (kind 1) rows [ch][frame][M or C] straight from the
+// signal: the power rows of launch_stft mode 2 feed k_mel_grp's arithmetic in
+// the same kernel, never written to HBM (bit-identical to the two launches).
+// hipErrorNotSupported when the fused kernel does not take this shape
+// (nfft != 1024, hop / alignment, M > 128, C > 64): the caller runs the two launches.
+hipError_t launch_stft_mel(int kind, long long nfft, long long hop, const float* sig, long long n, long long nch,
+                           long long ch_stride, long long frames, const float* win, const MelArgs& mel, float* out,
+                           long long out_ch_stride, hipStream_t s);
 // Frames given explicitly (stft_process batch): in real[count][nfft] -> cpx[count][nfft]
 hipError_t launch_stft_frames(long long nfft, const float* frames_in, const float* win,
                               float2* out, long long count, hipStream_t s);

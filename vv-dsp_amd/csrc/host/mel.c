@@ -192,6 +192,11 @@ vv_dsp_status vv_dsp_mfcc_process_device(const vv_dsp_mfcc_plan* plan, const vv_
     return (vv_dsp_status)vvhip_mel_device(plan->dev, d_power, num_frames, d_out_mfcc, 1, stream);
 }
 
+/* the plan's device tables, for the fused signal -> mel entries of stft.c */
+__attribute__((visibility("hidden"))) vvhip_mel* vv_amd_mfcc_device_plan(const vv_dsp_mfcc_plan* plan) {
+    return plan ? plan->dev : 0;
+}
+
 vv_dsp_status vv_dsp_log_mel_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power, size_t num_frames,
                                     vv_dsp_real* d_out_log_mel, void* stream) {
     if (!plan || !d_power || !d_out_log_mel) return VV_DSP_ERROR_NULL_POINTER;

@@ -111,6 +111,31 @@ vv_dsp_status vv_dsp_stft_power_device(vv_dsp_stft* h, const vv_dsp_real* d_sign
                                                         out_ch_stride, 2, stream);
 }
 
+__attribute__((visibility("hidden"))) vvhip_mel* vv_amd_mfcc_device_plan(const vv_dsp_mfcc_plan* plan);
+
+static vv_dsp_status stft_mel(vv_dsp_stft* h, const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_signal, size_t n,
+                              size_t nch, size_t ch_stride, vv_dsp_real* d_out, size_t out_ch_stride, void* stream,
+                              size_t* out_frames, int kind) {
+    if (!h || !plan || !d_signal || !d_out) return VV_DSP_ERROR_NULL_POINTER;
+    vvhip_mel* m = vv_amd_mfcc_device_plan(plan);
+    if (!m) return VV_DSP_ERROR_OUT_OF_RANGE;
+    if (out_frames) *out_frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    return (vv_dsp_status)vvhip_stft_mel_device(h->dev, m, d_signal, n, nch, ch_stride, d_out, out_ch_stride, kind,
+                                                stream);
+}
+
+vv_dsp_status vv_dsp_stft_log_mel_device(vv_dsp_stft* h, const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_signal,
+                                         size_t n, size_t nch, size_t ch_stride, vv_dsp_real* d_out,
+                                         size_t out_ch_stride, void* stream, size_t* out_frames) {
+    return stft_mel(h, plan, d_signal, n, nch, ch_stride, d_out, out_ch_stride, stream, out_frames, 0);
+}
+
+vv_dsp_status vv_dsp_stft_mfcc_device(vv_dsp_stft* h, const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_signal,
+                                      size_t n, size_t nch, size_t ch_stride, vv_dsp_real* d_out, size_t out_ch_stride,
+                                      void* stream, size_t* out_frames) {
+    return stft_mel(h, plan, d_signal, n, nch, ch_stride, d_out, out_ch_stride, stream, out_frames, 1);
+}
+
 vv_dsp_status vv_dsp_stft_frames_range_device(vv_dsp_stft* h, const vv_dsp_real* d_signal, size_t n, size_t nch,
                                               size_t ch_stride, size_t frame0, size_t nframes, void* d_out,
                                               size_t out_ch_stride, int out_kind, void* stream) {

@@ -53,6 +53,8 @@ def lib():
     L.vv_dsp_stft_spectrogram_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_spectrum_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_power_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_stft_log_mel_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_stft_mfcc_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_frames_range_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _sz, _sz, _vp, _sz, C.c_int, _vp]
     L.vv_dsp_stft_process_device.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.vv_dsp_stft_reconstruct_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp]
@@ -267,6 +269,27 @@ class Mfcc:
 
     def log_mel(self, power, stream=None):
         return self._run(power, self.n_mels, lib().vv_dsp_log_mel_device, "log_mel_device", stream)
+
+    def from_signal(self, stft, sig, log_mel=False, out=None, stream=None):
+        """Signal (nch, n) or (n,) float32 -> MFCC (nch, frames, n_coeffs), or log-mel
+        (nch, frames, n_mels) with log_mel=True, through `stft`'s power rows without
+        writing them to HBM (vv_dsp_stft_mfcc_device / vv_dsp_stft_log_mel_device):
+        equal to self(stft.power(sig)) / self.log_mel(stft.power(sig))."""
+        sig2 = sig if sig.dim() == 2 else sig.unsqueeze(0)
+        nch, n = sig2.shape
+        if sig2.dtype != torch.float32 or sig2.stride(1) != 1:
+            raise VvError("mel signal: float32 rows with unit sample stride")
+        fr = stft.frames(n)
+        width = self.n_mels if log_mel else self.n_coeffs
+        if out is None:
+            out = torch.empty((nch, fr, width), dtype=torch.float32, device=sig.device)
+        _expect(out, torch.float32, nch * fr * width, "mel output")
+        f = lib().vv_dsp_stft_log_mel_device if log_mel else lib().vv_dsp_stft_mfcc_device
+        nf = _sz(0)
+        _check(f(stft.h, self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * width, _stream(stream),
+                 C.byref(nf)), "stft_mel_device")
+        assert nf.value == fr
+        return out if sig.dim() == 2 else out[0]
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
