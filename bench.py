@@ -320,7 +320,7 @@ def kernel_traffic(prefixes, per_step_calls=None, channels=None):
 
 
 def hbm_traffic(channels):
-    return kernel_traffic(["vvh::k_stft_pair<1024, 0, 4"], channels=channels)
+    return kernel_traffic(["vvh::k_stft_pair<1024, 0, 5"], channels=channels)
 
 
 def gather_leg(out, total_ch, compute_s, frames_per_step, rank, half=True):
@@ -510,7 +510,7 @@ def main():
             "nfft": NFFT, "hop": HOP, "window": "hann (symmetric, window.c:25-36)",
             "output": "[ch][frame][1024] f32 magnitudes (stft.c:133-139)",
             "parallelism": f"dp{world} (channel shards, no data-path collective)"},
-        "roofline": {"kernel": "vvh::k_stft_pair<1024,0,4> (persistent dynamic band walk; LDS-DMA frame spans + "
+        "roofline": {"kernel": "vvh::k_stft_pair<1024,0,5> (persistent dynamic band walk in runs of 2 pairs; LDS-DMA frame spans kept as a ring of 256-float chunks + "
                                "Hann + two frames per 1024-pt complex FFT + |X| rows as full-line streaming stores; "
                                "the zero-padded tail pairs run in the same launch); kernel_ms = HIP events around "
                                "the launch on the launch stream",

@@ -485,6 +485,13 @@ CASES = {
     "mfccsig2": with_env(lambda: case_stft_mel(False), "VVHIP_MEL_FUSED", "0"),
     "stftpowdyn": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_DYN", "1"),
     "stftcdyn": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_DYN", "1"),
+    # probe: dynamic runs of r pairs on a ring (VAR 5)
+    **{f"stftdr{r}": with_env(with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DYN", "2"), "VVHIP_STFT_RUN", str(r))
+       for r in (1, 2, 3, 4, 8, 16)},
+    **{f"stftpowdr{r}": with_env(with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_DYN", "2"),
+                                 "VVHIP_STFT_RUN", str(r)) for r in (2, 4)},
+    **{f"stftcdr{r}": with_env(with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_DYN", "2"),
+                               "VVHIP_STFT_RUN", str(r)) for r in (2, 4)},
     "stftchunk256ch": with_env(lambda: case_stft(256, 600), "VVHIP_STFT_DYN", "0"),
     "stftpowspan": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RING", "0"),
     "stftcspan": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_RING", "0"),

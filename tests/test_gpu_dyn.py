@@ -1,6 +1,7 @@
-"""The dynamically scheduled STFT walk (k_stft_pair VAR 4: persistent grid,
-per-(device, stream) work counters that the kernel's last waves reset) against
-the chunked launch it replaces for large magnitude jobs (VVHIP_STFT_DYN=0):
+"""The dynamically scheduled STFT walks (k_stft_pair VAR 4 / VAR 5: persistent
+grid, per-(device, stream) work counters that the kernel's last waves reset;
+VAR 5 hands out runs of pairs walked on a ring of span chunks) against the
+chunked launch they replace for large jobs (VVHIP_STFT_DYN=0):
 bit-identical rows, repeated launches (the counters must come back to zero),
 two streams at once (each its own counter block), the zero-padded tail and a
 missing second frame (odd frame count), and sampled rows against NumPy f64 at
@@ -70,13 +71,15 @@ def test_dynamic_walk_rows_vs_numpy(job, orc):
         np.testing.assert_allclose(out[c][frames].cpu().numpy(), X, rtol=5e-5, atol=5e-5)
 
 
-@pytest.mark.parametrize("kind", ["power", "complex"])
+@pytest.mark.parametrize("kind", ["magnitude", "power", "complex"])
 def test_dynamic_walk_other_rows(job, kind):
-    """VVHIP_STFT_DYN=1 runs power (n/2+1) and complex rows through the same
-    walk: rows equal to the default launch's, bit for bit."""
+    """VVHIP_STFT_DYN=1 forces VAR 4 (one pair per counter value; magnitude rows
+    default to VAR 5's runs) and runs power (n/2+1) and complex rows through the
+    same walk: rows equal to the chunked launch's, bit for bit."""
     import torch
     sig, st, _ = job
-    run = (lambda: st.power(sig)) if kind == "power" else (lambda: st.spectrogram(sig, complex_out=True))
+    run = {"magnitude": lambda: st.spectrogram(sig), "power": lambda: st.power(sig),
+           "complex": lambda: st.spectrogram(sig, complex_out=True)}[kind]
     os.environ["VVHIP_STFT_DYN"] = "0"
     try:
         ref = run().clone()
@@ -90,3 +93,34 @@ def test_dynamic_walk_other_rows(job, kind):
             assert torch.equal(got, ref)
     finally:
         os.environ["VVHIP_STFT_DYN"] = ""
+
+
+@pytest.mark.parametrize("run_len", ["1", "3", "4", "16"])
+@pytest.mark.parametrize("kind", ["magnitude", "power", "complex"])
+def test_dynamic_ring_runs(job, kind, run_len):
+    """VVHIP_STFT_DYN=2 (VAR 5): the dynamic walk handing out runs of
+    VVHIP_STFT_RUN pairs, each walked on a ring of 256-float chunks -- runs that
+    cross channel ends, a short last run, repeated launches: rows equal to the
+    chunked launch's, bit for bit."""
+    import torch
+    sig, st, ref_mag = job
+    run = {"magnitude": lambda: st.spectrogram(sig), "power": lambda: st.power(sig),
+           "complex": lambda: st.spectrogram(sig, complex_out=True)}[kind]
+    if kind == "magnitude":
+        ref = ref_mag
+    else:
+        os.environ["VVHIP_STFT_DYN"] = "0"
+        try:
+            ref = run().clone()
+        finally:
+            os.environ["VVHIP_STFT_DYN"] = ""
+    os.environ["VVHIP_STFT_DYN"] = "2"
+    os.environ["VVHIP_STFT_RUN"] = run_len
+    try:
+        for _ in range(2):
+            got = run()
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref)
+    finally:
+        os.environ["VVHIP_STFT_DYN"] = ""
+        os.environ["VVHIP_STFT_RUN"] = ""

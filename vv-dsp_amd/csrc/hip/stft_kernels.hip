@@ -463,7 +463,7 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
 // with nt / sc1, bits 9/10 row stores with sc1 / nt (default sc0 sc1 nt).  Results are
 // wrong under bits 0-4 and 6.
 template <int N, int MODE, int VAR, int EXP = 0>
-__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4)) ? ((EXP & 2048) ? 4 : 3) : 1)
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ? ((EXP & 2048) ? 4 : 3) : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink,
@@ -474,11 +474,14 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // (launch_stft_mel; the tables of the MFCC plan in dynamic LDS)
     constexpr bool MEL = MODE == 3 || MODE == 4;
     constexpr bool TAIL = VAR == 2;
-    constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4;
+    constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5;
     // VAR 3: VAR 0 with each wave walking a contiguous run of pairs and its
     // span kept as a ring of 256-float chunks (hop % 256 == 0): a pair DMAs only
     // its 2*hop new samples instead of the whole N + hop span
-    constexpr bool RING = VAR == 3;
+    // VAR 5: the dynamic walk below handing out runs of `rl` consecutive pairs
+    // per counter value, each run walked with VAR 3's ring
+    constexpr bool DRING = VAR == 5;
+    constexpr bool RING = VAR == 3 || DRING;
     // EXP bit 13 (probe): dynamic band walk -- each wave takes its next pair from
     // its XCD's counter (ctr, passed as `sink`): counter value k is pair
     // (k / DB) * 8 DB + xcd * DB + k % DB, so the chip works on one moving band and
@@ -486,7 +489,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // counter atomics are hand-counted VMEM ops like the spans and stores.
     // VAR 4 (the library's bulk launch for magnitude rows of large jobs) is
     // this walk: a persistent grid, counters from stream_counters()
-    constexpr bool DYN = (EXP & 8192) != 0 || VAR == 4;
+    constexpr bool DYN = (EXP & 8192) != 0 || VAR == 4 || DRING;
     // EXP bit 14 (probe): two span buffers per transform slot, the span of pair
     // i+2 DMA'd while pair i is transformed, pair i+1's waited for before pair
     // i's stores (LDS: 2 workgroups per CU instead of 3)
@@ -589,7 +592,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // slot s walks run s of every group
     const long long rl = RING ? (chunk >> 40) : 1;
     long long kk = 0;   // items this slot has done
-    if constexpr (RING) {
+    if constexpr (RING && !DRING) {
         const long long ch = chunk & ((1LL << 40) - 1);
         p = (long long)blockIdx.x * ch + slot * rl;
         p_end = (long long)(blockIdx.x + 1) * ch < pairs ? (long long)(blockIdx.x + 1) * ch : pairs;
@@ -623,11 +626,15 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         unsigned r0 = 0;
         if (t == 0)
             asm volatile("global_atomic_add %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)" : "=v"(r0) : "v"(ctr), "v"(1u) : "memory");
-        grab();
-        unsigned k1;
-        asm volatile("s_waitcnt vmcnt(0)\n\tv_readfirstlane_b32 %0, %1" : "=s"(k1) : "v"(rr) : "memory");
-        p = band_pair(__builtin_amdgcn_readfirstlane(r0));
-        pn = band_pair(k1);
+        if constexpr (DRING) {   // counter value k -> the run of pairs [rl b(k), rl b(k) + rl)
+            p = rl * band_pair(__builtin_amdgcn_readfirstlane(r0));
+        } else {
+            grab();
+            unsigned k1;
+            asm volatile("s_waitcnt vmcnt(0)\n\tv_readfirstlane_b32 %0, %1" : "=s"(k1) : "v"(rr) : "memory");
+            p = band_pair(__builtin_amdgcn_readfirstlane(r0));
+            pn = band_pair(k1);
+        }
     }
     const bool any = p < p_end;   // uniform per transform
     // (channel, first frame) of a pair; this launch covers frames
@@ -718,7 +725,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     const int nd = D2 ? (int)((N + hop + 255) >> 8) : 0;
     bool d2_async = false;
     if constexpr (DYN) {
-        if (any && pn < pairs) grab();   // -> the pair after pn
+        if constexpr (DRING) {
+            if (any) grab();   // -> the next run
+        } else {
+            if (any && pn < pairs) grab();   // -> the pair after pn
+        }
     }
     if constexpr ((EXP & 2048) != 0) {
         for (int i = threadIdx.x; i < TWE; i += WG) ltab[i] = gpass[i];
@@ -740,8 +751,17 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     if constexpr (GLDS) vm_wait<0>();
     if constexpr (RING) rs = rsn;
     for (; p < p_end; p += p_step) {
-        if constexpr (RING) p_step = ((kk + 1) % rl) ? 1 : (long long)F * rl - rl + 1;
-        if constexpr (DYN) p_step = pn - p;
+        if constexpr (DRING) {
+            // the last grabbed run: its atomic is older than the previous pair's
+            // NST stores (issued with the DMA of its run's first pair)
+            unsigned kq;
+            asm volatile("s_waitcnt vmcnt(%1)\n\tv_readfirstlane_b32 %0, %2" : "=s"(kq) : "n"(NST), "v"(rr) : "memory");
+            const long long pq = p + 1 >= pairs ? pairs : kk + 1 < rl ? p + 1 : rl * band_pair(kq);
+            p_step = uni<G::T>(pq - p);
+        } else if constexpr (RING) {
+            p_step = ((kk + 1) % rl) ? 1 : (long long)F * rl - rl + 1;
+        }
+        if constexpr (DYN && !DRING) p_step = pn - p;
         const bool more = p + p_step < p_end;
         long long cn = c, fn = fa;
         if constexpr (RING) {   // within a run: the next pair, or frame 2*pair0 of the next channel
@@ -758,7 +778,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (more) locate(p + p_step, &cn, &fn);
         }
         if constexpr (RING) {
-            vm_wait<NST>();
+            if constexpr (!DRING) vm_wait<NST>();
             // chunk slots of frame a (chunks 0..3) and frame b (chunks hb..hb+3)
             int ca[4], cbk[4];
 #pragma unroll
@@ -776,6 +796,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (more) {
                 if (p_step == 1 && cn == c && fn * hop + (N + hop) <= n) issue_new(cn, fn);
                 else load_pair(cn, fn);
+                if constexpr (DRING) {
+                    if (kk + 1 == rl) grab();   // the next pair starts a run: fetch the one after it
+                }
             }
         } else if constexpr (DYN) {
             // this span's DMA and the counter atomic issued after it are older
@@ -908,7 +931,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         fa = fn;
         if constexpr (RING) {
             rs = rsn;
-            ++kk;
+            if constexpr (DRING) kk = kk + 1 == rl ? 0 : kk + 1;
+            else ++kk;
         }
         if constexpr (D2) ++kk;
     }
@@ -1049,7 +1073,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         long long mpc = (nfull < frames ? nfull : frames) / 2;
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
-        static std::atomic<int> capc[5];   // zero-initialised (static storage)
+        static std::atomic<int> capc[6];   // zero-initialised (static storage)
         // The bulk launch is NOT persistent: one workgroup per `cps` pairs per
         // transform slot, so the hardware dispatcher balances the CUs and the
         // launch has no straggler tail (measured 8-13 % faster than the
@@ -1078,7 +1102,14 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 chunk = cps * F;
                 grid = (nch * cnt + chunk - 1) / chunk;
             }
-            if (var == 4) grid = capv / 8 * 8;   // persistent, the same number of blocks per XCD group
+            if (var == 4 || var == 5) grid = capv / 8 * 8;   // persistent, the same number of blocks per XCD group
+            if (var == 5) {   // pairs per counter value; VVHIP_STFT_RUN overrides (A/B)
+                long long rl = 2;
+                const char* eru = getenv("VVHIP_STFT_RUN");
+                if (eru && *eru) rl = atoll(eru);
+                if (rl < 1 || rl > 64) rl = 2;
+                chunk = rl << 40;
+            }
             if (var == 3) {   // run length (pairs), a divisor of cps; VVHIP_STFT_RUN overrides (A/B)
                 long long rl = cps;
                 const char* eru = getenv("VVHIP_STFT_RUN");
@@ -1126,7 +1157,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         bool dyn = false;
         if constexpr (Geo<N>::T == 64) {
             const int capd = cached_grid(capc[4], (const void*)k_stft_pair<N, MODE, 4>, WG, 0, 1LL << 40);
-            const bool want = ed && *ed ? *ed == '1' : (MODE == 0 || MODE == 1);
+            const bool want = ed && *ed ? *ed != '0' : (MODE == 0 || MODE == 1);
             dyn = aligned && FUSE_TAIL && want && capd >= 8 &&
                   bulk_pairs >= 16LL * F * capd;   // >= 16 pairs per wave: the band walk pays off
             if (dyn) {
@@ -1134,7 +1165,15 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 if (!ctrs) return hipErrorOutOfMemory;
             }
         }
-        if (dyn) {
+        // Magnitude rows with whole-chunk hops: the dynamic walk in runs of 2
+        // pairs on a ring (VAR 5): 3.357 vs 3.440 ms (VAR 4) vs 3.501 ms (chunked)
+        // for 32 ch x 10 min, runs of 1 / 3 / 4 / 8 / 16 slower; power and complex
+        // rows measured 1-4 % slower with it (profiles/r03_kbench_dynring.jsonl).
+        // VVHIP_STFT_DYN = 1 / 2 forces VAR 4 / VAR 5 (A/B)
+        const bool dring = ed && *ed ? *ed == '2' : MODE == 0;
+        if (dyn && dring && hop % 256 == 0) {
+            if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 5>, 5, 0LL, ppc);
+        } else if (dyn) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 4>, 4, 0LL, ppc);
         } else if (aligned && FUSE_TAIL && ring) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 3>, 3, 0LL, ppc);
