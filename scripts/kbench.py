@@ -473,6 +473,8 @@ CASES = {
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
                                                                           256, 320)},
+    **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
+       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152,
                                                                          2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194,
@@ -488,6 +490,9 @@ CASES = {
     # probe: dynamic runs of r pairs on a ring (VAR 5)
     **{f"stftdr{r}": with_env(with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DYN", "2"), "VVHIP_STFT_RUN", str(r))
        for r in (1, 2, 3, 4, 8, 16)},
+    **{f"stftdb{d}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DBS", str(d)) for d in (2, 3, 4, 5, 6, 7, 8)},
+    **{f"stftdb{d}r1": with_env(with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DBS", str(d)), "VVHIP_STFT_RUN", "1")
+       for d in (5, 6, 7)},
     **{f"stftpowdr{r}": with_env(with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_DYN", "2"),
                                  "VVHIP_STFT_RUN", str(r)) for r in (2, 4)},
     **{f"stftcdr{r}": with_env(with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_DYN", "2"),

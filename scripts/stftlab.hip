@@ -28,6 +28,23 @@ static hipError_t lab_launch(const float* sig, long long n, long long nch, const
                        0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk, sink, ctr, MelArgs{});
     return hipGetLastError();
 }
+// the product's magnitude launch for large jobs: k_stft_pair<1024, 0, 5, EXP> (persistent,
+// dynamic walk in runs of 2 pairs on a span ring, band 2^6 runs per stream)
+template <int EXP>
+static hipError_t lab_launch5(const float* sig, long long n, long long nch, const float* win, float* out,
+                              hipStream_t s) {
+    constexpr int N = 1024;
+    const long long hop = 256, frames = n < N ? 1 : 1 + (n - N + hop) / hop, ppc = (frames + 1) / 2;
+    static std::atomic<int> cap;
+    const int capv = cached_grid(cap, (const void*)k_stft_pair<N, 0, 5, EXP>, 256, 0, 1LL << 40);
+    const long long chunk = (2LL << 40) | 6;
+    unsigned* ctr = stream_counters(s);
+    if (!ctr) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL((k_stft_pair<N, 0, 5, EXP>), dim3((unsigned)(capv / 8 * 8)), dim3(256), 0, s, sig, n, nch, n,
+                       frames, hop, 0LL, ppc, win, (void*)out, frames * N, pass_twiddles(N), twiddle_table(N), chunk,
+                       store_sink(), ctr, MelArgs{});
+    return hipGetLastError();
+}
 // config 4's bulk launch (8 ch x 2^24, 257 taps: N 1024, le 256) of k_fir_bulk<1024, true, EXP>
 template <int EXP>
 static hipError_t lab_fir(const float2* H, const float* x, float* y, long long n, long long nch, hipStream_t s) {
@@ -117,6 +134,17 @@ extern "C" int stftlab_run(int exp, const float* sig, long long n, long long nch
         C(16) C(18) C(24) C(26) C(32) C(34) C(40) C(42) C(64) C(66) C(68) C(80) C(82)
         C(128) C(256) C(512) C(1024) C(640) C(1152) C(2048) C(2050) C(2052) C(2056) C(4096) C(4098) C(8192) C(8194)
         C(16384) C(16448)
+#undef C
+        default: return -1;
+    }
+}
+
+extern "C" int stftlab5_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
+                            void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (exp) {
+#define C(E) case E: return (int)vvh::lab_launch5<E>(sig, n, nch, win, out, s);
+        C(0) C(2) C(4) C(6) C(8) C(10) C(16) C(18) C(32) C(34) C(512) C(514) C(1024) C(1026)
 #undef C
         default: return -1;
     }

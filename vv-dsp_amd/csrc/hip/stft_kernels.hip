@@ -613,9 +613,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // atomic per workgroup of its XCD per pair
     const int stream = __builtin_amdgcn_readfirstlane((int)(blockIdx.x & 7) * F + slot);
     unsigned* const ctr = DYN ? ctrs + 32 * stream : nullptr;
-    constexpr long long DB = 64;
+    // DB = 2^dbs consecutive items per stream and band (VAR 5: log2 in chunk's low bits)
+    const int dbs = DRING ? (int)(chunk & 15) : 6;
     auto band_pair = [&](unsigned k) -> long long {
-        return (long long)(k / DB) * (8 * F * DB) + (long long)stream * DB + (long long)(k % DB);
+        const long long DB = 1LL << dbs;
+        return (long long)(k >> dbs) * (8 * F * DB) + (long long)stream * DB + (long long)(k & (DB - 1));
     };
     unsigned rr = 0;   // lane 0: an issued counter atomic's result (valid after a vmcnt wait)
     auto grab = [&]() {
@@ -1108,7 +1110,11 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 const char* eru = getenv("VVHIP_STFT_RUN");
                 if (eru && *eru) rl = atoll(eru);
                 if (rl < 1 || rl > 64) rl = 2;
-                chunk = rl << 40;
+                long long dbs = 6;   // band: 2^dbs runs per (XCD group, slot) stream; VVHIP_STFT_DBS (A/B)
+                const char* edb = getenv("VVHIP_STFT_DBS");
+                if (edb && *edb) dbs = atoll(edb);
+                if (dbs < 0 || dbs > 12) dbs = 6;
+                chunk = (rl << 40) | dbs;
             }
             if (var == 3) {   // run length (pairs), a divisor of cps; VVHIP_STFT_RUN overrides (A/B)
                 long long rl = cps;
