@@ -504,6 +504,8 @@ CASES = {
     **{f"stftrun{r}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RUN", str(r)) for r in (1, 2, 4, 8, 16)},
     **{f"stftpowrun{r}": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RUN", str(r)) for r in (1, 2, 4, 8, 16)},
     "stft60": lambda: case_stft(1, 60),
+    "stft60cps1": with_env(lambda: case_stft(1, 60), "VVHIP_STFT_CPS", "1"),
+    "stft60ring": with_env(lambda: case_stft(1, 60), "VVHIP_STFT_RING", "1"),
     "stftpow": lambda: case_stft_power(32, 600),
     "stftpowold": with_env(lambda: case_stft_power(32, 600), "VVHIP_POW_OLD", "1"),
     "stftc": lambda: case_stft(8, 600, complex_out=True),
