@@ -286,6 +286,16 @@ def case_lab(e, nch=32, seconds=600, fn="stftlab_run"):
         byts, (sig, win, out, lib)
 
 
+def case_empty(grid):
+    """an empty kernel of grid x 256 threads (scripts/stftlab.hip emptylab_run): launch +
+    kernel-boundary floor; bytes = config 3's, for a comparable frac column"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
+    lib.emptylab_run.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    s = torch.cuda.current_stream().cuda_stream
+    return (lambda: lib.emptylab_run(grid, s)), 57591808, (lib,)
+
+
 def case_firreglab(e, nch=8, n=1 << 24):
     """the product's k_fir_bulk_reg with parts switched off (scripts/stftlab.hip firreglab_run:
     2 no FFTs, 4 no stores, 8 no loads)"""
@@ -473,6 +483,8 @@ CASES = {
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
                                                                           256, 320)},
+    **{f"lab60_{e}": (lambda e=e: case_lab(e, nch=1, seconds=60)) for e in (0, 2, 4, 6, 8, 10, 14, 32782, 65550, 98318)},
+    **{f"empty{g}": (lambda g=g: case_empty(g)) for g in (703, 2048)},
     **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
        for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,

@@ -10,6 +10,9 @@
 #include "../vv-dsp_amd/csrc/hip/fft_kernels.hip"
 
 namespace vvh {
+__global__ void __launch_bounds__(256) k_lab_empty(float* sink, int flag) {
+    if (flag == 12345 && threadIdx.x == 0) sink[blockIdx.x] = 1.0f;
+}
 template <int EXP>
 static hipError_t lab_launch(const float* sig, long long n, long long nch, const float* win, float* out,
                              hipStream_t s) {
@@ -133,7 +136,7 @@ extern "C" int stftlab_run(int exp, const float* sig, long long n, long long nch
         C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15)
         C(16) C(18) C(24) C(26) C(32) C(34) C(40) C(42) C(64) C(66) C(68) C(80) C(82)
         C(128) C(256) C(512) C(1024) C(640) C(1152) C(2048) C(2050) C(2052) C(2056) C(4096) C(4098) C(8192) C(8194)
-        C(16384) C(16448)
+        C(16384) C(16448) C(32782) C(65550) C(98318)
 #undef C
         default: return -1;
     }
@@ -148,4 +151,10 @@ extern "C" int stftlab5_run(int exp, const float* sig, long long n, long long nc
 #undef C
         default: return -1;
     }
+}
+
+// an empty kernel of `grid` x 256 threads: the launch + boundary floor of config 3
+extern "C" int emptylab_run(int grid, void* stream) {
+    hipLaunchKernelGGL(vvh::k_lab_empty, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, vvh::store_sink(), 0);
+    return (int)hipGetLastError();
 }

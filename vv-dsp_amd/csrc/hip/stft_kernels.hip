@@ -533,7 +533,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     vf2_t wp[(G::P + 1) / 2];
 #pragma unroll
     for (int r = 0; r < G::P; ++r) {
-        const float wr = 0.5f * win[t + r * G::T];
+        const float wr = (EXP & 65536) ? 0.5f : 0.5f * win[t + r * G::T];   // bit 16 (probe): no window loads
         if (r & 1) wp[r / 2].y = wr;
         else wp[r / 2] = vf2_t{wr, 0.0f};
     }
@@ -733,7 +733,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (any && pn < pairs) grab();   // -> the pair after pn
         }
     }
-    if constexpr ((EXP & 2048) != 0) {
+    if constexpr ((EXP & 32768) != 0) {   // bit 15 (probe): no twiddle staging
+    } else if constexpr ((EXP & 2048) != 0) {
         for (int i = threadIdx.x; i < TWE; i += WG) ltab[i] = gpass[i];
     } else {
         stage_twiddles<N, WG>(ltab, gpass, gtab);
