@@ -124,3 +124,24 @@ def test_dynamic_ring_runs(job, kind, run_len):
     finally:
         os.environ["VVHIP_STFT_DYN"] = ""
         os.environ["VVHIP_STFT_RUN"] = ""
+
+
+@pytest.mark.parametrize("hop", [128, 512])
+def test_dynamic_walks_other_hops(vdev, hop):
+    """hop 512 (a 6-chunk ring refilled 4 chunks per pair) takes VAR 5, hop 128
+    (not whole chunks) VAR 4: rows equal to the chunked launch's, bit for bit,
+    for a multi-channel job past the dynamic-walk threshold."""
+    import torch
+    nch, n = 5, 4 * 60 * 48000 + 4097
+    g = torch.Generator(device="cuda").manual_seed(hop)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
+    st = vdev.Stft(1024, hop)
+    os.environ["VVHIP_STFT_DYN"] = "0"
+    try:
+        ref = st.spectrogram(sig).clone()
+    finally:
+        os.environ["VVHIP_STFT_DYN"] = ""
+    for _ in range(2):
+        got = st.spectrogram(sig)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
