@@ -482,7 +482,7 @@ CASES = {
     **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2, 4, 6)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
-                                                                          256, 320)},
+                                                                          256, 258, 266)},
     **{f"lab60_{e}": (lambda e=e: case_lab(e, nch=1, seconds=60)) for e in (0, 2, 4, 6, 8, 10, 14, 32782, 65550, 98318)},
     **{f"empty{g}": (lambda g=g: case_empty(g)) for g in (703, 2048)},
     **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
@@ -528,6 +528,7 @@ CASES = {
     "filtfilt": lambda: case_fir_direct(8, 1 << 24, filtfilt=True),
     "filtfiltlds": with_env(lambda: case_fir_direct(8, 1 << 24, filtfilt=True), "VVHIP_FIR_DIRECT_LDS", "1"),
     "firspan": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_REG", "0"),
+    "firstatic": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_DYN", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),

@@ -75,9 +75,10 @@ static hipError_t lab_firreg(const float2* H, const float* x, float* y, long lon
     static std::atomic<int> cap;
     const int capv = cached_grid(cap, (const void*)k_fir_bulk_reg<N, EXP>, 256, 0, 1LL << 40);
     const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
-    const int grid = (EXP & 64) ? (int)((nch * cnt + 31) / 32) : (EXP & 128) ? capv / 8 * 8 : (int)(need < capv ? need : capv);
+    const int grid = (EXP & 64) ? (int)((nch * cnt + 31) / 32) : (EXP & (128 | 256)) ? capv / 8 * 8 : (int)(need < capv ? need : capv);
+    unsigned* ctr = (EXP & 256) ? stream_counters(s) : nullptr;
     hipLaunchKernelGGL((k_fir_bulk_reg<N, EXP>), dim3(grid), dim3(256), 0, s, H, x, y, nch, n, n, cnt, qf,
-                       pass_twiddles(N), n, (const float*)nullptr, le, qf, ql);
+                       pass_twiddles(N), n, (const float*)nullptr, le, qf, ql, ctr);
     return hipGetLastError();
 }
 template <int EXP>
@@ -123,6 +124,7 @@ extern "C" int firreglab_run(int exp, const void* H, const float* x, float* y, l
     switch (exp) {
 #define C(E) case E: return (int)vvh::lab_firreg<E>(h, x, y, n, nch, s);
         C(0) C(2) C(4) C(6) C(8) C(10) C(12) C(14) C(16) C(32) C(64) C(80) C(18) C(34) C(66) C(82) C(128) C(144) C(130)
+        C(256) C(258) C(266)
 #undef C
         default: return -1;
     }

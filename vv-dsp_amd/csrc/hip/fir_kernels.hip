@@ -325,13 +325,16 @@ k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long n
 // EXP: timing ablations for scripts/stftlab.hip only (library: EXP = 0): bit 1 no
 // FFTs, bit 2 no output stores, bit 3 no input loads (results are wrong); bit 4
 // stores as sc0 sc1 nt, bit 5 plain stores, bit 6 non-persistent walk (8 pairs per
-// wave, the launcher sizes the grid).
+// wave, the launcher sizes the grid), bit 8 the dynamic band walk of k_stft_pair
+// VAR 4 (persistent grid, each wave's next pair from a per-(XCD group, slot)
+// counter in `ctrs`, the last wave of each counter stream resets it).
 template <int N, int EXP = 0>
 __global__ void __launch_bounds__(256, 4)
 k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
                long long cnt, long long q0, const float2* gpass, long long n, const float* prefix, long long lm1,
-               long long qf, long long ql) {
+               long long qf, long long ql, unsigned* ctrs) {
     using G = Geo<N>;
+    constexpr bool DYN = (EXP & 256) != 0;
     static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
     constexpr int F = 4, RL = G::RL;
     constexpr int LE = N / 4, LOUT = N - LE;   // taps <= N/4 + 1
@@ -349,19 +352,36 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
     __syncthreads();
     float2* my = reinterpret_cast<float2*>(xch + slot * XW);
     long long p, p_end, p_step;
-    if constexpr (EXP & 64) work_walk(nch * cnt, F, slot, 8 * F, &p, &p_end, &p_step);
-    else if constexpr (EXP & 128) band_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
-    else xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
-    p = uni<64>(p);
-    p_end = uni<64>(p_end);
-    p_step = uni<64>(p_step);
-    if (p >= p_end) return;
+    // DYN: counter value k of stream s (= XCD group, slot) is pair
+    // (k / 64) * 8 F 64 + s * 64 + k % 64: the chip sweeps one moving band
+    const int stream = __builtin_amdgcn_readfirstlane((int)(blockIdx.x & 7) * F + slot);
+    unsigned* const ctr = DYN ? ctrs + 32 * stream : nullptr;
+    auto band_pair = [&](unsigned k) -> long long {
+        return (long long)(k >> 6) * (8 * F * 64) + (long long)stream * 64 + (long long)(k & 63);
+    };
+    unsigned rk = 0;   // lane 0: the counter value of the pair after p
+    if constexpr (DYN) {
+        unsigned r0 = 0;
+        if (t == 0) r0 = atomicAdd(ctr, 1u);
+        p = band_pair(__builtin_amdgcn_readfirstlane(r0));
+        p_end = nch * cnt;
+        p_step = 0;
+        if (p < p_end && t == 0) rk = atomicAdd(ctr, 1u);
+    } else {
+        if constexpr (EXP & 64) work_walk(nch * cnt, F, slot, 8 * F, &p, &p_end, &p_step);
+        else if constexpr (EXP & 128) band_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+        else xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+        p = uni<64>(p);
+        p_end = uni<64>(p_end);
+        p_step = uni<64>(p_step);
+        if (p >= p_end) return;
+    }
     auto locate = [&](long long it, long long* cc, long long* jj) {
         *cc = it / cnt;
         *jj = 2 * (q0 + (it - *cc * cnt));
     };
-    long long c, j;
-    locate(p, &c, &j);
+    long long c = 0, j = 0;
+    if (p < p_end) locate(p, &c, &j);
     float xa[G::P], xb[G::P];
     auto load_a = [&](long long cc, long long jj) {
         if constexpr (EXP & 8) return;
@@ -386,11 +406,12 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 #pragma unroll
         for (int r = 0; r < G::P; ++r) xa[r] = xb[r] = (float)(t + r);
     }
-    if (!is_edge(j)) {
+    if (p < p_end && !is_edge(j)) {
         load_a(c, j);
         load_b(c, j);
     }
     for (; p < p_end; p += p_step) {
+        if constexpr (DYN) p_step = band_pair(__builtin_amdgcn_readfirstlane(rk)) - p;
         const bool more = p + p_step < p_end;
         long long cn = c, jn = j;
         if (more) locate(p + p_step, &cn, &jn);
@@ -438,6 +459,9 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
             load_a(cn, jn);
             load_b(cn, jn);
         }
+        if constexpr (DYN) {
+            if (more && t == 0) rk = atomicAdd(ctr, 1u);   // -> the pair after cn/jn
+        }
         float* ya = y + c * y_stride + j * LOUT - LE;   // + e: block j output (e >= LE)
         if (is_edge(j)) {   // outputs past n are not stored
             long long rem = n - (j * LOUT - LE + t);   // this lane's outputs below n: e < rem
@@ -483,6 +507,15 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
         }
         c = cn;
         j = jn;
+    }
+    if constexpr (DYN) {   // the XCD group's last wave out resets its counters for the next launch
+        if (t == 0) {
+            const unsigned nw = (unsigned)((gridDim.x - (blockIdx.x & 7) + 7) / 8);
+            if (atomicAdd(ctr + 16, 1u) == nw - 1) {
+                atomicExch(ctr, 0u);
+                atomicExch(ctr + 16, 0u);
+            }
+        }
     }
 }
 
@@ -537,12 +570,24 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
         // [ql, ppc) take the kernel's bounds-checked branch (round 2 ran them as a
         // second, latency-bound launch: 11 us of config 4's 237)
         if constexpr (FIR_BULK<N>) {
-            static std::atomic<int> capc_r;
+            static std::atomic<int> capc_r, capc_rd;
+            // the dynamic band walk (k_fir_bulk_reg EXP bit 8): 0.2385 -> 0.2323 ms
+            // for config 4, same buffers, bit-identical (profiles/r03_kbench_fir_dyn.jsonl);
+            // VVHIP_FIR_DYN = 0 keeps the static XCD walk (A/B switch, read per call)
+            const char* ed = getenv("VVHIP_FIR_DYN");
+            if (!(ed && *ed == '0')) {
+                const int cap_d = cached_grid(capc_rd, (const void*)k_fir_bulk_reg<N, 256>, 256, 0, 1LL << 40);
+                unsigned* ctrs = stream_counters(s);
+                if (!ctrs || cap_d < 8) return hipErrorOutOfMemory;
+                hipLaunchKernelGGL((k_fir_bulk_reg<N, 256>), dim3(cap_d / 8 * 8), dim3(256), 0, s, H, x, y, nch,
+                                   x_stride, y_stride, ppc, 0LL, pN, n, prefix, lm1, qf, ql, ctrs);
+                return hipGetLastError();
+            }
             const int cap_r = cached_grid(capc_r, (const void*)k_fir_bulk_reg<N>, 256, 0, 1LL << 40);
             const long long need = (nch * ppc + 3) / 4;
             const int grid = (int)(need < cap_r ? need : cap_r);
             hipLaunchKernelGGL((k_fir_bulk_reg<N>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, ppc,
-                               0LL, pN, n, prefix, lm1, qf, ql);
+                               0LL, pN, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
         }
         return hipGetLastError();
     } else if (ql > qf && le == N / 4 && !old) {
