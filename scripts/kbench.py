@@ -440,6 +440,7 @@ CASES = {
     "blue48000": lambda: case_c2c(48000, 1024),
     "blue48000nomix": with_env(lambda: case_c2c(48000, 1024), "VVHIP_NO_MIXED", "1"),
     "mix44100": lambda: case_c2c(44100, 1024),
+    "mix192000": lambda: case_c2c(192000, 256),
     "mix96000": lambda: case_c2c(96000, 512),
     "blue48000unf": with_env(lambda: case_c2c(48000, 1024), "VVHIP_BLUE_UNFUSED", "1"),
     "blue48000old": with_env(lambda: case_c2c(48000, 1024), "VVHIP_FS_OLD", "1"),

@@ -133,7 +133,8 @@ def test_stft_smooth_device_kinds(vdev, nfft, hop, nch, n):
         np.testing.assert_allclose(pw[c], np.abs(X[:, :nfft // 2 + 1]) ** 2, rtol=2 * r, atol=2 * a * nfft)
 
 
-LARGE = [4800, 11025, 16807, 24576 * 3, 44100, 48000, 88200, 96000]
+LARGE = [4800, 11025, 16807, 24576 * 3, 44100, 48000, 88200, 96000,
+         16000, 22050, 24000, 32000, 176400, 192000, 480000]
 
 
 @pytest.mark.parametrize("n", LARGE)
