@@ -361,6 +361,15 @@ k_fft_mixed_fs(MixedPlan pl, FsIO io, long long groups, const float2* __restrict
     float2* buf = sm + m + slot * m;
     float2* bufs = sm + m;
     for (int i = lt; i < m; i += 256) tab[i] = gtab[i];
+    // PASS 0: the two-level W_n table (2 sqrt(n) entries) in LDS after the
+    // tile, so the twiddle of each stored element is two LDS reads instead of
+    // two dependent global loads
+    const int nlo = 1 << io.lo_bits;
+    float2* const ltw = sm + (long long)m * (1 + F);
+    if constexpr (PASS == 0) {
+        const int ntw = nlo + (int)((io.n + nlo - 1) >> io.lo_bits);
+        for (int i = lt; i < ntw; i += 256) ltw[i] = io.twn[i];
+    }
     __syncthreads();
     const int N1 = io.N1, N2 = io.N2;
     const int width = PASS == 0 ? N2 : N1;   // columns or rows per transform of the batch
@@ -402,7 +411,7 @@ k_fft_mixed_fs(MixedPlan pl, FsIO io, long long groups, const float2* __restrict
                 const int k1 = idx / F, sl = idx % F, col = i0 + sl;
                 if (col < N2) {
                     const int tw = col * k1;   // < n <= 2^24
-                    const float2 w = cmul(io.twn[tw & ((1 << io.lo_bits) - 1)], io.twn[(1 << io.lo_bits) + (tw >> io.lo_bits)]);
+                    const float2 w = cmul(ltw[tw & (nlo - 1)], ltw[nlo + (tw >> io.lo_bits)]);
                     dst[(long long)k1 * N2 + col] = cmul(bufs[sl * m + k1], w);
                 }
             }
@@ -947,7 +956,8 @@ hipError_t run_fs_t(const MixedPlan& pl, const FsIO& io0, long long batch, hipSt
     FsIO io = io0;
     io.groups_per_b = ((PASS == 0 ? io.N2 : io.N1) + F - 1) / F;
     const long long groups = batch * io.groups_per_b;
-    const size_t lds = sizeof(float2) * (size_t)pl.n * (1 + F);
+    const long long nlo = 1LL << io.lo_bits;
+    const size_t lds = sizeof(float2) * ((size_t)pl.n * (1 + F) + (PASS == 0 ? (size_t)(nlo + ((io.n + nlo - 1) >> io.lo_bits)) : 0));
     const int grid = persistent_grid((const void*)k_fft_mixed_fs<T, PASS>, 256, lds, groups);
     hipLaunchKernelGGL((k_fft_mixed_fs<T, PASS>), dim3(grid), dim3(256), lds, s, pl, io, groups, tab);
     return hipGetLastError();
