@@ -111,6 +111,26 @@ def test_real_large_pow2(amd, n):
     assert _normwise(y, xr) <= 1e-5
 
 
+@pytest.mark.parametrize("n,b", [(1 << 15, 3), (1 << 16, 5), (1 << 17, 2)])
+def test_real_large_pow2_batched(vdev, n, b):
+    """Batched R2C / C2R above the fused kernels: the n/2-point four-step plus the
+    split kernels (k_real_split_fwd / _inv, bins j and n/2 - j per thread), every
+    row against NumPy f64 (normwise, 4x SciPy's f32 error) and round trip."""
+    import scipy.fft
+    import torch
+    rng = np.random.default_rng(n + b)
+    xr = (rng.random((b, n)) - 0.5).astype(np.float32)
+    X = vdev.FftPlan(n, vdev.R2C, vdev.FWD, batch=b)(torch.from_numpy(xr).cuda())
+    Xh = X.cpu().numpy()
+    for i in range(b):
+        ref = np.fft.rfft(xr[i].astype(np.float64))
+        assert Xh[i, -1].imag == 0.0 and Xh[i, 0].imag == 0.0
+        assert _normwise(Xh[i], ref) <= max(4 * _normwise(scipy.fft.rfft(xr[i]), ref), 1e-6), i
+    y = vdev.FftPlan(n, vdev.C2R, vdev.BWD, batch=b)(X).cpu().numpy()
+    for i in range(b):
+        assert _normwise(y[i], xr[i]) <= 1e-5, i
+
+
 @pytest.mark.parametrize("n", [1025, 3000, 48000, 100003])
 def test_c2c_bluestein(amd, orc, n):
     """Non-power-of-two lengths from 1025 on run Bluestein over the power-of-two

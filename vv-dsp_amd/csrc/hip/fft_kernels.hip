@@ -373,56 +373,67 @@ __device__ __forceinline__ float2 tw_split_at(const float2* __restrict__ tab, lo
     return cmul(tab[k & mask], tab[(1LL << lo_bits) + (k >> lo_bits)]);
 }
 
-// Z: [batch][M] -> X: [batch][M+1] (bins 0..n/2 of the real rows)
+// Z: [batch][M] -> X: [batch][M+1] (bins 0..n/2 of the real rows).  Thread j of
+// row f (blockIdx.y) makes bins j and M - j from the same two loads z[j], z[M-j]
+// (each bin's twiddle from the table as before, so the bins are unchanged);
+// 32-bit indices within a row.
 __global__ void k_real_split_fwd(const float2* __restrict__ Z, float2* __restrict__ X, long long M, long long batch,
                                  const float2* __restrict__ tab, int lo_bits) {
-    const long long nh = M + 1, total = nh * batch;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const long long f = i / nh, k = i - f * nh;
+    const int m = (int)M, h = m / 2;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > h) return;
+    for (long long f = blockIdx.y; f < batch; f += gridDim.y) {
         const float2* z = Z + f * M;
-        float2 x;
-        if (k == 0 || k == M) {   // DC and Nyquist (fft_kiss.c:141-143: imaginary part 0)
-            const float2 a = z[0];
-            x = make_float2(k == 0 ? a.x + a.y : a.x - a.y, 0.0f);
+        float2* x = X + f * (M + 1);
+        const float2 a = z[j];
+        if (j == 0) {   // DC and Nyquist (fft_kiss.c:141-143: imaginary part 0)
+            x[0] = make_float2(a.x + a.y, 0.0f);
+            x[m] = make_float2(a.x - a.y, 0.0f);
+        } else if (j == h && 2 * h == m) {
+            x[j] = split_fwd(a, cconj(a), tw_split_at(tab, j, lo_bits));
         } else {
-            x = split_fwd(z[k], cconj(z[M - k]), tw_split_at(tab, k, lo_bits));
+            const float2 b = z[m - j];
+            x[j] = split_fwd(a, cconj(b), tw_split_at(tab, j, lo_bits));
+            x[m - j] = split_fwd(b, cconj(a), tw_split_at(tab, m - j, lo_bits));
         }
-        X[i] = x;
     }
 }
 
 // X: [batch][M+1] -> V: [batch][M], the inverse split (imaginary parts of DC and
-// Nyquist ignored, the fft_kiss.c:158-171 result), before the M-point inverse
+// Nyquist ignored, the fft_kiss.c:158-171 result), before the M-point inverse;
+// thread j makes V[j] and V[M-j] from x[j], x[M-j]
 __global__ void k_real_split_inv(const float2* __restrict__ X, float2* __restrict__ V, long long M, long long batch,
                                  const float2* __restrict__ tab, int lo_bits) {
-    const long long total = M * batch;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const long long f = i / M, k = i - f * M;
+    const int m = (int)M, h = m / 2;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > h) return;
+    for (long long f = blockIdx.y; f < batch; f += gridDim.y) {
         const float2* x = X + f * (M + 1);
-        float2 A = x[k], B;
-        if (k == 0) {
-            A.y = 0.0f;
-            B = make_float2(x[M].x, 0.0f);
+        float2* v = V + f * M;
+        float2 a = x[j];
+        if (j == 0) {
+            a.y = 0.0f;
+            v[0] = split_inv(a, make_float2(x[m].x, 0.0f), tw_split_at(tab, 0, lo_bits));
+        } else if (j == h && 2 * h == m) {
+            v[j] = split_inv(a, a, tw_split_at(tab, j, lo_bits));
         } else {
-            B = x[M - k];
+            const float2 b = x[m - j];
+            v[j] = split_inv(a, b, tw_split_at(tab, j, lo_bits));
+            v[m - j] = split_inv(b, a, tw_split_at(tab, m - j, lo_bits));
         }
-        V[i] = split_inv(A, B, tw_split_at(tab, k, lo_bits));
     }
 }
 
-static unsigned grid_for(long long total) {
-    long long b = (total + 255) / 256;
-    return (unsigned)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
+static dim3 split_grid(long long M, long long batch) {
+    const long long bx = (M / 2 + 1 + 255) / 256;
+    return dim3((unsigned)bx, (unsigned)(batch < 65535 ? (batch < 1 ? 1 : batch) : 65535));
 }
 
 hipError_t launch_real_split_fwd(const float2* Z, float2* X, long long M, long long batch, hipStream_t s) {
     int lo_bits = 0;
     const float2* tab = twiddle_split(2 * M, &lo_bits);
     if (!tab) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL(k_real_split_fwd, dim3(grid_for((M + 1) * batch)), dim3(256), 0, s, Z, X, M, batch, tab,
-                       lo_bits);
+    hipLaunchKernelGGL(k_real_split_fwd, split_grid(M, batch), dim3(256), 0, s, Z, X, M, batch, tab, lo_bits);
     return hipGetLastError();
 }
 
@@ -430,7 +441,7 @@ hipError_t launch_real_split_inv(const float2* X, float2* V, long long M, long l
     int lo_bits = 0;
     const float2* tab = twiddle_split(2 * M, &lo_bits);
     if (!tab) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL(k_real_split_inv, dim3(grid_for(M * batch)), dim3(256), 0, s, X, V, M, batch, tab, lo_bits);
+    hipLaunchKernelGGL(k_real_split_inv, split_grid(M, batch), dim3(256), 0, s, X, V, M, batch, tab, lo_bits);
     return hipGetLastError();
 }
 
