@@ -487,7 +487,7 @@ CASES = {
     **{f"lab60_{e}": (lambda e=e: case_lab(e, nch=1, seconds=60)) for e in (0, 2, 4, 6, 8, 10, 14, 32782, 65550, 98318)},
     **{f"empty{g}": (lambda g=g: case_empty(g)) for g in (703, 2048)},
     **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
-       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026)},
+       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026, 128, 256)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152,
                                                                          2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194,

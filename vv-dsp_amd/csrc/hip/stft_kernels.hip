@@ -690,7 +690,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         rsn = rs + h2 >= rc ? rs + h2 - rc : rs + h2;
         for (int k = rc - h2; k < rc; ++k) {
             const int sl = rsn + k >= rc ? rsn + k - rc : rsn + k;
-            glds16(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
+            if constexpr (EXP & 128) glds16_pol<1>(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
+            else if constexpr (EXP & 256) glds16_pol<2>(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
+            else glds16(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
         }
     };
     auto load_pair = [&](long long cc, long long ff) {
