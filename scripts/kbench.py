@@ -449,6 +449,14 @@ CASES = {
     **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
     **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
     "stft400": lambda: case_stft_n(32, 600, 400, 160),
+    "stftp256half": with_env(lambda: case_stft_n(8, 600, 256, 64, sr=48000), "VVHIP_STFT_HALF", "1"),
+    "stftp4096half": with_env(lambda: case_stft_n(8, 600, 4096, 1024, sr=48000), "VVHIP_STFT_HALF", "1"),
+    "stftp128": lambda: case_stft_n(8, 600, 128, 32, sr=48000),
+    "stftp256": lambda: case_stft_n(8, 600, 256, 64, sr=48000),
+    "stftp512": lambda: case_stft_n(8, 600, 512, 128, sr=48000),
+    "stftp2048": lambda: case_stft_n(8, 600, 2048, 512, sr=48000),
+    "stftp4096": lambda: case_stft_n(8, 600, 4096, 1024, sr=48000),
+    "stftp8192": lambda: case_stft_n(8, 600, 8192, 2048, sr=48000),
     **{f"sqpow{nf}": (lambda nf=nf: case_stft_pow_n(32, 600, nf, nf // 4, sr=48000)) for nf in (400, 480, 960)},
     "sqpow400k16": lambda: case_stft_pow_n(32, 600, 400, 160, sr=16000),
     # speech lengths at 48 kHz (hop = nfft / 4), and VVHIP_MIX_VAR=1 (the conjugate-symmetric row emit)

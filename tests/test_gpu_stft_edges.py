@@ -17,10 +17,10 @@ def _np_frames(x, nfft, hop, w):
     return np.abs(np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(frames)]) * w, axis=1))
 
 
-@pytest.mark.parametrize("nfft,hop", [(1024, 256), (400, 160), (512, 512), (480, 120)])
+@pytest.mark.parametrize("nfft,hop", [(1024, 256), (400, 160), (512, 512), (480, 120), (256, 64), (4096, 1024)])
 def test_stft_short_and_ragged_signals(amd, orc, nfft, hop):
     """against NumPy f64 at the harness tolerance (the primary parity rule,
-    SURVEY 8c note 5); for pow2 nfft also against the oracle (Kiss)"""
+    SURVEY 8c note 5); for pow2 nfft <= 1024 also against the oracle (Kiss)"""
     rng = np.random.default_rng(nfft + hop)
     w = orc.window(1, nfft).astype(np.float64)
     for n in (1, 7, nfft - 1, nfft, nfft + 1, nfft + hop - 1, nfft + hop, 3 * nfft + 5):
@@ -29,7 +29,7 @@ def test_stft_short_and_ragged_signals(amd, orc, nfft, hop):
         ref = _np_frames(x, nfft, hop, w)
         assert got.shape == ref.shape == (1 if n < nfft else 1 + (n - nfft + hop) // hop, nfft)
         np.testing.assert_allclose(got, ref, rtol=5e-5, atol=5e-5)
-        if nfft & (nfft - 1) == 0:
+        if nfft & (nfft - 1) == 0 and nfft <= 1024:   # Kiss itself misses the tolerance above 1024
             np.testing.assert_allclose(got, orc.spectrogram(x, nfft, hop), rtol=1e-4, atol=1e-4)
 
 
@@ -66,3 +66,35 @@ def test_stft_device_short_signal_writes_every_bin(vdev, orc, nfft, hop, n):
     w = orc.window(1, nfft).astype(np.float64)
     for c in range(3):
         np.testing.assert_allclose(got[c], _np_frames(sig[c].cpu().numpy(), nfft, hop, w), rtol=5e-5, atol=5e-5)
+
+
+@pytest.mark.parametrize("nfft,hop", [(256, 64), (256, 100), (4096, 1024), (4096, 441)])
+def test_stft_mirror_through_lds_all_row_kinds(vdev, orc, nfft, hop):
+    """nfft 256 / 4096 (k_stft_pair_lds: the mirror bins read back through LDS):
+    magnitude, complex and power rows of a multi-channel ragged job against
+    NumPy f64 at the harness tolerance, and against the one-frame-per-half-FFT
+    kernel they replace (VVHIP_STFT_HALF=1)."""
+    import os
+    import torch
+    n = 5 * nfft + 3 * hop + 17
+    g = torch.Generator(device="cuda").manual_seed(nfft + hop)
+    sig = torch.rand(3, n, device="cuda", generator=g) * 2 - 1
+    st = vdev.Stft(nfft, hop)
+    mag = st.spectrogram(sig).cpu().numpy()
+    cpx = st.spectrogram(sig, complex_out=True).cpu().numpy()
+    pw = st.power(sig).cpu().numpy()
+    w = orc.window(1, nfft).astype(np.float64)
+    for c in range(3):
+        x = sig[c].cpu().numpy()
+        fr = st.frames(n)
+        pad = np.concatenate([x.astype(np.float64), np.zeros(fr * hop + nfft)])
+        X = np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1)
+        np.testing.assert_allclose(mag[c], np.abs(X), rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))
+        np.testing.assert_allclose(cpx[c], X, rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))
+        np.testing.assert_allclose(pw[c], np.abs(X[:, :nfft // 2 + 1]) ** 2, rtol=1e-4, atol=1e-4 * nfft)
+    os.environ["VVHIP_STFT_HALF"] = "1"
+    try:
+        old = st.spectrogram(sig).cpu().numpy()
+    finally:
+        os.environ["VVHIP_STFT_HALF"] = ""
+    np.testing.assert_allclose(mag, old, rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))

@@ -953,6 +953,91 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     }
 }
 
+// Frame pairs for the lengths whose last FFT pass cannot be mirror-paired in
+// registers (N = 256 = 16 x 16, 4096 = 16^3: one last-pass butterfly per
+// thread): two windowed real frames per complex FFT as k_stft_pair, then the
+// spectrum goes through the (idle) LDS exchange buffer in natural order, and
+// each thread reads Z[k], Z[N-k] for bins k = t + T j -- so both rows leave
+// as lane-contiguous, full-line stores.  Persistent XCD walk with the next
+// pair's samples loaded into registers while this pair is transformed.
+template <int N, int MODE>
+__global__ void __launch_bounds__(Wg<N>::value)
+k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
+                long long hop, const float* win, void* out, long long out_ch_stride, const float2* gpass,
+                const float2* gtab) {
+    using G = Geo<N>;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+    __shared__ float2 lds[F * G::LDS];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + slot * G::LDS;
+    float w[G::P];   // 0.5 w: Xa = Z[k] + conj Z[N-k] needs no further scaling (pair_post)
+#pragma unroll
+    for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * G::T];
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    constexpr long long ES = MODE == 1 ? 8 : 4;
+    constexpr long long ROW = MODE == 2 ? N / 2 + 1 : N;
+    const long long ppc = (frames + 1) / 2, pairs = nch * ppc;
+    long long p, p_end, p_step;
+    xcd_walk(pairs, F, slot, &p, &p_end, &p_step);
+    p = uni<G::T>(p);
+    p_end = uni<G::T>(p_end);
+    p_step = uni<G::T>(p_step);
+    float xa[G::P], xb[G::P];
+    auto load = [&](long long q) {
+        const long long c = q / ppc, fa = 2 * (q - c * ppc);
+        const float* s = sig + c * ch_stride;
+        const long long sa = fa * hop, sb = sa + hop;
+        const bool hb = fa + 1 < frames;
+        if (sb + N <= n) {   // both frames inside the signal
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = s[sa + t + r * G::T];
+                xb[r] = s[sb + t + r * G::T];
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const long long i = t + r * G::T;
+                xa[r] = sa + i < n ? s[sa + i] : 0.0f;
+                xb[r] = hb && sb + i < n ? s[sb + i] : 0.0f;
+            }
+        }
+    };
+    if (p < p_end) load(p);
+    for (; p < p_end; p += p_step) {
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
+        const long long c = p / ppc, fa = 2 * (p - c * ppc);
+        const bool hb = fa + 1 < frames;
+        if (p + p_step < p_end) load(p + p_step);   // in flight across this pair's FFT and stores
+        fft_regs<N, true>(v, t, my, tw);
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<N>(t, q))] = v[q];
+        xsync<G::T>();
+        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
+        char* rowb = rowa + ROW * ES;
+#pragma unroll
+        for (int j = 0; j < G::P; ++j) {
+            const int k = t + G::T * j;
+            if (MODE == 2 && k > N / 2) continue;
+            float2 A, B;
+            pair_post<MODE>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
+            if constexpr (MODE == 1) {
+                st_nt(A, reinterpret_cast<float2*>(rowa) + k);
+                if (hb) st_nt(B, reinterpret_cast<float2*>(rowb) + k);
+            } else {
+                __builtin_nontemporal_store(A.x, reinterpret_cast<float*>(rowa) + k);
+                if (hb) __builtin_nontemporal_store(B.x, reinterpret_cast<float*>(rowb) + k);
+            }
+        }
+        xsync<G::T>();   // the next pair's FFT exchange reuses `my`
+    }
+}
+
 template <int M, int MODE>
 __global__ void __launch_bounds__(Wg<M>::value)
 k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
@@ -1195,6 +1280,20 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             }
             if (tpc > 0) launch(k_stft_pair<N, MODE, 2>, 2, mpc, tpc);
         }
+    } else if (!(getenv("VVHIP_STFT_HALF") && *getenv("VVHIP_STFT_HALF") == '1')) {
+        // frame pairs with the mirror read through LDS (VVHIP_STFT_HALF = 1: the
+        // one-frame-per-half-length-FFT kernel below, A/B)
+        const float2* tN = twiddle_table(N);
+        const float2* pN = pass_twiddles(N);
+        if (!tN || !pN) return hipErrorOutOfMemory;
+        constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+        static std::atomic<int> capl;
+        const int cap = cached_grid(capl, (const void*)k_stft_pair_lds<N, MODE>, WG, 0, 1LL << 40);
+        const long long need = (nch * ((frames + 1) / 2) + F - 1) / F;
+        const int grid = (int)(need < cap ? need : cap);
+        if (grid < 1) return hipSuccess;
+        hipLaunchKernelGGL((k_stft_pair_lds<N, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
+                           hop, win, out, out_ch_stride, pN, tN);
     } else {
         constexpr int M = N / 2;
         const float2* tM = twiddle_table(M);
