@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """bench.py -- MI355X benchmark of the vv-dsp spectral hot path.
 
-Headline (BASELINE.json metric): STFT frames/sec, 1024-pt Hann, hop 256.
-Workload per GPU (weak scaling): config 5's per-GPU shard -- 32 channels x
-10 min @ 48 kHz (28,800,000 samples, 112,498 frames each; 256 channels at 8
-GPUs = config 5), magnitude spectrogram [ch][frame][1024] f32, computed by the
-fused gfx950 STFT kernel (one launch per step).  Inputs are synthetic
-(uniform[-1,1), seed = global channel id), generated on the device and resident
-in HBM before timing.  Channels are independent: ranks process disjoint
-channel shards with no collective in the timed region.
+Headline (BASELINE.json metric): STFT frames/sec, 1024-pt Hann, hop 256, on
+config 5 itself -- 256 channels x 10 min @ 48 kHz (28,800,000 samples, 112,498
+frames each; 28,799,488 frames, 29.5 GB in + 118 GB out), magnitude spectrogram
+[ch][frame][1024] f32 (src/spectral/stft.c:112-144), computed by the fused gfx950
+STFT kernel (one launch per step and rank).  Strong scaling: the 256 channels
+are split over the N ranks (channel_shard: contiguous ranges, 32 per rank at
+N = 8), so at N = 1 the whole job runs on one GPU (147 GB of its 288 GB HBM).
+Inputs are synthetic (uniform[-1,1), seed = global channel id), generated on
+the device and resident in HBM before timing.  Channels are independent: ranks
+process disjoint channel shards with no collective in the timed region.
 
 Also measured (same JSON line): the roofline of the dominant kernel (HIP events
 on the launch stream), config 2 (65536 x 1024 c2c f32 FFT) and config 4 (FIR
@@ -41,7 +43,8 @@ import vvdsp_dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 NFFT, HOP = 1024, 256
 FS = 48000
-CH_PER_GPU = 32
+CH_TOTAL = 256               # config 5: the whole job, split over the ranks
+CH_SHARD = 32                # config 5 per-GPU shard at 8 GPUs (extra leg at N = 1)
 SAMPLES = 10 * 60 * FS        # 10 min per channel
 PUBLISHED_CPU_FPS = 24903.0   # BASELINE.md §1 STFT_size_1024 (CPU, 1 thread) -- informational only:
                               # BASELINE.json "published" is empty, so vs_baseline is null
@@ -197,17 +200,35 @@ def _threaded(threads, seconds, work):
     return done, time.perf_counter() - t0
 
 
-def cpu_baseline(threads=None, seconds=15.0):
+def _repeats(threads, seconds, work, reps):
+    """`reps` back-to-back samples of _threaded; each sample's rate (units/s)."""
+    rates, units, secs = [], 0, 0.0
+    for _ in range(reps):
+        n, dt = _threaded(threads, seconds, work)
+        rates.append(n / dt)
+        units += n
+        secs += dt
+    return rates, units, secs
+
+
+def _spread(rates):
+    med = float(np.median(rates))
+    return {"value": round(med, 1), "repeats": [round(r, 1) for r in rates],
+            "spread_pct": round(100.0 * (max(rates) - min(rates)) / med, 2) if med > 0 else None}
+
+
+def cpu_baseline(threads=None, seconds=5.0, reps=3):
     """The reference's own code (oracle/_ref = the reference sources compiled in
     the build container, KissFFT backend) on this host's CPU share, on bounded
-    samples of three BASELINE workloads:
+    samples of three BASELINE workloads, each timed as `reps` back-to-back
+    samples (value = the median, spread = (max - min) / median):
       * headline: vv_dsp_stft_spectrogram of 60 s mono (stft.c:112-144) back to
-        back on every thread (frames/s; the bench line's cpu_baseline value);
+        back on every thread, 3 x 5 s (frames/s; the bench line's cpu_baseline value);
       * config 2: 1024-pt C2C transforms through vv_dsp_fft_execute
-        (fft_kiss.c:27-74), whole 65,536-transform batches per thread;
-      * config 4: vv_dsp_fir_apply direct form (fir.c:160-196), 257 taps, one
-        2^22-sample quarter channel per thread (the reference's fir_apply_fft
-        is O(n^2) there)."""
+        (fft_kiss.c:27-74), 4096-transform chunks of a 65,536 x 1024 batch, 3 x 3 s;
+      * config 4: vv_dsp_fir_apply direct form (fir.c:160-196), 257 taps, 2^22-
+        sample quarter channels (fresh state each) back to back, 3 x 2 s (the
+        reference's fir_apply_fft is O(n^2) there)."""
     from vvapi import VvDsp, FirState
     path = os.path.join(ROOT, "oracle", "_ref", "libvvref.so")
     bpath = os.path.join(ROOT, "oracle", "_ref", "librefbench.so")
@@ -225,18 +246,18 @@ def cpu_baseline(threads=None, seconds=15.0):
         done = 0
         while time.perf_counter() < t_end:
             ref.spectrogram(sigs[i], NFFT, HOP)
-            done += 1
+            done += frames_of(n)
         return done
 
-    runs, dt = _threaded(threads, seconds, stft_work)
-    frames = runs * frames_of(n)
+    rates, frames, dt = _repeats(threads, seconds, stft_work, reps)
     t1 = time.perf_counter()
     ref.spectrogram(sigs[0], NFFT, HOP)
     d1 = time.perf_counter() - t1
     del sigs
-    res = {"value": round(frames / dt, 1), "unit": "frames/s", "cores": threads, "kind": "reference",
+    res = {**_spread(rates), "unit": "frames/s", "cores": threads, "kind": "reference",
            "sample": f"{threads} threads x vv_dsp_stft_spectrogram(60 s @ 48 kHz mono, 1024 Hann, hop 256) "
-                     f"back to back for {seconds:.0f} s: {runs} runs = {frames} frames in {dt:.2f} s",
+                     f"back to back, {reps} samples of {seconds:.0f} s: {frames} frames in {dt:.2f} s; "
+                     f"value = median of the samples",
            "single_thread_frames_per_s": round(frames_of(n) / d1, 1),
            "cpu_model": model, "host_cpus": ncpu, "thread_caps": cands}
 
@@ -256,12 +277,13 @@ def cpu_baseline(threads=None, seconds=15.0):
                 done += chunk
             return done
 
-        cnt, dt2 = _threaded(threads, 5.0, fft_work)
+        rates2, cnt, dt2 = _repeats(threads, 3.0, fft_work, reps)
+        sp = _spread(rates2)
         res["config2_fft_c2c_1024"] = {
-            "value": round(cnt / dt2, 1), "unit": "transforms/s", "cores": threads,
-            "batch_65536_s": round(B / (cnt / dt2), 4),
+            **sp, "unit": "transforms/s", "cores": threads,
+            "batch_65536_s": round(B / sp["value"], 4),
             "sample": f"{threads} threads x vv_dsp_fft_execute (Kiss radix-2, one plan per thread) over rows of a "
-                      f"65536 x 1024 uniform[-0.5,0.5) batch for 5 s: {cnt} transforms in {dt2:.2f} s"}
+                      f"65536 x 1024 uniform[-0.5,0.5) batch, {reps} samples of 3 s: {cnt} transforms in {dt2:.2f} s"}
         del x, ys
 
     h = np.zeros(257, np.float32)          # config 4
@@ -271,21 +293,25 @@ def cpu_baseline(threads=None, seconds=15.0):
     ys = [np.empty(ns, np.float32) for _ in range(threads)]
 
     def fir_work(i, t_end):
-        st = FirState()
-        assert ref.lib.vv_dsp_fir_state_init(C.byref(st), 257) == 0
+        done = 0
         fp = C.POINTER(C.c_float)
-        r = ref.lib.vv_dsp_fir_apply(C.byref(st), h.ctypes.data_as(fp), xs[i].ctypes.data_as(fp),
-                                     ys[i].ctypes.data_as(fp), ns)
-        ref.lib.vv_dsp_fir_state_free(C.byref(st))
-        assert r == 0
-        return ns
+        while time.perf_counter() < t_end:
+            st = FirState()
+            assert ref.lib.vv_dsp_fir_state_init(C.byref(st), 257) == 0
+            r = ref.lib.vv_dsp_fir_apply(C.byref(st), h.ctypes.data_as(fp), xs[i].ctypes.data_as(fp),
+                                         ys[i].ctypes.data_as(fp), ns)
+            ref.lib.vv_dsp_fir_state_free(C.byref(st))
+            assert r == 0
+            done += ns
+        return done
 
-    cnt, dt4 = _threaded(threads, 0.0, fir_work)
+    rates4, cnt, dt4 = _repeats(threads, 2.0, fir_work, reps)
+    sp = _spread(rates4)
     res["config4_fir_direct_257"] = {
-        "value": round(cnt / dt4, 1), "unit": "samples/s", "cores": threads,
-        "config4_s": round(8 * (1 << 24) / (cnt / dt4), 3),
-        "sample": f"{threads} threads x vv_dsp_fir_apply (direct form, fresh state) on 2^22 uniform[-1,1) "
-                  f"samples each: {cnt} samples in {dt4:.2f} s"}
+        **sp, "unit": "samples/s", "cores": threads,
+        "config4_s": round(8 * (1 << 24) / sp["value"], 3),
+        "sample": f"{threads} threads x vv_dsp_fir_apply (direct form, fresh state per 2^22-sample block) on "
+                  f"uniform[-1,1) samples, {reps} samples of >= 2 s: {cnt} samples in {dt4:.2f} s"}
     return res
 
 
@@ -361,11 +387,10 @@ def gather_leg(out, total_ch, compute_s, frames_per_step, rank, half=True):
         return {"error": repr(e)[:300]}
 
 
-def full_job_leg(steps=3):
-    """Config 5's whole job -- 256 ch x 10 min @ 48 kHz, 147.5 GB in + out --
-    on ONE GPU (it fits the 288 GB of HBM): the strong-scaling anchor for the
-    driver's 1/2/4/8-GPU runs.  Same kernel and output layout as the headline."""
-    ch = 256
+def shard_leg(ch=CH_SHARD, steps=20, warm=10):
+    """Config 5's per-GPU shard at 8 GPUs -- 32 ch x 10 min @ 48 kHz, 18.4 GB in
+    + out -- on one GPU: what each rank of the driver's N = 8 run computes.  Same
+    kernel, walk and output layout as the headline."""
     nfr = frames_of(SAMPLES)
     try:
         sig = torch.empty(ch, SAMPLES, device="cuda")
@@ -376,29 +401,25 @@ def full_job_leg(steps=3):
     except torch.OutOfMemoryError as e:
         return {"error": repr(e)[:200]}
     st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
-    st.spectrogram(sig, out=out)
-    torch.cuda.synchronize()
-    s = torch.cuda.current_stream()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(s)
-    for _ in range(steps):
-        st.spectrogram(sig, out=out)
-    b.record(s)
-    torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / steps
+    avg, best = timed_launches(lambda: st.spectrogram(sig, out=out), steps, warm=warm)
     fr = 12345
-    x0 = sig[255, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
-    w = np.array([0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(NFFT - 1) * np.float32(i))
-                  for i in range(NFFT)], np.float64)
-    ok = np.allclose(out[255, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * w)), rtol=5e-5, atol=5e-5)
+    x0 = sig[ch - 1, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
+    ok = np.allclose(out[ch - 1, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * hann64())), rtol=5e-5, atol=5e-5)
     byts = ch * SAMPLES * 4 + ch * nfr * NFFT * 4 + NFFT * 4
     del sig, out, st
     torch.cuda.empty_cache()
-    return {"workload": "config5 whole job on one GPU: 256 ch x 10 min @ 48 kHz, 1024 Hann, hop 256 "
-                        "(28,799,488 frames; 29.5 GB in, 118 GB out)",
-            "steps": steps, "ms_per_step": round(ms, 3), "frames_per_s": round(ch * nfr / (ms * 1e-3), 1),
-            "bytes_per_step": byts, "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+    return {"workload": f"config5 per-GPU shard at 8 GPUs: {ch} ch x 10 min @ 48 kHz, 1024 Hann, hop 256 "
+                        f"({ch * nfr:,} frames; 3.7 GB in, 14.7 GB out)",
+            "steps": steps, "ms_avg": round(avg, 4), "ms_min": round(best, 4),
+            "frames_per_s": round(ch * nfr / (avg * 1e-3), 1),
+            "bytes_per_launch": byts, "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "check_row_vs_numpy_f64": bool(ok)}
+
+
+def hann64():
+    """The reference's symmetric Hann (window.c:25-36, float arithmetic) in f64."""
+    return np.array([0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(NFFT - 1) * np.float32(i))
+                     for i in range(NFFT)], np.float64)
 
 
 def main():
@@ -406,14 +427,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=25)
-    ap.add_argument("--channels", type=int, default=CH_PER_GPU, help="channels per GPU")
-    ap.add_argument("--no-extras", action="store_true", help="skip config 2/3/4 and CPU baseline legs")
+    ap.add_argument("--channels", type=int, default=CH_TOTAL,
+                    help="channels of the whole job (config 5: 256), split over the ranks (strong scaling)")
+    ap.add_argument("--no-extras", action="store_true", help="skip config 2/3/4, shard and CPU baseline legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
-    ap.add_argument("--legs", default="c2c,fir,config3",
-                    help="extra GPU legs: c2c (config 2), fir (config 4), config3 (profiling runs leave config3 "
-                         "out so the headline kernel's PMC average covers the headline launches only)")
-    ap.add_argument("--full-job", choices=["auto", "on", "off"], default="auto",
-                    help="config 5's whole 256-channel job on one GPU as an extra leg (auto: on at N = 1 with extras)")
+    ap.add_argument("--legs", default="c2c,fir,config3,shard",
+                    help="extra GPU legs: c2c (config 2), fir (config 4), config3, shard (config 5's 32-channel "
+                         "per-GPU shard of the N = 8 run); profiling runs leave config3 and shard out so the "
+                         "headline kernel's PMC average covers the headline launches only")
     ap.add_argument("--gather-bins", choices=["half", "full"], default="half",
                     help="gather bins 0..512 and expand on rank 0 (half, default) or all 1024 bins (full)")
     ap.add_argument("--gather", choices=["auto", "on", "off"], default="auto",
@@ -430,12 +451,14 @@ def main():
     if vv.device_count() <= 0:
         raise SystemExit("libvvdsp_amd.so sees no HIP device")
 
-    # ---- per-rank shard: channels [rank*C, rank*C + C) of the job ----
-    C_ = args.channels
+    # ---- this rank's shard of the job: channels [lo, hi) (contiguous, sizes differ by <= 1) ----
+    total_ch = args.channels
+    lo, hi = vvdsp_dist.channel_shard(total_ch, world, rank)
+    C_ = hi - lo
     nfr = frames_of(SAMPLES)
     sig = torch.empty(C_, SAMPLES, device="cuda")
     for c in range(C_):
-        g = torch.Generator(device="cuda").manual_seed(rank * C_ + c)
+        g = torch.Generator(device="cuda").manual_seed(lo + c)
         sig[c].uniform_(-1.0, 1.0, generator=g)
     out = torch.empty(C_, nfr, NFFT, device="cuda")
     st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
@@ -467,22 +490,23 @@ def main():
     elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    frames_total = world * C_ * nfr * args.steps
+    frames_total = total_ch * nfr * args.steps      # every rank's frames
     value = frames_total / elapsed
     bytes_per_launch = C_ * SAMPLES * 4 + C_ * nfr * NFFT * 4 + NFFT * 4
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
     traffic, traffic_src = hbm_traffic(C_)
 
-    # spot-check one frame row against NumPy f64 so a fast-but-wrong kernel cannot report
+    # spot-check one frame row of the first and last channel against NumPy f64
+    # so a fast-but-wrong kernel cannot report
     fr = 12345
-    x0 = sig[0, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
-    w = np.array([0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(NFFT - 1) * np.float32(i))
-                  for i in range(NFFT)], np.float64)
-    ok = np.allclose(out[0, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * w)), rtol=5e-5, atol=5e-5)
+    ok = True
+    for c in (0, C_ - 1):
+        x0 = sig[c, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
+        ok = ok and np.allclose(out[c, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * hann64())), rtol=5e-5, atol=5e-5)
     gather = None
     if world > 1 and (args.gather == "on" or args.gather == "auto"):
-        gather = gather_leg(out, C_ * world, elapsed / args.steps, frames_total / args.steps, rank,
+        gather = gather_leg(out, total_ch, elapsed / args.steps, frames_total / args.steps, rank,
                             half=args.gather_bins == "half")
     del sig, out, st
     torch.cuda.empty_cache()
@@ -496,7 +520,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "published_cpu_reference": {"value": PUBLISHED_CPU_FPS, "unit": "frames/s",
                                     "what": "BASELINE.md §1 STFT_size_1024, Ryzen 9 7950X, 1 thread, KissFFT "
@@ -504,16 +528,18 @@ def main():
         "dtype": "f32",
         "data": "synthetic: uniform[-1,1) per channel, seed = global channel id, generated in HBM",
         "config": {
-            "workload": f"config5 per-GPU shard: multi-channel STFT magnitude, {C_} ch x 10 min @ 48 kHz "
-                        f"per GPU ({C_ * world} ch total; 256 ch = config 5 at 8 GPUs), nfft 1024 Hann, hop 256",
-            "channels_per_gpu": C_, "samples_per_channel": SAMPLES, "frames_per_channel": nfr,
+            "workload": f"config5: multi-channel STFT magnitude, {total_ch} ch x 10 min @ 48 kHz "
+                        f"({total_ch * nfr:,} frames per step), nfft 1024 Hann, hop 256; strong scaling: "
+                        f"{C_} ch on this rank" + (" (the whole job on one GPU)" if world == 1 else ""),
+            "channels_total": total_ch, "channels_per_gpu": C_, "samples_per_channel": SAMPLES,
+            "frames_per_channel": nfr, "frames_per_step": total_ch * nfr,
             "nfft": NFFT, "hop": HOP, "window": "hann (symmetric, window.c:25-36)",
             "output": "[ch][frame][1024] f32 magnitudes (stft.c:133-139)",
             "parallelism": f"dp{world} (channel shards, no data-path collective)"},
         "roofline": {"kernel": "vvh::k_stft_pair<1024,0,5> (persistent dynamic band walk in runs of 2 pairs; LDS-DMA frame spans kept as a ring of 256-float chunks + "
                                "Hann + two frames per 1024-pt complex FFT + |X| rows as full-line streaming stores; "
                                "the zero-padded tail pairs run in the same launch); kernel_ms = HIP events around "
-                               "the launch on the launch stream",
+                               f"each of the {args.steps} timed launches on the launch stream ({C_} channels per launch)",
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
@@ -524,6 +550,9 @@ def main():
         res["with_gather"] = gather
     legs = set(args.legs.split(","))
     if rank == 0 and not args.no_extras and world == 1:
+        if "shard" in legs:
+            res["config5_shard_32ch"] = shard_leg()
+            torch.cuda.empty_cache()
         if "c2c" in legs:
             res["fft_c2c_1024"] = fft_c2c_roofline()
             torch.cuda.empty_cache()
@@ -533,9 +562,6 @@ def main():
         if "config3" in legs:
             res["stft_config3"] = stft_config3()
             torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and (args.full_job == "on" or (args.full_job == "auto" and not args.no_extras)):
-        res["config5_full_job_1gpu"] = full_job_leg()
-        torch.cuda.empty_cache()
     if rank == 0 and not args.no_extras and not args.no_cpu and world == 1:
         res["cpu_baseline"] = cpu_baseline()
     if rank == 0:

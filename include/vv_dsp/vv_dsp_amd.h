@@ -62,11 +62,14 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_frames_range_device(vv_dsp_stft* h, c
                                                                size_t n, size_t nch, size_t ch_stride,
                                                                size_t frame0, size_t nframes, void* d_out,
                                                                size_t out_ch_stride, int out_kind, void* stream);
+/* the handle's fft_size and hop_size (either pointer may be NULL) */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_get_sizes(const vv_dsp_stft* h, size_t* fft_size, size_t* hop_size);
 /* ---- Multi-GPU layout of config 5: channels shard with no
  * exchange; the only collective is the caller's gather of the rows. ----
  * The contiguous block split rank `rank` of `world` owns: channels
  * [*first, *first + *count), rank order = channel order, sizes differ by at most
- * one (the same split as vv-dsp_amd/vvdsp_dist.py channel_shard). */
+ * one (the same split as vv-dsp_amd/vvdsp_dist.py channel_shard).  The RCCL
+ * shard + gather entry points are in vv_dsp/vv_dsp_dist.h. */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_shard_range(size_t total, size_t world, size_t rank, size_t* first,
                                                   size_t* count);
 /* One rank's share of a multi-channel spectrogram on `device`: the rows of
@@ -156,9 +159,13 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_log_mel_device(const vv_dsp_mfcc_plan* pla
  * apart.  The values are those of vv_dsp_stft_power_device followed by
  * vv_dsp_log_mel_device / vv_dsp_mfcc_process_device (the stft's window,
  * nfft and hop; the plan's filterbank, log epsilon, DCT and lifter), bit for
- * bit: for nfft = 1024 one kernel computes them with the power rows kept in
- * LDS, otherwise the two steps run through a scratch buffer.  The plan's
- * n_fft must equal the stft's nfft (VV_DSP_ERROR_INVALID_SIZE). */
+ * bit.  One kernel computes them with the power rows kept in LDS when
+ * nfft = 1024, hop <= 256 and a multiple of 4, the signal 16-B aligned with
+ * ch_stride a multiple of 4, n_mels <= 128 (log-mel) or n_mels <= 60 and
+ * num_mfcc_coeffs <= 64 (MFCC: the log-mel rows stay in the exchange buffer's
+ * spare tail); any other shape runs the two steps through a scratch buffer
+ * (vvhip_debug_get("STAT_MEL_FUSED") / ("STAT_MEL_SPLIT") count which ran).
+ * The plan's n_fft must equal the stft's nfft (VV_DSP_ERROR_INVALID_SIZE). */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_log_mel_device(vv_dsp_stft* h, const vv_dsp_mfcc_plan* plan,
                                                           const vv_dsp_real* d_signal, size_t n, size_t nch,
                                                           size_t ch_stride, vv_dsp_real* d_out, size_t out_ch_stride,

@@ -48,6 +48,21 @@ typedef struct vvhip_czt vvhip_czt;
 int vvhip_available(void);
 /* Text of the last error seen by this thread ("" if none). */
 const char* vvhip_last_error(void);
+
+/* A/B switches and path counters (csrc/hip/debug.hip), for tests and the
+ * scripts/kbench.py timing harness; the defaults are the adopted kernels.
+ *   vvhip_debug_set("STFT_DYN", 0)  selects a launcher alternative (the names
+ *       are the VVHIP_* switches of DESIGN.md, with or without the prefix);
+ *       0 on success, -1 for an unknown name or a negative value;
+ *   vvhip_debug_clear(name)  back to the default (NULL: every knob, and every
+ *       path counter to 0);
+ *   vvhip_debug_get(name)  a knob's value (-1 unset) or a path counter
+ *       ("STAT_STFT_DYN", "STAT_FIR_DYN", "STAT_FIR_STATIC", "STAT_MEL_FUSED",
+ *       "STAT_MEL_SPLIT": launches of that path since the last clear); -2 unknown.
+ * The environment is read once per process, and only with VVHIP_AB=1 set. */
+int vvhip_debug_set(const char* name, long long value);
+int vvhip_debug_clear(const char* name);
+long long vvhip_debug_get(const char* name);
 /* Build identification, e.g. "vvhip gfx950 ROCm 7.2". */
 const char* vvhip_version(void);
 
@@ -57,6 +72,13 @@ void vvhip_free(void* p);
 int vvhip_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int vvhip_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int vvhip_memset(void* dst, int value, size_t bytes);
+/* stream-ordered scratch on the stream's device (hipMallocAsync / hipFreeAsync)
+ * and a device-to-device copy on a stream */
+int vvhip_malloc_async(void** p, size_t bytes, void* stream);
+int vvhip_free_async(void* p, void* stream);
+int vvhip_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream);
+/* sets the text vvhip_last_error() returns on this thread (host front-end errors) */
+void vvhip_set_error(const char* what);
 int vvhip_stream_sync(void* stream);
 int vvhip_device_sync(void);
 /* the calling thread's current HIP device (hipSetDevice / hipGetDevice) */

@@ -383,15 +383,17 @@ def case_model(depth, work, lds_bytes, walk=0, ld=0, pairs=1799968):
 
 
 def with_env(case, key, val):
-    """run a case with an environment switch the launcher reads at each call"""
+    """run a case with a launcher knob (csrc/hip/debug.hip, vvhip_debug_set) set
+    around each call; `key` is the knob's VVHIP_* name"""
     def make():
         inner = case()
         fn = inner[0]
+        name = key[6:] if key.startswith("VVHIP_") else key
 
         def run():
-            os.environ[key] = val
+            vv.debug_set(name, int(val))
             fn()
-            os.environ[key] = ""
+            vv.debug_clear(name)
         return (run,) + tuple(inner[1:])
     return make
 
@@ -464,9 +466,6 @@ CASES = {
        for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960)},
     **{f"sq{nf}v{v}": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_MIX_VAR", str(v))
        for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960) for v in (1, 3, 4, 5, 6)},
-    **{f"sq{nf}lb4": with_env(lambda nf=nf: case_stft_n(32, 600, nf, nf // 4, sr=48000), "VVHIP_SQ_LB4", "1")
-       for nf in (320, 480)},
-    **{f"mix{n}lb4": with_env(lambda n=n: case_c2c(n, (1 << 26) // n), "VVHIP_SQ_LB4", "1") for n in (320, 480)},
     **{f"r2cmix{n}": (lambda n=n: case_r2c(n, (1 << 27) // n)) for n in (400, 960, 1000)},
     **{f"r2cmix{n}gen": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_STFT_SQ", "0") for n in (400, 960)},
     **{f"r2cmix{n}full": with_env(lambda n=n: case_r2c(n, (1 << 27) // n), "VVHIP_MIX_R2C_FULL", "1") for n in (400, 1000)},

@@ -87,3 +87,23 @@ def vdev(amd_lib_path):
     if not torch.cuda.is_available() or vvdsp_amd.device_count() <= 0:
         pytest.fail("GPU tests need an MI355X")
     return vvdsp_amd
+
+
+@pytest.fixture
+def knob():
+    """knob("STFT_DYN", 0): select a launcher alternative of the product library
+    (vvhip_debug_set, csrc/hip/debug.hip) for this test; every knob the test set
+    is cleared at teardown.  "" / None clears at once."""
+    import vvdsp_amd as vv
+    touched = []
+
+    def setter(name, value):
+        name = name[6:] if name.startswith("VVHIP_") else name
+        if value in ("", None):
+            vv.debug_clear(name)
+        else:
+            vv.debug_set(name, int(value))
+            touched.append(name)
+    yield setter
+    for n in touched:
+        vv.debug_clear(n)

@@ -192,9 +192,9 @@ def test_cepstrum_batched_device(vdev, amd):
 
 
 @pytest.mark.parametrize("n,m", [(8, 8), (100, 64), (257, 300), (1000, 17), (1500, 2000), (2049, 2048), (1, 1)])
-def test_czt_fused_equals_unfused(vdev, monkeypatch, n, m):
+def test_czt_fused_equals_unfused(vdev, knob, n, m):
     """P = next_pow2(N + M - 1) <= 4096 runs the one-pass kernel (k_czt_fused);
-    VVHIP_CZT_UNFUSED=1 the chain of element-wise kernels and library FFTs.  The
+    knob CZT_UNFUSED=1 the chain of element-wise kernels and library FFTs.  The
     arithmetic is the same (the 1/P of the inverse folded into B is a power of
     two), so the rows must be bit-identical, complex and real input."""
     import torch
@@ -202,18 +202,18 @@ def test_czt_fused_equals_unfused(vdev, monkeypatch, n, m):
     plan = vdev.CztPlan(n, m, _c64(np.exp(-2j * np.pi * 0.13 / m)), _c64(np.exp(0.2j)))
     xc = torch.complex(torch.randn(41, n, device="cuda", generator=g), torch.randn(41, n, device="cuda", generator=g))
     for x in (xc, xc.real.contiguous()):
-        monkeypatch.setenv("VVHIP_CZT_UNFUSED", "0")
+        knob("CZT_UNFUSED", "0")
         a = plan(x)
-        monkeypatch.setenv("VVHIP_CZT_UNFUSED", "1")
+        knob("CZT_UNFUSED", "1")
         b = plan(x)
         torch.cuda.synchronize()
         assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("n", [2, 16, 256, 1024, 4096])
-def test_cepstrum_fused_vs_chain(vdev, monkeypatch, n):
+def test_cepstrum_fused_vs_chain(vdev, knob, n):
     """Power-of-two n <= 4096 runs the one-pass kernels (k_ceps_fused);
-    VVHIP_CEPS_UNFUSED=1 the element-wise chains around the library FFTs (the
+    knob CEPS_UNFUSED=1 the element-wise chains around the library FFTs (the
     chain's cepstrum goes through R2C/C2R instead of the reference's C2C pair).
     Both are f32 computations of the same definitions: normwise within 2e-6 (the
     one-pass kernel is compiled separately, so its FMA contractions may differ)."""
@@ -221,9 +221,9 @@ def test_cepstrum_fused_vs_chain(vdev, monkeypatch, n):
     g = torch.Generator(device="cuda").manual_seed(n)
     x = torch.randn(23, n, device="cuda", generator=g)
     c = (0.1 * torch.randn(23, n, device="cuda", generator=g)).contiguous()
-    monkeypatch.setenv("VVHIP_CEPS_UNFUSED", "0")
+    knob("CEPS_UNFUSED", "0")
     a = (vdev.cepstrum(x), vdev.icepstrum_minphase(c), vdev.minphase_from_cepstrum(c))
-    monkeypatch.setenv("VVHIP_CEPS_UNFUSED", "1")
+    knob("CEPS_UNFUSED", "1")
     b = (vdev.cepstrum(x), vdev.icepstrum_minphase(c), vdev.minphase_from_cepstrum(c))
     torch.cuda.synchronize()
     for u, v in zip(a, b):

@@ -1,0 +1,157 @@
+"""The plain-C multi-GPU layer (include/vv_dsp/vv_dsp_dist.h, csrc/host/dist.c)
+on the one GPU of the test box, and the Python gathers (vvdsp_dist.py) on a
+world-1 nccl (= RCCL) process group:
+
+* an RCCL context of one rank (ncclCommInitAll over device 0): the sharded STFT
+  and the gather (full and half-spectrum rows) give the unsharded rows, bit for
+  bit -- RCCL's ncclGroupStart/End path with no peer;
+* loopback contexts of 2 and 3 ranks on device 0 (the same slab / offset /
+  pack-unpack logic with device copies in place of ncclSend/ncclRecv): uneven
+  channel shards (vv_dsp_shard_range), roots 0 and world-1, small slabs;
+* config 2 / config 4 shard helpers (batch shards of an FFT, channel shards of
+  the FIR) against the unsharded calls, bit for bit.
+Reference semantics: stft.c:112-144 (rows), SURVEY.md 8e (shards + gather)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import vvdsp_amd as vv
+
+pytestmark = pytest.mark.gpu
+
+NCH, N = 7, 48000 * 20 + 333     # 7 channels: shards 4/3 (world 2), 3/2/2 (world 3)
+
+
+@pytest.fixture(scope="module")
+def job():
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(5)
+    sig = torch.rand(NCH, N, device="cuda", generator=g) * 2 - 1
+    st = vv.Stft(1024, 256)
+    ref = st.spectrogram(sig).clone()
+    torch.cuda.synchronize()
+    return sig, st, ref
+
+
+def _shards(total, world):
+    return [vv.shard_range(total, world, r) for r in range(world)]
+
+
+def _sharded_rows(d, sig, st, world, kind=0):
+    import torch
+    fr = st.frames(N)
+    width = 1024 if kind != 2 else 513
+    dt = torch.complex64 if kind == 1 else torch.float32
+    sl = _shards(NCH, world)
+    rows = [torch.full((c, fr, width), -3.0, device="cuda").to(dt) for (_, c) in sl]
+    sigs = [sig[f] for (f, _) in sl]
+    assert d.stft(st, sigs, N, NCH, sig.stride(0), rows, out_kind=kind) == fr
+    return rows
+
+
+def test_rccl_one_rank_stft_and_gather(job):
+    import torch
+    sig, st, ref = job
+    d = vv.Dist.all([0])
+    assert d.slots == 1 and d.rank_info(0) == (0, 1, 0)
+    rows = _sharded_rows(d, sig, st, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(rows[0], ref)
+    for half in (False, True):
+        out = torch.full_like(ref, -1.0)
+        d.gather_rows([rows[0]], NCH * ref.shape[1], 1024, out, root=0, half=half)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("world,root", [(2, 0), (3, 0), (3, 2)])
+@pytest.mark.parametrize("half", [False, True])
+def test_loopback_gather_uneven(job, world, root, half):
+    import torch
+    sig, st, ref = job
+    d = vv.Dist.loopback(world)
+    assert d.slots == world
+    rows = _sharded_rows(d, sig, st, world)
+    torch.cuda.synchronize()
+    for (f, c), r in zip(_shards(NCH, world), rows):
+        assert torch.equal(r, ref[f:f + c])
+    out = torch.full_like(ref, -1.0)
+    d.gather_rows(rows, NCH * ref.shape[1], 1024, out, root=root, half=half)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+def test_loopback_power_and_complex_rows(job):
+    import torch
+    sig, st, _ = job
+    d = vv.Dist.loopback(3)
+    for kind, full in ((2, st.power(sig)), (1, st.spectrogram(sig, complex_out=True))):
+        rows = _sharded_rows(d, sig, st, 3, kind)
+        torch.cuda.synchronize()
+        for (f, c), r in zip(_shards(NCH, 3), rows):
+            assert torch.equal(r, full[f:f + c])
+        # power rows gather as plain rows (513 floats)
+        if kind == 2:
+            out = torch.full_like(full, -1.0)
+            d.gather_rows(rows, NCH * full.shape[1], 513, out, root=1)
+            torch.cuda.synchronize()
+            assert torch.equal(out, full)
+
+
+def test_loopback_fft_and_fir_shards():
+    import torch
+    total, n = 1001, 1024
+    g = torch.Generator(device="cuda").manual_seed(8)
+    x = torch.complex(torch.rand(total, n, device="cuda", generator=g) - 0.5,
+                      torch.rand(total, n, device="cuda", generator=g) - 0.5)
+    ref = vv.FftPlan(n, vv.C2C, vv.FWD, batch=total)(x)
+    d = vv.Dist.loopback(3)
+    sl = _shards(total, 3)
+    y = torch.empty_like(x)
+    d.fft(n, vv.C2C, vv.FWD, total, [x[f] for f, _ in sl], [y[f] for f, _ in sl])
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    # config 4's FIR over channel shards
+    h = torch.from_numpy(np.hanning(257).astype(np.float32) / 128.0)
+    xs = torch.rand(5, 3_000_001, device="cuda", generator=g) * 2 - 1
+    plan = vv.FirPlan(h)
+    yref = plan(xs)
+    ys = torch.empty_like(xs)
+    sl = _shards(5, 2)
+    d2 = vv.Dist.loopback(2)
+    d2.fir([plan, plan], xs.shape[1], 5, [xs[f] for f, _ in sl], xs.stride(0), [ys[f] for f, _ in sl], ys.stride(0))
+    torch.cuda.synchronize()
+    assert torch.equal(ys, yref)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_torch_nccl_world1_gathers(job):
+    """vvdsp_dist.gather_rows_half / gather_rows_stream on a world-1 nccl
+    process group (RCCL), i.e. the bench's with_gather path on hardware."""
+    import torch
+    import torch.distributed as dist
+    import vvdsp_dist
+    sig, st, ref = job
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        out = vvdsp_dist.gather_rows_half(ref, NCH, 1024, dst=0)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        host = torch.empty(ref.shape, dtype=ref.dtype).pin_memory()
+        vvdsp_dist.gather_rows_stream(ref, NCH, vvdsp_dist.host_sink(host), dst=0, slab_bytes=3 * ref[0].numel() * 4 // 2)
+        torch.cuda.synchronize()
+        assert torch.equal(host, ref.cpu())
+        full = vvdsp_dist.gather_rows(ref, NCH, dst=0)
+        assert torch.equal(full, ref)
+    finally:
+        dist.destroy_process_group()

@@ -1,15 +1,14 @@
 """The dynamically scheduled STFT walks (k_stft_pair VAR 4 / VAR 5: persistent
 grid, per-(device, stream) work counters that the kernel's last waves reset;
 VAR 5 hands out runs of pairs walked on a ring of span chunks) against the
-chunked launch they replace for large jobs (VVHIP_STFT_DYN=0):
+chunked launch they replace for large jobs (knob STFT_DYN=0):
 bit-identical rows, repeated launches (the counters must come back to zero),
 two streams at once (each its own counter block), the zero-padded tail and a
 missing second frame (odd frame count), and sampled rows against NumPy f64 at
 the harness tolerance (stft.c:112-144, python/test_fft.py:37-38)."""
-import os
-
 import numpy as np
 import pytest
+import vvdsp_amd as vv
 
 pytestmark = pytest.mark.gpu
 
@@ -23,11 +22,11 @@ def job(vdev):
     g = torch.Generator(device="cuda").manual_seed(11)
     sig = torch.rand(NCH, N, device="cuda", generator=g) * 2 - 1
     st = vdev.Stft(1024, 256)
-    os.environ["VVHIP_STFT_DYN"] = "0"
+    vv.debug_set("STFT_DYN", 0)
     try:
         ref = st.spectrogram(sig).clone()
     finally:
-        os.environ["VVHIP_STFT_DYN"] = ""
+        vv.debug_clear("STFT_DYN")
     torch.cuda.synchronize()
     return sig, st, ref
 
@@ -73,33 +72,33 @@ def test_dynamic_walk_rows_vs_numpy(job, orc):
 
 @pytest.mark.parametrize("kind", ["magnitude", "power", "complex"])
 def test_dynamic_walk_other_rows(job, kind):
-    """VVHIP_STFT_DYN=1 forces VAR 4 (one pair per counter value; magnitude rows
+    """knob STFT_DYN=1 forces VAR 4 (one pair per counter value; magnitude rows
     default to VAR 5's runs) and runs power (n/2+1) and complex rows through the
     same walk: rows equal to the chunked launch's, bit for bit."""
     import torch
     sig, st, _ = job
     run = {"magnitude": lambda: st.spectrogram(sig), "power": lambda: st.power(sig),
            "complex": lambda: st.spectrogram(sig, complex_out=True)}[kind]
-    os.environ["VVHIP_STFT_DYN"] = "0"
+    vv.debug_set("STFT_DYN", 0)
     try:
         ref = run().clone()
     finally:
-        os.environ["VVHIP_STFT_DYN"] = ""
-    os.environ["VVHIP_STFT_DYN"] = "1"
+        vv.debug_clear("STFT_DYN")
+    vv.debug_set("STFT_DYN", 1)
     try:
         for _ in range(2):
             got = run()
             torch.cuda.synchronize()
             assert torch.equal(got, ref)
     finally:
-        os.environ["VVHIP_STFT_DYN"] = ""
+        vv.debug_clear("STFT_DYN")
 
 
 @pytest.mark.parametrize("run_len", ["1", "3", "4", "16"])
 @pytest.mark.parametrize("kind", ["magnitude", "power", "complex"])
 def test_dynamic_ring_runs(job, kind, run_len):
-    """VVHIP_STFT_DYN=2 (VAR 5): the dynamic walk handing out runs of
-    VVHIP_STFT_RUN pairs, each walked on a ring of 256-float chunks -- runs that
+    """knob STFT_DYN=2 (VAR 5): the dynamic walk handing out runs of
+    knob STFT_RUN pairs, each walked on a ring of 256-float chunks -- runs that
     cross channel ends, a short last run, repeated launches: rows equal to the
     chunked launch's, bit for bit."""
     import torch
@@ -109,21 +108,21 @@ def test_dynamic_ring_runs(job, kind, run_len):
     if kind == "magnitude":
         ref = ref_mag
     else:
-        os.environ["VVHIP_STFT_DYN"] = "0"
+        vv.debug_set("STFT_DYN", 0)
         try:
             ref = run().clone()
         finally:
-            os.environ["VVHIP_STFT_DYN"] = ""
-    os.environ["VVHIP_STFT_DYN"] = "2"
-    os.environ["VVHIP_STFT_RUN"] = run_len
+            vv.debug_clear("STFT_DYN")
+    vv.debug_set("STFT_DYN", 2)
+    vv.debug_set("STFT_RUN", int(run_len))
     try:
         for _ in range(2):
             got = run()
             torch.cuda.synchronize()
             assert torch.equal(got, ref)
     finally:
-        os.environ["VVHIP_STFT_DYN"] = ""
-        os.environ["VVHIP_STFT_RUN"] = ""
+        vv.debug_clear("STFT_DYN")
+        vv.debug_clear("STFT_RUN")
 
 
 @pytest.mark.parametrize("hop", [128, 512])
@@ -136,12 +135,45 @@ def test_dynamic_walks_other_hops(vdev, hop):
     g = torch.Generator(device="cuda").manual_seed(hop)
     sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
     st = vdev.Stft(1024, hop)
-    os.environ["VVHIP_STFT_DYN"] = "0"
+    vv.debug_set("STFT_DYN", 0)
     try:
         ref = st.spectrogram(sig).clone()
     finally:
-        os.environ["VVHIP_STFT_DYN"] = ""
+        vv.debug_clear("STFT_DYN")
     for _ in range(2):
         got = st.spectrogram(sig)
         torch.cuda.synchronize()
         assert torch.equal(got, ref)
+
+
+def test_dynamic_walks_under_graph_capture(job, vdev, orc):
+    """A large STFT and a config-4-sized FIR call captured on a fresh stream
+    inside torch.cuda.graph: the capture takes counter blocks of
+    its own, zeroed by a captured memset, so every replay starts from zero and
+    never shares counters with eager launches on the stream.  Replays, with
+    eager launches in between, give the eager rows bit for bit."""
+    import torch
+    sig, st, ref = job
+    h = orc.fir_design_lowpass(257, 0.25, 2)
+    plan = vdev.FirPlan(torch.from_numpy(h))
+    x = torch.rand(6, 9_000_001, device="cuda") * 2 - 1
+    yref = plan(x).clone()
+    out, y = torch.empty_like(ref), torch.empty_like(x)
+    torch.cuda.synchronize()
+    d0, f0 = vv.debug_get("STAT_STFT_DYN"), vv.debug_get("STAT_FIR_DYN")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):          # torch captures on a side stream of its own
+        st.spectrogram(sig, out=out)
+        plan(x, out=y)
+    # the captured launches took the dynamic walks
+    assert vv.debug_get("STAT_STFT_DYN") - d0 == 1 and vv.debug_get("STAT_FIR_DYN") - f0 == 1
+    for _ in range(3):
+        out.fill_(-1.0)
+        y.fill_(-1.0)
+        g.replay()
+        eager = st.spectrogram(sig)      # eager work on the default stream between replays
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        assert torch.equal(y, yref)
+        assert torch.equal(eager, ref)
+    del g

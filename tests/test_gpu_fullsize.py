@@ -89,3 +89,35 @@ def test_config4_fir_8ch_2p24(vdev, orc):
     # linearity across channels
     y2 = plan(x[:2] * 2.0 - x[2:4])
     torch.testing.assert_close(y2, y[:2] * 2.0 - y[2:4], rtol=1e-4, atol=1e-5)
+
+
+def test_config5_real_shard_32ch_10min(vdev, orc):
+    """Config 5's actual per-GPU shard at 8 GPUs -- 32 ch x 10 min @ 48 kHz
+    (28,800,000 samples, 112,498 frames per channel; 3.7 GB in, 14.7 GB out),
+    the bench's kernel and walk -- with sampled rows of EVERY channel (first,
+    interior, and the zero-padded last frames) against NumPy f64 at the harness
+    tolerance (stft.c:112-144, python/test_fft.py:37-38), and one whole channel's
+    row sums against the single-channel call (bit-identical)."""
+    import torch
+    C, n = 32, 10 * 60 * 48000
+    sig = torch.empty(C, n, device="cuda")
+    for c in range(C):
+        g = torch.Generator(device="cuda").manual_seed(c)
+        sig[c].uniform_(-1.0, 1.0, generator=g)
+    st = vdev.Stft(1024, 256)
+    fr = st.frames(n)
+    assert fr == 112498
+    mag = st.spectrogram(sig)
+    w = orc.window(1, 1024).astype(np.float64)
+    for c in range(C):
+        frames = [0, 1, 2 + 3517 * c, 56249, 91111 - c, fr - 3, fr - 2, fr - 1]
+        idx = torch.tensor(frames, device="cuda")
+        got = mag[c].index_select(0, idx).cpu().numpy()
+        x = sig[c].cpu().numpy().astype(np.float64)
+        pad = np.concatenate([x, np.zeros(1024)])
+        ref = np.abs(np.fft.fft(np.stack([pad[f * 256:f * 256 + 1024] for f in frames]) * w, axis=1))
+        np.testing.assert_allclose(got, ref, rtol=5e-5, atol=5e-5, err_msg=f"channel {c}")
+    one = st.spectrogram(sig[17:18])
+    assert torch.equal(one[0], mag[17])
+    del mag, one, sig
+    torch.cuda.empty_cache()

@@ -13,6 +13,8 @@ import os
 import numpy as np
 import pytest
 
+from test_gpu_parity import harness_or_normwise
+
 from conftest import tolerances
 from vvapi import C2C, R2C, C2R, FWD, BWD
 
@@ -76,15 +78,15 @@ def test_mixed_batched_device(vdev, n, b):
 
 
 @pytest.mark.parametrize("n", [100, 400, 1000, 3000])
-def test_mixed_matches_dft_kernel(vdev, monkeypatch, n):
+def test_mixed_matches_dft_kernel(vdev, knob, n):
     """The mixed-radix result agrees with the exact-angle f64 DFT kernel (n < 1025)
-    or Bluestein (VVHIP_NO_MIXED=1 selects them) to f32 FFT accuracy."""
+    or Bluestein (knob NO_MIXED=1 selects them) to f32 FFT accuracy."""
     import torch
     rng = np.random.default_rng(n + 11)
     b = 4
     x = torch.from_numpy((rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)).cuda()
     ym = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(x).cpu().numpy()
-    monkeypatch.setenv("VVHIP_NO_MIXED", "1")
+    knob("NO_MIXED", "1")
     yo = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(x).cpu().numpy()
     assert _nw(ym, yo) <= 2e-6
 
@@ -147,7 +149,7 @@ def test_mixed_fourstep_c2c(amd, n):
     for d, npf, spf in ((FWD, np.fft.fft, scipy.fft.fft), (BWD, np.fft.ifft, scipy.fft.ifft)):
         ref = npf(x.astype(np.complex128))
         y = amd.fft(x, C2C, d)
-        assert _nw(y, ref) <= max(4 * _nw(spf(x), ref), 1e-6), (d, _nw(y, ref), _nw(spf(x), ref))
+        harness_or_normwise(y, ref, spf(x), 4)
     assert _nw(amd.fft(amd.fft(x, C2C, FWD), C2C, BWD), x) <= 1e-5
 
 
@@ -159,30 +161,31 @@ def test_mixed_fourstep_real(amd, n):
     ref = np.fft.rfft(xr.astype(np.float64))
     X = amd.fft(xr, R2C)
     assert X.shape == (n // 2 + 1,) and X[-1].imag == 0.0
-    assert _nw(X, ref) <= max(4 * _nw(scipy.fft.rfft(xr), ref), 1e-6)
+    harness_or_normwise(X, ref, scipy.fft.rfft(xr), 4)
     assert _nw(amd.fft(X, C2R, BWD, n=n), xr) <= 1e-5
 
 
 @pytest.mark.parametrize("n,b,chunk_mb", [(48000, 5, ""), (44100, 3, "1"), (4800, 33, "0")])
-def test_mixed_fourstep_batched(vdev, monkeypatch, n, b, chunk_mb):
+def test_mixed_fourstep_batched(vdev, knob, n, b, chunk_mb):
     """Batched device plans through the four-step (chunks of one transform
-    with VVHIP_MIX_CHUNK_MB=1), in place, and against Bluestein
-    (VVHIP_NO_MIXED=1) to f32 FFT accuracy."""
+    with knob MIX_CHUNK_MB=1), in place, and against Bluestein
+    (knob NO_MIXED=1) to f32 FFT accuracy."""
     import torch
     rng = np.random.default_rng(n + b)
     x = (rng.random((b, n)) - 0.5 + 1j * (rng.random((b, n)) - 0.5)).astype(np.complex64)
     xd = torch.from_numpy(x).cuda()
-    monkeypatch.setenv("VVHIP_MIX_CHUNK_MB", chunk_mb)
+    knob("MIX_CHUNK_MB", chunk_mb)
     yf = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xd).cpu().numpy()
     yb = vdev.FftPlan(n, vdev.C2C, vdev.BWD, batch=b)(xd).cpu().numpy()
+    import scipy.fft
     x64 = x.astype(np.complex128)
     for i in range(b):
-        assert _nw(yf[i], np.fft.fft(x64[i])) <= 2e-6, i
-        assert _nw(yb[i], np.fft.ifft(x64[i])) <= 2e-6, i
+        harness_or_normwise(yf[i], np.fft.fft(x64[i]), scipy.fft.fft(x[i]), 4)
+        harness_or_normwise(yb[i], np.fft.ifft(x64[i]), scipy.fft.ifft(x[i]), 4)
     xi = xd.clone()
     vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xi, out=xi)
     np.testing.assert_array_equal(xi.cpu().numpy(), yf)
-    monkeypatch.setenv("VVHIP_NO_MIXED", "1")
+    knob("NO_MIXED", "1")
     yo = vdev.FftPlan(n, vdev.C2C, vdev.FWD, batch=b)(xd).cpu().numpy()
     assert _nw(yf, yo) <= 4e-6
 
@@ -250,13 +253,13 @@ def _per_bin(y, ref, what, r=None, a=None):
                                            (320, 160, 2, 16000), (441, 220, 2, 44100), (600, 240, 3, 9999),
                                            (640, 320, 1, 32000), (720, 360, 2, 14401), (800, 200, 2, 8000),
                                            (900, 450, 2, 27000)])
-def test_stft_speech_register_kernel(vdev, orc, monkeypatch, nfft, hop, nch, n):
+def test_stft_speech_register_kernel(vdev, orc, knob, nfft, hop, nch, n):
     """The two-pass register kernel (k_stft_sq) at every length it serves:
     magnitude, complex and power rows of a multi-channel device STFT against
     NumPy f64 per bin at the harness tolerance (python/test_fft.py:37-38;
     power rows scale |X|'s bound by 2|X|), magnitudes at least as close to f64
     as the reference's own rows (the oracle: its f32 O(n^2) DFT,
-    fft_kiss.c:76-92), and the generic kernel (VVHIP_STFT_SQ=0) as a third
+    fft_kiss.c:76-92), and the generic kernel (knob STFT_SQ=0) as a third
     opinion."""
     import torch
     r, a = tolerances()
@@ -280,7 +283,7 @@ def test_stft_speech_register_kernel(vdev, orc, monkeypatch, nfft, hop, nch, n):
     kiss = orc.spectrogram(x[0][: (sel.stop - 1) * hop + nfft], nfft, hop)[sel]
     X = np.abs(_stft_f64(x[0], nfft, hop, fr)[sel])
     assert np.all(np.abs(mag[0][sel] - X) <= np.abs(kiss - X) + a + r * X)
-    monkeypatch.setenv("VVHIP_STFT_SQ", "0")
+    knob("STFT_SQ", "0")
     for f, g in zip((mag, cpx, pw), rows()):
         assert f.shape == g.shape
         assert np.abs(f - g).max() <= 2e-6 * np.abs(g).max()
@@ -289,11 +292,11 @@ def test_stft_speech_register_kernel(vdev, orc, monkeypatch, nfft, hop, nch, n):
 @pytest.mark.parametrize("n,b", [(400, 1001), (480, 7), (960, 130), (320, 33), (441, 65), (600, 9), (640, 64),
                                  (720, 5), (800, 100), (900, 17)])
 @pytest.mark.parametrize("fwd", [True, False])
-def test_c2c_register_kernel(vdev, orc, monkeypatch, n, b, fwd):
+def test_c2c_register_kernel(vdev, orc, knob, n, b, fwd):
     """c2c rows through the register kernel, both directions, out of place and
     in place: per bin against NumPy f64 at the harness tolerance, at least as
     close to f64 as the reference (Kiss restatement, its O(n^2) DFT) on a
-    sample of rows, and against the generic kernel (VVHIP_STFT_SQ=0)."""
+    sample of rows, and against the generic kernel (knob STFT_SQ=0)."""
     import torch
     r, a = tolerances()
     rng = np.random.default_rng(n + b)
@@ -310,19 +313,19 @@ def test_c2c_register_kernel(vdev, orc, monkeypatch, n, b, fwd):
         k = orc.fft(x[i], C2C, d)
         assert np.all(np.abs(fast[i] - ref[i]) <= np.abs(k - ref[i]) + a + r * np.abs(ref[i])), i
     np.testing.assert_array_equal(inplace.cpu().numpy(), fast)
-    monkeypatch.setenv("VVHIP_STFT_SQ", "0")
+    knob("STFT_SQ", "0")
     gen = plan(xd).cpu().numpy()
     assert np.abs(fast - gen).max() <= 2e-6 * np.abs(ref).max()
 
 
 @pytest.mark.parametrize("n,b", [(400, 1001), (480, 3), (960, 77), (640, 12), (882, 31), (1200, 8), (1600, 40),
                                  (1800, 3), (1920, 5)])
-def test_r2c_register_kernel(vdev, orc, monkeypatch, n, b):
+def test_r2c_register_kernel(vdev, orc, knob, n, b):
     """Real rows whose n/2-point transform is a register length (the even/odd
     pair transform plus the split step): per bin against NumPy f64 at the
     harness tolerance, Im(Nyquist) = 0 exactly (fft_kiss.c:120-147), at least
     as close to f64 as the reference's R2C on a sample of rows, and against the
-    generic kernel (VVHIP_STFT_SQ=0)."""
+    generic kernel (knob STFT_SQ=0)."""
     import torch
     r, a = tolerances()
     rng = np.random.default_rng(3 * n + b)
@@ -337,7 +340,7 @@ def test_r2c_register_kernel(vdev, orc, monkeypatch, n, b):
     for i in sorted({0, b - 1}):
         k = orc.fft(x[i], R2C)
         assert np.all(np.abs(fast[i] - ref[i]) <= np.abs(k - ref[i]) + a + r * np.abs(ref[i])), i
-    monkeypatch.setenv("VVHIP_STFT_SQ", "0")
+    knob("STFT_SQ", "0")
     gen = plan(xd).cpu().numpy()
     assert np.abs(fast - gen).max() <= 2e-6 * np.abs(ref).max()
 
@@ -423,7 +426,8 @@ def test_stft_smooth_nfft_above_fused(vdev, nfft, hop):
         pad = np.concatenate([x[c], np.zeros(nfft, np.float32)])
         f32 = np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w
         X = np.fft.fft(f32.astype(np.float64), axis=1)
-        bound = max(4 * _nw(scipy.fft.fft(f32, axis=1), X), 1e-6)
-        assert _nw(cpx[c], X) <= bound
-        assert _nw(mag[c], np.abs(X)) <= bound
+        X32 = scipy.fft.fft(f32, axis=1)
+        harness_or_normwise(cpx[c], X, X32, 4)
+        harness_or_normwise(mag[c], np.abs(X), np.abs(X32), 4)
+        bound = max(4 * _nw(X32, X), 1e-6)
         assert _nw(pw[c], np.abs(X[:, :nfft // 2 + 1]) ** 2) <= 2 * bound

@@ -5,6 +5,7 @@ at the harness tolerance (python/test_fft.py:37-38), and the device entry
 writing every element of a sentinel-filled output."""
 import numpy as np
 import pytest
+import vvdsp_amd as vv
 
 pytestmark = pytest.mark.gpu
 
@@ -73,8 +74,7 @@ def test_stft_mirror_through_lds_all_row_kinds(vdev, orc, nfft, hop):
     """nfft 256 / 4096 (k_stft_pair_lds: the mirror bins read back through LDS):
     magnitude, complex and power rows of a multi-channel ragged job against
     NumPy f64 at the harness tolerance, and against the one-frame-per-half-FFT
-    kernel they replace (VVHIP_STFT_HALF=1)."""
-    import os
+    kernel they replace (knob STFT_HALF=1)."""
     import torch
     n = 5 * nfft + 3 * hop + 17
     g = torch.Generator(device="cuda").manual_seed(nfft + hop)
@@ -92,9 +92,9 @@ def test_stft_mirror_through_lds_all_row_kinds(vdev, orc, nfft, hop):
         np.testing.assert_allclose(mag[c], np.abs(X), rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))
         np.testing.assert_allclose(cpx[c], X, rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))
         np.testing.assert_allclose(pw[c], np.abs(X[:, :nfft // 2 + 1]) ** 2, rtol=1e-4, atol=1e-4 * nfft)
-    os.environ["VVHIP_STFT_HALF"] = "1"
+    vv.debug_set("STFT_HALF", 1)
     try:
         old = st.spectrogram(sig).cpu().numpy()
     finally:
-        os.environ["VVHIP_STFT_HALF"] = ""
+        vv.debug_clear("STFT_HALF")
     np.testing.assert_allclose(mag, old, rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))

@@ -8,9 +8,8 @@ vv_dsp_log_mel_device / vv_dsp_mfcc_process_device (both pinned against the
 reference elsewhere: tests/test_gpu_parity.py mel golden rows) -- bit for bit,
 for the fused nfft = 1024 kernel (chunked and dynamic-walk launches) and for
 the two-launch path other shapes take."""
-import os
-
 import pytest
+import vvdsp_amd as vv
 
 pytestmark = pytest.mark.gpu
 
@@ -36,15 +35,21 @@ def test_stft_mel_equals_two_step(vdev, nfft, hop, sr, n_mels, n_coeffs, nch, n,
     st = vdev.Stft(nfft, hop)
     mf = vdev.Mfcc(nfft, n_mels, n_coeffs, float(sr), 20.0, sr / 2.0, lifter=22.0)
     ref = _two_step(vdev, st, mf, sig, log_mel)
+    f0, s0 = vv.debug_get("STAT_MEL_FUSED"), vv.debug_get("STAT_MEL_SPLIT")
     got = mf.from_signal(st, sig, log_mel=log_mel)
     torch.cuda.synchronize()
+    # the path that ran (vv_dsp_amd.h: one kernel for nfft 1024, hop <= 256, and
+    # for MFCC at most 60 mel bands; otherwise the two launches)
+    fused = nfft == 1024 and hop <= 256 and (log_mel or n_mels <= 60)
+    assert (vv.debug_get("STAT_MEL_FUSED") - f0, vv.debug_get("STAT_MEL_SPLIT") - s0) == \
+        ((1, 0) if fused else (0, 1))
     assert got.shape == ref.shape
     assert torch.equal(got, ref)
-    os.environ["VVHIP_MEL_FUSED"] = "0"   # the two-launch path of the same entry point
+    vv.debug_set("MEL_FUSED", 0)   # the two-launch path of the same entry point
     try:
         two = mf.from_signal(st, sig, log_mel=log_mel)
     finally:
-        os.environ["VVHIP_MEL_FUSED"] = ""
+        vv.debug_clear("MEL_FUSED")
     assert torch.equal(two, ref)
 
 

@@ -35,9 +35,9 @@ def _run_threads(fns, iters=6):
 
 @pytest.mark.parametrize("kind,n,batch,chunk_mb", [(C2C, 1024, 1, ""), (R2C, 4096, 3, ""),
                                                    (C2C, 1024, 600, "1")])
-def test_shared_fft_plan_two_threads(amd_lib_path, monkeypatch, kind, n, batch, chunk_mb):
+def test_shared_fft_plan_two_threads(amd_lib_path, knob, kind, n, batch, chunk_mb):
     if chunk_mb:
-        monkeypatch.setenv("VVHIP_HOST_CHUNK_MB", chunk_mb)   # the pipelined two-lane host path
+        knob("HOST_CHUNK_MB", chunk_mb)   # the pipelined two-lane host path
     L = C.CDLL(amd_lib_path)
     L.vv_dsp_fft_make_plan_many.argtypes = [C.c_size_t, C.c_int, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]
     L.vv_dsp_fft_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]

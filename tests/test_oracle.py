@@ -340,3 +340,31 @@ def test_oracle_register_golden(orc, golden):
     for key in (k for k in g if k.startswith("x")):
         n = int(key[1:])
         assert np.array_equal(orc.fft(g[key], R2C), g[f"kiss{n}"]), n
+
+
+def test_perfect_reconstruction_known_answer(orc, ref):
+    """tests/gtest/test_stft.cpp:452-519 (512/128 Hann, three tones, max error
+    < 1e-3, RMS < 1e-5 over [512, 1536)) holds for the compiled reference
+    through its own API and for the oracle's restatement: the known answer the
+    GPU tests (test_gpu_parity.py::test_stft_perfect_reconstruction_*) assert."""
+    import ctypes as C
+    from test_gpu_parity import _pr_check, _pr_signal
+    x, F, H = _pr_signal()
+    fp = lambda a, off=0: a[off:].ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+    st, h = ref.stft_create(F, H, 1)
+    assert st == 0
+    try:
+        y, norm = np.zeros(len(x), np.float32), np.zeros(len(x), np.float32)
+        for start in range(0, len(x) - F + 1, H):
+            spec = np.ascontiguousarray(ref.stft_process(h, np.ascontiguousarray(x[start:start + F]), F).view(np.float32))
+            assert ref.lib.vv_dsp_stft_reconstruct(h, fp(spec), fp(y, start), fp(norm, start)) == 0
+        ref_err = _pr_check(x, y, norm, F)
+    finally:
+        ref.lib.vv_dsp_stft_destroy(h)
+    w = orc.window(1, F)
+    y, norm = np.zeros(len(x), np.float32), np.zeros(len(x), np.float32)
+    for start in range(0, len(x) - F + 1, H):
+        spec = orc.fft((x[start:start + F] * w).astype(np.complex64), C2C, FWD)
+        row = np.ascontiguousarray(spec.view(np.float32))
+        assert orc.lib.orc_stft_reconstruct(fp(w), F, fp(row), fp(y, start), fp(norm, start)) == 0
+    assert _pr_check(x, y, norm, F) == ref_err   # the restatement reproduces the reference's errors exactly

@@ -93,8 +93,7 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
 // LDS (gfx950 gives one workgroup up to 160 KB).  16384 would need 1024
 // threads at <= 128 VGPRs and spills: it stays on the two-pass four-step.
 bool c2c_supported(long long n) {
-    const char* e = getenv("VVHIP_C2C_MAX");   // A/B: 4096 sends 8192 to the two-pass four-step
-    const long long mx = e && *e ? atoll(e) : 8192;
+    const long long mx = knob(KNOB_C2C_MAX, 8192);   // A/B: 4096 sends 8192 to the two-pass four-step
     return n >= 2 && n <= mx && n <= 8192 && (n & (n - 1)) == 0;
 }
 
@@ -284,8 +283,7 @@ static hipError_t run_c2r(const float2* in, float* out, long long batch, long lo
 
 // real 16384: the 8192-point complex kernel geometry (512 threads, 70 KB of LDS)
 bool r2c_supported(long long n) {
-    const char* e = getenv("VVHIP_C2C_MAX");   // A/B: 4096 keeps real 16384 on the promote + four-step path
-    const long long mx = e && *e ? 2 * atoll(e) : 16384;
+    const long long mx = 2 * knob(KNOB_C2C_MAX, 8192);   // A/B: 4096 keeps real 16384 on the promote + four-step path
     return n >= 4 && n <= mx && n <= 16384 && (n & (n - 1)) == 0;
 }
 

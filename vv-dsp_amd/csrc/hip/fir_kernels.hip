@@ -560,11 +560,9 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     if (ql > qf && (2 * qf * lout < le || 2 * ql * lout > n || N + lout > N + (3 * N) / 4))
         return hipErrorInvalidValue;
     static std::atomic<int> capc_b, capc_e, capc_v2;
-    const char* eo = getenv("VVHIP_FIR_OLD");   // A/B switch (scripts/kbench.py), read per call
-    const bool old = eo && *eo == '1';
+    const bool old = knob(KNOB_FIR_OLD, 0) == 1;   // A/B knob (scripts/kbench.py)
     // le == N/4 holds for every filter fir_block gives N = 1024 (taps <= 257)
-    const char* er = getenv("VVHIP_FIR_REG");   // A/B switch (scripts/kbench.py): 0 = LDS-span k_fir_bulk
-    const bool reg = !(er && *er == '0');
+    const bool reg = knob(KNOB_FIR_REG, 1) != 0;   // A/B knob: 0 = LDS-span k_fir_bulk
     if (ql > qf && le == N / 4 && !old && reg) {
         // every pair of every channel in one launch: the edge pairs [0, qf) and
         // [ql, ppc) take the kernel's bounds-checked branch (round 2 ran them as a
@@ -573,19 +571,24 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
             static std::atomic<int> capc_r, capc_rd;
             // the dynamic band walk (k_fir_bulk_reg EXP bit 8): 0.2385 -> 0.2323 ms
             // for config 4, same buffers, bit-identical (profiles/r03_kbench_fir_dyn.jsonl);
-            // VVHIP_FIR_DYN = 0 keeps the static XCD walk (A/B switch, read per call)
-            const char* ed = getenv("VVHIP_FIR_DYN");
-            if (!(ed && *ed == '0')) {
+            // knob FIR_DYN = 0 keeps the static XCD walk (A/B)
+            // Small jobs (< 8 pairs per wave slot of the persistent grid), a grid
+            // too small for 8 XCD groups, or no counter block (pool exhausted, a
+            // first use inside a graph capture) take the static walk below.
+            if (knob(KNOB_FIR_DYN, -1) != 0) {
                 const int cap_d = cached_grid(capc_rd, (const void*)k_fir_bulk_reg<N, 256>, 256, 0, 1LL << 40);
-                unsigned* ctrs = stream_counters(s);
-                if (!ctrs || cap_d < 8) return hipErrorOutOfMemory;
-                hipLaunchKernelGGL((k_fir_bulk_reg<N, 256>), dim3(cap_d / 8 * 8), dim3(256), 0, s, H, x, y, nch,
-                                   x_stride, y_stride, ppc, 0LL, pN, n, prefix, lm1, qf, ql, ctrs);
-                return hipGetLastError();
+                unsigned* ctrs = (cap_d >= 8 && nch * ppc >= 8LL * 4 * cap_d) ? stream_counters(s) : nullptr;
+                if (ctrs) {
+                    stat_inc(STAT_FIR_DYN);
+                    hipLaunchKernelGGL((k_fir_bulk_reg<N, 256>), dim3(cap_d / 8 * 8), dim3(256), 0, s, H, x, y, nch,
+                                       x_stride, y_stride, ppc, 0LL, pN, n, prefix, lm1, qf, ql, ctrs);
+                    return hipGetLastError();
+                }
             }
             const int cap_r = cached_grid(capc_r, (const void*)k_fir_bulk_reg<N>, 256, 0, 1LL << 40);
             const long long need = (nch * ppc + 3) / 4;
             const int grid = (int)(need < cap_r ? need : cap_r);
+            stat_inc(STAT_FIR_STATIC);
             hipLaunchKernelGGL((k_fir_bulk_reg<N>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, ppc,
                                0LL, pN, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
         }
@@ -864,10 +867,7 @@ static hipError_t run_fir_reg(const float* h, long long taps, const float* x, fl
     return hipGetLastError();
 }
 
-static bool fir_reg_enabled() {
-    const char* e = getenv("VVHIP_FIR_DIRECT_LDS");   // A/B: 1 = the LDS kernel
-    return !(e && *e == '1');
-}
+static bool fir_reg_enabled() { return knob(KNOB_FIR_DIRECT_LDS, 0) != 1; }   // A/B: 1 = the LDS kernel
 
 hipError_t launch_fir_direct(const float* h, long long taps, const float* x, float* y, long long n,
                              long long nch, long long x_stride, long long y_stride,

@@ -313,11 +313,6 @@ hipError_t fs_rows_any(int N2, int var, const float2* in, float2* out, int N1, l
     }
 }
 
-long long env_ll(const char* name, long long dflt) {
-    const char* e = getenv(name);
-    return (e && *e) ? atoll(e) : dflt;
-}
-
 // n = N1*N2, 64 <= N1 <= N2 <= 1024
 // One two-pass transform chain over a batch in chunks.  With hooks, the
 // columns pass may read the raw Bluestein input (pre) instead of `in`, and the
@@ -329,9 +324,9 @@ hipError_t twopass_chain(long long n, int lg, int fwd, const float2* in, float2*
     int lo_bits = 0;
     const float2* split = twiddle_split(n, &lo_bits);
     if (!split) return hipErrorOutOfMemory;
-    const int var = (int)env_ll("VVHIP_FS_VAR", 1);
+    const int var = (int)knob(KNOB_FS_VAR, 1);
     // chunk of transforms whose intermediate stays in the Infinity Cache
-    const long long chunk_bytes = env_ll("VVHIP_FS_CHUNK_MB", 0) << 20;
+    const long long chunk_bytes = knob(KNOB_FS_CHUNK_MB, 0) << 20;
     long long chunk = chunk_bytes > 0 ? chunk_bytes / (8 * n) : batch;
     if (chunk < 1) chunk = 1;
     if (chunk > batch) chunk = batch;
@@ -423,7 +418,7 @@ hipError_t launch_c2c_large(long long n, int fwd, const float2* in, float2* out,
         return launch_c2c(n, fwd, in, out, batch, n, n, 1.0f / (float)n, s);
     int lg = 0;
     while ((1LL << lg) < n) ++lg;
-    if (lg <= 20 && env_ll("VVHIP_FS_OLD", 0) == 0) return launch_c2c_twopass(n, lg, fwd, in, out, batch, s);
+    if (lg <= 20 && knob(KNOB_FS_OLD, 0) == 0) return launch_c2c_twopass(n, lg, fwd, in, out, batch, s);
     const long long N1 = 1LL << (lg / 2), N2 = n / N1;   // N1 <= N2 <= 4096
     int lo_bits = 0;
     const float2* tab = twiddle_split(n, &lo_bits);
@@ -570,7 +565,7 @@ hipError_t launch_bluestein(long long n, int fwd, const void* in, int real_in, f
     if (!p) return hipErrorOutOfMemory;
     const long long M = p->M, total = M * batch;
     const int lgM = ilog2((int)(M < (1LL << 30) ? M : (1LL << 30)));
-    if (!c2c_supported(M) && lgM <= 20 && env_ll("VVHIP_FS_OLD", 0) == 0 && env_ll("VVHIP_BLUE_UNFUSED", 0) == 0) {
+    if (!c2c_supported(M) && lgM <= 20 && knob(KNOB_FS_OLD, 0) == 0 && knob(KNOB_BLUE_UNFUSED, 0) == 0) {
         // two-pass M (8192..2^20): chirp pre-multiply and zero padding in the forward
         // columns pass, the product with V in its rows pass, and the post-multiply,
         // scale and truncation to nout in the inverse rows pass -- four kernels,

@@ -861,8 +861,7 @@ hipError_t run_stft_sq(const MixIO& io, long long pairs, hipStream_t s) {
 #define VVH_SQ_HALF_LENGTHS(X) X(200, 10, 20) X(240, 12, 20) VVH_SQ_LENGTHS(X)
 
 bool sq_enabled() {
-    const char* esq = getenv("VVHIP_STFT_SQ");   // 0: the generic kernel (A/B)
-    return !(esq && *esq == '0');
+    return knob(KNOB_STFT_SQ, 1) != 0;   // 0: the generic kernel (A/B)
 }
 
 // c2c rows of n = N1 * N2 through the register kernel
@@ -938,8 +937,7 @@ hipError_t run_mixed_t(const MixedPlan& pl, const MixIO& io, long long batch, hi
 
 template <int MODE>
 hipError_t run_mixed(const MixedPlan& pl, MixIO io, long long batch, hipStream_t s) {
-    const char* ev = getenv("VVHIP_MIX_VAR");
-    io.var = ev ? atoi(ev) : 0;
+    io.var = (int)knob(KNOB_MIX_VAR, 0);
     switch (mixed_threads(pl.n)) {
         case 16: return run_mixed_t<16, MODE>(pl, io, batch, s);
         case 32: return run_mixed_t<32, MODE>(pl, io, batch, s);
@@ -1016,8 +1014,7 @@ static hipError_t launch_fft_mixed_fs(long long n, int fwd, const void* in, int 
     int lo_bits = 0;
     const float2* twn = twiddle_split(n, &lo_bits);   // sqrt(n)-sized, not an n-entry table
     if (!twn) return hipErrorOutOfMemory;
-    const char* ec = getenv("VVHIP_MIX_CHUNK_MB");
-    const long long cmb = ec ? atoll(ec) : 0;
+    const long long cmb = knob(KNOB_MIX_CHUNK_MB, 0);
     long long chunk = cmb > 0 ? (cmb << 20) / (8 * n) : batch;
     if (chunk < 1) chunk = 1;
     if (chunk > batch) chunk = batch;
@@ -1071,8 +1068,8 @@ hipError_t launch_fft_mixed(long long n, int fwd, const void* in, int real_in, f
     // the row with imaginary part zero (MODE 4).
     if (real_in) {
         MixedPlan ph;
-        const char* eh = getenv("VVHIP_MIX_R2C_FULL");   // A/B: 1 = MODE 4 for even n too
-        const bool half = fwd && n % 2 == 0 && nout <= n / 2 + 1 && !(eh && *eh == '1') && make_plan(n / 2, &ph);
+        // knob MIX_R2C_FULL = 1: MODE 4 for even n too (A/B)
+        const bool half = fwd && n % 2 == 0 && nout <= n / 2 + 1 && knob(KNOB_MIX_R2C_FULL, 0) != 1 && make_plan(n / 2, &ph);
         if (half) {
             io.twn = twiddle_table((int)n);
             if (!io.twn) return hipErrorOutOfMemory;

@@ -77,6 +77,23 @@ struct DevBuf {
 };
 
 // Stream-ordered scratch for multi-kernel paths on device pointers.
+// Makes device `d` current for a scope and restores the caller's device after
+// (host-buffer calls of a handle run on the handle's creation device: its
+// stream, staging buffers and window live there).
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev >= 0 && prev != d && hipSetDevice(d) != hipSuccess) prev = -1;
+        if (prev == d) prev = -1;
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DevGuard(const DevGuard&) = delete;
+    DevGuard& operator=(const DevGuard&) = delete;
+};
+
 struct Scratch {
     void* p = nullptr;
     hipStream_t s;
@@ -110,8 +127,7 @@ struct HostLane {
 };
 
 size_t host_chunk_bytes() {
-    const char* e = getenv("VVHIP_HOST_CHUNK_MB");
-    const long long mb = (e && *e) ? atoll(e) : 16;
+    const long long mb = knob(KNOB_HOST_CHUNK_MB, 16);
     return (size_t)(mb > 0 ? mb : 16) << 20;
 }
 
@@ -184,16 +200,9 @@ static size_t fft_out_elems_bytes(const vvhip_fft* p) {
 
 // Non-power-of-two DFT: the mixed-radix kernel for 7-smooth n <= 4096, else the
 // exact-angle f64 O(n^2) kernel for short lengths and Bluestein over the
-// power-of-two kernels from BLUESTEIN_MIN on.  VVHIP_NO_MIXED=1 skips the
+// power-of-two kernels from BLUESTEIN_MIN on.  Knob NO_MIXED = 1 skips the
 // mixed-radix kernel (A/B and the tests that compare the two).
-static bool env_flag(const char* name) {
-    const char* e = getenv(name);
-    return e && *e == '1';
-}
-static bool use_mixed(long long n) {
-    const char* e = getenv("VVHIP_NO_MIXED");
-    return !(e && *e == '1') && mixed_supported(n);
-}
+static bool use_mixed(long long n) { return knob(KNOB_NO_MIXED, 0) != 1 && mixed_supported(n); }
 static hipError_t dft_any(long long n, int fwd, const void* in, int real_in, float2* out, long long nout,
                           long long batch, long long in_dist, long long out_dist, float scale, hipStream_t s) {
     if (use_mixed(n))
@@ -239,7 +248,7 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
             HIPCHK(launch_r2c(N, (const float*)in, (float2*)out, B, N, NH, s), ST_INTERNAL);
             return ST_OK;
         }
-        if (is_pow2(n) && n > 8192 && c2c_large_supported(N / 2) && !env_flag("VVHIP_REAL_PROMOTE")) {
+        if (is_pow2(n) && n > 8192 && c2c_large_supported(N / 2) && knob(KNOB_REAL_PROMOTE, 0) != 1) {
             // the n/2-point C2C of the rows as complex pairs, then the split step
             Scratch Z(s);
             HIPCHK(Z.alloc(8 * (n / 2) * batch), ST_INTERNAL);
@@ -270,7 +279,7 @@ static int fft_run(size_t n, int type, int dir, const void* in, void* out, size_
         HIPCHK(launch_c2r(N, (const float2*)in, (float*)out, B, NH, N, s), ST_INTERNAL);
         return ST_OK;
     }
-    if (is_pow2(n) && n > 8192 && c2c_large_supported(N / 2) && !env_flag("VVHIP_REAL_PROMOTE")) {
+    if (is_pow2(n) && n > 8192 && c2c_large_supported(N / 2) && knob(KNOB_REAL_PROMOTE, 0) != 1) {
         // inverse split step, then the n/2-point inverse C2C straight into the real rows
         Scratch V(s);
         HIPCHK(V.alloc(8 * (n / 2) * batch), ST_INTERNAL);
@@ -316,6 +325,25 @@ int vvhip_memcpy_d2h(void* dst, const void* src, size_t bytes) {
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), ST_INTERNAL);
     return ST_OK;
 }
+// stream-ordered scratch (hipMallocAsync pool of the stream's device) and copies,
+// for the C host code (dist.c); errors land in vvhip_last_error
+int vvhip_malloc_async(void** p, size_t bytes, void* stream) {
+    if (!p) return ST_NULL;
+    *p = nullptr;
+    HIPCHK(hipMallocAsync(p, bytes ? bytes : 16, (hipStream_t)stream), ST_INTERNAL);
+    return ST_OK;
+}
+int vvhip_free_async(void* p, void* stream) {
+    if (p) HIPCHK(hipFreeAsync(p, (hipStream_t)stream), ST_INTERNAL);
+    return ST_OK;
+}
+int vvhip_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream) {
+    if (bytes == 0 || dst == src) return ST_OK;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream), ST_INTERNAL);
+    return ST_OK;
+}
+void vvhip_set_error(const char* what) { g_err = what ? what : ""; }
+
 int vvhip_memset(void* dst, int value, size_t bytes) {
     HIPCHK(hipMemset(dst, value, bytes), ST_INTERNAL);
     return ST_OK;
@@ -347,7 +375,12 @@ int vvhip_get_device(int* device) {
 int vvhip_rows_half_device(const float* d_in, float* d_out, size_t rows, size_t n, int unpack, void* stream) {
     if (!d_in || !d_out) return ST_NULL;
     if (n == 0) return ST_SIZE;
-    if (d_in == d_out) return fail(ST_RANGE, "half-row pack/unpack: in and out must not alias");
+    {   // the kernel reads rows while writing others: any overlap of the byte ranges races
+        const size_t h = n / 2 + 1, in_w = unpack ? h : n, out_w = unpack ? n : h;
+        const uintptr_t a0 = (uintptr_t)d_in, a1 = a0 + sizeof(float) * rows * in_w;
+        const uintptr_t b0 = (uintptr_t)d_out, b1 = b0 + sizeof(float) * rows * out_w;
+        if (rows > 0 && a0 < b1 && b0 < a1) return fail(ST_RANGE, "half-row pack/unpack: in and out overlap");
+    }
     HIPCHK(launch_rows_half(d_in, d_out, (long long)rows, (long long)n, unpack ? 1 : 0, (hipStream_t)stream),
            ST_INTERNAL);
     return ST_OK;
@@ -490,7 +523,7 @@ static int stft_frames_run(vvhip_stft* h, const float* sig, size_t n, size_t nch
                ST_INTERNAL);
         return ST_OK;
     }
-    if (!env_flag("VVHIP_NO_MIXED") && stft_mixed_supported(NF)) {   // 7-smooth nfft <= 4096: one kernel
+    if (knob(KNOB_NO_MIXED, 0) != 1 && stft_mixed_supported(NF)) {   // 7-smooth nfft <= 4096: one kernel
         HIPCHK(launch_stft_mixed(NF, (long long)h->hop, out_kind, sig, (long long)n, (long long)nch,
                                  (long long)ch_stride, (long long)frames, win, out, (long long)out_ch_stride, s),
                ST_INTERNAL);
@@ -593,6 +626,7 @@ int vvhip_stft_spectrogram_range_device(vvhip_stft* h, const float* d_signal, si
 int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, float* out_mag) {
     if (!h || !signal || !out_mag) return ST_NULL;
     std::lock_guard<std::mutex> host_lock(h->host_mu);
+    DevGuard on_dev(h->dev);   // the handle's stream, buffers and window live on its creation device
     if (int st = stft_stream(h)) return st;
     const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
     const size_t ob = sizeof(float) * frames * h->nfft;
@@ -654,6 +688,7 @@ int vvhip_stft_process_device(vvhip_stft* h, const float* d_frames, size_t count
 int vvhip_stft_process_host(vvhip_stft* h, const float* frame, float* spec_out) {
     if (!h || !frame || !spec_out) return ST_NULL;
     std::lock_guard<std::mutex> host_lock(h->host_mu);
+    DevGuard on_dev(h->dev);   // the handle's stream, buffers and window live on its creation device
     if (int st = stft_stream(h)) return st;
     HIPCHK(h->b0.ensure(sizeof(float) * h->nfft), ST_INTERNAL);
     HIPCHK(h->b1.ensure(8 * h->nfft), ST_INTERNAL);
@@ -673,8 +708,8 @@ int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t cou
     hipStream_t s = (hipStream_t)stream;
     const float* win = stft_window_here(h);
     if (!win) return fail(ST_INTERNAL, "stft window on the current device");
-    const char* eo = getenv("VVHIP_ISTFT_OLD");   // A/B switch (scripts/kbench.py): IFFT to scratch + k_ola
-    if (istft_fused_supported((long long)h->nfft, (long long)hop) && !(eo && *eo == '1')) {
+    // knob ISTFT_OLD = 1 (A/B, scripts/kbench.py): IFFT to scratch + k_ola
+    if (istft_fused_supported((long long)h->nfft, (long long)hop) && knob(KNOB_ISTFT_OLD, 0) != 1) {
         HIPCHK(launch_istft_fused((long long)h->nfft, (long long)hop, (const float2*)d_spec, (long long)count,
                                   win, d_out_add, d_norm_add, s),
                ST_INTERNAL);
@@ -693,6 +728,7 @@ int vvhip_stft_reconstruct_device(vvhip_stft* h, const float* d_spec, size_t cou
 int vvhip_stft_reconstruct_host(vvhip_stft* h, const float* spec, float* out_add, float* norm_add) {
     if (!h || !spec || !out_add) return ST_NULL;
     std::lock_guard<std::mutex> host_lock(h->host_mu);
+    DevGuard on_dev(h->dev);   // the handle's stream, buffers and window live on its creation device
     if (int st = stft_stream(h)) return st;
     const size_t nb = sizeof(float) * h->nfft;
     HIPCHK(h->b0.ensure(2 * nb), ST_INTERNAL);
@@ -733,17 +769,11 @@ struct vvhip_fir {
 // of two >= max(4*(L-1), 64), so that at least 3/4 of every block is output,
 // grown toward the preferred size (1024: four transforms per 256-thread
 // workgroup, H and twiddles in 51 KB of LDS) while the signal is longer.
-// VVHIP_FIR_BLOCK overrides the preferred size.  0 = no OLS block (long
+// Knob FIR_BLOCK overrides the preferred size.  0 = no OLS block (long
 // filters use the direct form).
 static size_t fir_block(const vvhip_fir* f, size_t n) {
-    static std::atomic<size_t> pref_cache{0};   // read once; concurrent first calls agree
-    size_t pref = pref_cache.load(std::memory_order_relaxed);
-    if (!pref) {
-        const char* e = getenv("VVHIP_FIR_BLOCK");
-        pref = e ? (size_t)atol(e) : 1024;
-        if (pref < 64 || pref > 8192 || (pref & (pref - 1))) pref = 1024;
-        pref_cache.store(pref, std::memory_order_relaxed);
-    }
+    size_t pref = (size_t)knob(KNOB_FIR_BLOCK, 1024);
+    if (pref < 64 || pref > 8192 || (pref & (pref - 1))) pref = 1024;
     const size_t lm1 = f->taps - 1;
     size_t nr = 64;
     while (nr < 4 * lm1 && nr < 8192) nr <<= 1;
@@ -1387,8 +1417,7 @@ int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_ou
     if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
     if ((kind != 2 && m->nbins == 0) || (kind != 0 && m->n_coeffs == 0)) return fail(ST_RANGE, "mel plan lacks tables");
     if (frames == 0) return ST_OK;
-    const char* eo = getenv("VVHIP_MEL_OLD");   // A/B switch (scripts/kbench.py): one wave per frame
-    if (eo && *eo == '1')
+    if (knob(KNOB_MEL_OLD, 0) == 1)   // A/B knob (scripts/kbench.py): one wave per frame
         HIPCHK(launch_mel(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->meta, m->nnz,
                           m->D, m->lift, m->eps, d_out, (hipStream_t)stream),
                ST_INTERNAL);
@@ -1413,8 +1442,7 @@ int vvhip_stft_mel_device(vvhip_stft* h, vvhip_mel* m, const float* d_signal, si
     const size_t frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
     const float* win = stft_window_here(h);
     if (!win) return fail(ST_INTERNAL, "stft window on the current device");
-    const char* ef = getenv("VVHIP_MEL_FUSED");   // 0: the two launches (A/B), read per call
-    if (!(ef && *ef == '0')) {
+    if (knob(KNOB_MEL_FUSED, 1) != 0) {   // 0: the two launches (A/B)
         MelArgs a;
         a.W = m->W;
         a.chunks = m->chunks;
@@ -1429,10 +1457,14 @@ int vvhip_stft_mel_device(vvhip_stft* h, vvhip_mel* m, const float* d_signal, si
         const hipError_t e = launch_stft_mel(kind, (long long)h->nfft, (long long)h->hop, d_signal, (long long)n,
                                              (long long)nch, (long long)ch_stride, (long long)frames, win, a, d_out,
                                              (long long)out_ch_stride, s);
-        if (e == hipSuccess) return ST_OK;
+        if (e == hipSuccess) {
+            stat_inc(STAT_MEL_FUSED);
+            return ST_OK;
+        }
         if (e != hipErrorNotSupported) return fail(ST_INTERNAL, hipGetErrorString(e));
         (void)hipGetLastError();
     }
+    stat_inc(STAT_MEL_SPLIT);
     const size_t nb = h->nfft / 2 + 1, width = kind == 0 ? (size_t)m->n_mels : (size_t)m->n_coeffs;
     Scratch pw(s);
     HIPCHK(pw.alloc(sizeof(float) * nch * frames * nb), ST_INTERNAL);
@@ -1497,8 +1529,7 @@ float2 chirp_value(long double log_mag, long double angle) {
 
 int czt_run(const vvhip_czt* h, const void* x, int real_in, size_t batch, float2* X, hipStream_t s) {
     if (batch == 0) return ST_OK;
-    const char* eu = getenv("VVHIP_CZT_UNFUSED");   // A/B switch (tests, kbench): the multi-kernel chain
-    if (h->Bs && !(eu && *eu == '1')) {
+    if (h->Bs && knob(KNOB_CZT_UNFUSED, 0) != 1) {   // knob CZT_UNFUSED = 1: the multi-kernel chain (A/B, tests)
         HIPCHK(launch_czt_fused((long long)h->p, x, real_in, (long long)h->n, (long long)h->m, (long long)batch, h->g,
                                 h->Bs, h->post, X, s),
                ST_INTERNAL);
@@ -1633,11 +1664,8 @@ int vvhip_czt_exec_host(const void* x, int real_in, size_t n, size_t m, float w_
     return st;
 }
 
-// one-pass kernels for pow2 n <= 4096; VVHIP_CEPS_UNFUSED=1 selects the chains (A/B, tests)
-static bool ceps_fused(size_t n) {
-    const char* e = getenv("VVHIP_CEPS_UNFUSED");
-    return ceps_fused_supported((long long)n) && !(e && *e == '1');
-}
+// one-pass kernels for pow2 n <= 4096; knob CEPS_UNFUSED = 1 selects the chains (A/B, tests)
+static bool ceps_fused(size_t n) { return ceps_fused_supported((long long)n) && knob(KNOB_CEPS_UNFUSED, 0) != 1; }
 
 int vvhip_cepstrum_device(const float* d_x, size_t n, size_t batch, float* d_c, void* stream) {
     if (!d_x || !d_c) return ST_NULL;

@@ -1175,9 +1175,8 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const int cap0 = cached_grid(capc[0], (const void*)k_stft_pair<N, MODE, 0>, WG, 0, 1LL << 40);
         long long cps = (bulk_pairs + (long long)F * cap0 - 1) / ((long long)F * cap0);
         cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
-        {   // A/B switch (scripts/kbench.py stftcps*): an upper bound on the pairs per slot
-            const char* ec = getenv("VVHIP_STFT_CPS");
-            const long long cmax = ec && *ec ? atoll(ec) : 0;
+        {   // A/B knob (scripts/kbench.py stftcps*): an upper bound on the pairs per slot
+            const long long cmax = knob(KNOB_STFT_CPS, 0);
             if (cmax > 0 && cps > cmax) cps = cmax;
         }
         float* sink = store_sink();
@@ -1193,21 +1192,15 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 grid = (nch * cnt + chunk - 1) / chunk;
             }
             if (var == 4 || var == 5) grid = capv / 8 * 8;   // persistent, the same number of blocks per XCD group
-            if (var == 5) {   // pairs per counter value; VVHIP_STFT_RUN overrides (A/B)
-                long long rl = 2;
-                const char* eru = getenv("VVHIP_STFT_RUN");
-                if (eru && *eru) rl = atoll(eru);
+            if (var == 5) {   // pairs per counter value; knob STFT_RUN overrides (A/B)
+                long long rl = knob(KNOB_STFT_RUN, 2);
                 if (rl < 1 || rl > 64) rl = 2;
-                long long dbs = 6;   // band: 2^dbs runs per (XCD group, slot) stream; VVHIP_STFT_DBS (A/B)
-                const char* edb = getenv("VVHIP_STFT_DBS");
-                if (edb && *edb) dbs = atoll(edb);
+                long long dbs = knob(KNOB_STFT_DBS, 6);   // band: 2^dbs runs per (XCD group, slot) stream (A/B)
                 if (dbs < 0 || dbs > 12) dbs = 6;
                 chunk = (rl << 40) | dbs;
             }
-            if (var == 3) {   // run length (pairs), a divisor of cps; VVHIP_STFT_RUN overrides (A/B)
-                long long rl = cps;
-                const char* eru = getenv("VVHIP_STFT_RUN");
-                if (eru && *eru) rl = atoll(eru);
+            if (var == 3) {   // run length (pairs), a divisor of cps; knob STFT_RUN overrides (A/B)
+                long long rl = knob(KNOB_STFT_RUN, cps);
                 if (rl < 1 || cps % rl) rl = cps;
                 chunk |= rl << 40;
             }
@@ -1223,48 +1216,45 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // T >= 64: VAR 0 also reads its input spans by 16 B LDS-DMA
         if (Geo<N>::T >= 64)
             aligned = aligned && hop % 4 == 0 && hop <= N / 2 && ((uintptr_t)sig & 15) == 0 && (ch_stride & 3) == 0;
-        if (MODE != 0) {   // A/B switch: the register-load variant with per-bin stores
-            const char* e = getenv("VVHIP_POW_OLD");
-            if (e && *e == '1') aligned = false;
-        }
+        if (MODE != 0 && knob(KNOB_POW_OLD, 0) == 1) aligned = false;   // A/B: register loads, per-bin stores
         // the VAR 0 kernels that read spans by LDS-DMA run the tail pairs too:
         // one launch for the whole job
         constexpr bool FUSE_TAIL = (MODE == 0 || Geo<N>::T == 64) && Geo<N>::NPASS > 1 && Geo<N>::T >= 64;
         // ring spans (VAR 3) when the span is whole 256-float chunks: power rows only
         // (2.74 vs 2.84 ms for 32 ch x 10 min; magnitude and complex rows measured
         // 1-2 % slower than with VAR 0's interleaved walk, profiles/r02_kbench_ring.jsonl).
-        // VVHIP_STFT_RING = 0 / 1 forces VAR 0 / VAR 3 (A/B switch, read per call)
-        const char* er = getenv("VVHIP_STFT_RING");
-        const bool ring = Geo<N>::T == 64 && hop % 256 == 0 &&
-                          (er && *er ? *er == '1' : MODE == 2);
+        // knob STFT_RING = 0 / 1 forces VAR 0 / VAR 3 (A/B)
+        const long long kring = knob(KNOB_STFT_RING, -1);
+        const bool ring = Geo<N>::T == 64 && hop % 256 == 0 && (kring >= 0 ? kring == 1 : MODE == 2);
         // Magnitude and complex rows of large jobs: the persistent dynamic walk (VAR 4) --
         // each wave takes its next pair from a per-(XCD group, slot) counter, so
         // the chip sweeps one moving band of pairs with the load balanced on the
         // fly (-1.6 % against the chunked launch in two same-buffer measurements,
         // profiles/r03_kbench_ablation_samebuf.jsonl lab8192; bit-identical rows).
-        // VVHIP_STFT_DYN = 0 keeps the chunked VAR 0 (A/B switch, read per call).
+        // Knob STFT_DYN = 0 keeps the chunked VAR 0 (A/B).
         // Complex rows take it too (1.629 -> 1.579 ms for 8 ch x 10 min, -3.1 %);
         // power rows keep the ring walk below (2.689 ring vs 2.730 dynamic vs
-        // 2.760 chunked, profiles/r03_kbench_dyn_modes.jsonl).  VVHIP_STFT_DYN =
+        // 2.760 chunked, profiles/r03_kbench_dyn_modes.jsonl).  Knob STFT_DYN =
         // 1 forces it for every row kind (A/B).
-        const char* ed = getenv("VVHIP_STFT_DYN");
+        const long long kdyn = knob(KNOB_STFT_DYN, -1);
         bool dyn = false;
         if constexpr (Geo<N>::T == 64) {
             const int capd = cached_grid(capc[4], (const void*)k_stft_pair<N, MODE, 4>, WG, 0, 1LL << 40);
-            const bool want = ed && *ed ? *ed != '0' : (MODE == 0 || MODE == 1);
+            const bool want = kdyn >= 0 ? kdyn != 0 : (MODE == 0 || MODE == 1);
             dyn = aligned && FUSE_TAIL && want && capd >= 8 &&
                   bulk_pairs >= 16LL * F * capd;   // >= 16 pairs per wave: the band walk pays off
-            if (dyn) {
+            if (dyn) {   // no counter block (pool exhausted, or first use inside a capture): static walk
                 ctrs = stream_counters(s);
-                if (!ctrs) return hipErrorOutOfMemory;
+                dyn = ctrs != nullptr;
             }
         }
         // Magnitude rows with whole-chunk hops: the dynamic walk in runs of 2
         // pairs on a ring (VAR 5): 3.357 vs 3.440 ms (VAR 4) vs 3.501 ms (chunked)
         // for 32 ch x 10 min, runs of 1 / 3 / 4 / 8 / 16 slower; power and complex
         // rows measured 1-4 % slower with it (profiles/r03_kbench_dynring.jsonl).
-        // VVHIP_STFT_DYN = 1 / 2 forces VAR 4 / VAR 5 (A/B)
-        const bool dring = ed && *ed ? *ed == '2' : MODE == 0;
+        // knob STFT_DYN = 1 / 2 forces VAR 4 / VAR 5 (A/B)
+        const bool dring = kdyn >= 0 ? kdyn == 2 : MODE == 0;
+        if (dyn) stat_inc(STAT_STFT_DYN);
         if (dyn && dring && hop % 256 == 0) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 5>, 5, 0LL, ppc);
         } else if (dyn) {
@@ -1280,8 +1270,8 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             }
             if (tpc > 0) launch(k_stft_pair<N, MODE, 2>, 2, mpc, tpc);
         }
-    } else if (!(getenv("VVHIP_STFT_HALF") && *getenv("VVHIP_STFT_HALF") == '1')) {
-        // frame pairs with the mirror read through LDS (VVHIP_STFT_HALF = 1: the
+    } else if (knob(KNOB_STFT_HALF, 0) != 1) {
+        // frame pairs with the mirror read through LDS (knob STFT_HALF = 1: the
         // one-frame-per-half-length-FFT kernel below, A/B)
         const float2* tN = twiddle_table(N);
         const float2* pN = pass_twiddles(N);
@@ -1341,12 +1331,13 @@ static hipError_t run_stft_mel(const float* sig, long long n, long long nch, lon
         per_cu < 1)
         return hipErrorNotSupported;
     unsigned* ctrs = nullptr;
-    const char* ed = getenv("VVHIP_STFT_DYN");
-    const bool dyn_walk = !(ed && *ed == '0') && cap >= 8 && pairs >= 16LL * F * cap;
+    bool dyn_walk = knob(KNOB_STFT_DYN, -1) != 0 && cap >= 8 && pairs >= 16LL * F * cap;
+    if (dyn_walk) {   // no counter block: the chunked walk (bit-identical)
+        ctrs = stream_counters(s);
+        dyn_walk = ctrs != nullptr;
+    }
     long long grid, chunk = 0;
     if (dyn_walk) {
-        ctrs = stream_counters(s);
-        if (!ctrs) return hipErrorOutOfMemory;
         grid = cap / 8 * 8;
     } else {
         long long cps = (pairs + (long long)F * cap - 1) / ((long long)F * cap);

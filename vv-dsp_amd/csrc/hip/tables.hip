@@ -17,7 +17,7 @@ namespace {
 std::mutex g_mu;
 std::map<std::tuple<int, int, long long>, void*> g_cache;   // (device, kind, n) -> device buffer
 
-enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2, KIND_SINK = 3, KIND_SPLIT = 4, KIND_CTR = 5 };
+enum Kind { KIND_WN = 0, KIND_WN_D = 1, KIND_PASS = 2, KIND_SINK = 3, KIND_SPLIT = 4 };
 
 int current_device() {
     int dev = 0;
@@ -104,19 +104,76 @@ const float2* twiddle_split(long long n, int* lo_bits) {
     });
 }
 
-// Write sink for lanes whose store has no destination in a kernel that keeps
-// its count of memory instructions fixed (SINK_FLOATS floats, never read).
-// Work counters of the dynamically scheduled STFT launch (k_stft_pair VAR 4),
-// one zeroed block per (device, stream): the kernel's last wave of each counter
-// stream resets it, so launches ordered on one stream find it zero, and launches
-// on different streams never share one.
+// Work counters of the dynamically scheduled launches (k_stft_pair VAR 4/5,
+// k_fir_bulk_reg's band walk): blocks of STFT_CTR_WORDS words from a per-device
+// pool allocated and zeroed ONCE (hipMalloc + synchronous memset, on the first
+// dynamic launch of the device outside a graph capture).
+//  * eager launches: one block per (device, stream), handed out on the stream's
+//    first dynamic launch and kept; the kernel's last wave of each counter
+//    stream resets it, so launches ordered on one stream find it zero, and
+//    launches on different streams never share one;
+//  * launches recorded into a HIP graph (hipStreamIsCapturing): a block of the
+//    capture's own that no other launch ever uses, zeroed by a captured
+//    one-block kernel ahead of the launch, so every replay starts from zero and a
+//    replay never shares counters with eager work on the capture stream.
+// Nothing here blocks inside a capture.  When the pool is exhausted (or a
+// capture comes before the pool exists) it returns nullptr and the launcher
+// takes its static walk (bit-identical results).
+namespace {
+// the captured zeroing of a capture's counter block (a kernel node)
+__global__ void k_zero_words(unsigned* p, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0u;
+}
+constexpr int CTR_POOL_BLOCKS = 256;   // 256 x 4 KB per device
+struct CtrPool {
+    unsigned* base = nullptr;
+    int used = 0;
+    bool failed = false;
+    std::map<hipStream_t, unsigned*> by_stream;
+};
+std::map<int, CtrPool> g_ctr;
+}  // namespace
+
 unsigned* stream_counters(hipStream_t s) {
-    return (unsigned*)cached(KIND_CTR, (long long)(uintptr_t)s, sizeof(unsigned) * STFT_CTR_WORDS,
-                             [](unsigned char* b) {
-                                 for (size_t i = 0; i < sizeof(unsigned) * STFT_CTR_WORDS; ++i) b[i] = 0;
-                             });
+    constexpr size_t bytes = sizeof(unsigned) * STFT_CTR_WORDS;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    const int dev = current_device();
+    std::lock_guard<std::mutex> lk(g_mu);
+    CtrPool& p = g_ctr[dev];
+    if (!p.base) {
+        if (capturing || p.failed) return nullptr;
+        void* d = nullptr;
+        if (hipMalloc(&d, bytes * CTR_POOL_BLOCKS) != hipSuccess) {
+            p.failed = true;
+            return nullptr;
+        }
+        if (hipMemset(d, 0, bytes * CTR_POOL_BLOCKS) != hipSuccess) {
+            (void)hipFree(d);
+            p.failed = true;
+            return nullptr;
+        }
+        p.base = (unsigned*)d;
+    }
+    if (capturing) {
+        if (p.used >= CTR_POOL_BLOCKS) return nullptr;
+        unsigned* b = p.base + (size_t)p.used * STFT_CTR_WORDS;
+        hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, b, (int)STFT_CTR_WORDS);
+        if (hipGetLastError() != hipSuccess) return nullptr;
+        ++p.used;
+        return b;
+    }
+    auto it = p.by_stream.find(s);
+    if (it != p.by_stream.end()) return it->second;
+    if (p.used >= CTR_POOL_BLOCKS) return nullptr;
+    unsigned* b = p.base + (size_t)p.used++ * STFT_CTR_WORDS;
+    p.by_stream[s] = b;
+    return b;
 }
 
+// Write sink for lanes whose store has no destination in a kernel that keeps
+// its count of memory instructions fixed (SINK_FLOATS floats, never read).
 float* store_sink() {
     return (float*)cached(KIND_SINK, 0, sizeof(float) * SINK_FLOATS, [](unsigned char* b) {
         for (size_t i = 0; i < sizeof(float) * SINK_FLOATS; ++i) b[i] = 0;

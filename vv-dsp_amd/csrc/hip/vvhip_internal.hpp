@@ -9,6 +9,22 @@
 
 namespace vvh {
 
+// ---- A/B switches and path counters (debug.hip) ---------------------------
+// Knob values come from vvhip_debug_set (or, with VVHIP_AB=1, from the
+// environment read once per process); knob(k, dflt) returns dflt when unset.
+enum Knob : int {
+    KNOB_STFT_CPS, KNOB_STFT_RUN, KNOB_STFT_DBS, KNOB_POW_OLD, KNOB_STFT_RING, KNOB_STFT_DYN, KNOB_STFT_HALF,
+    KNOB_FS_VAR, KNOB_FS_CHUNK_MB, KNOB_FS_OLD, KNOB_BLUE_UNFUSED, KNOB_C2C_MAX, KNOB_STFT_SQ, KNOB_MIX_VAR,
+    KNOB_MIX_CHUNK_MB, KNOB_MIX_R2C_FULL, KNOB_FIR_OLD, KNOB_FIR_REG, KNOB_FIR_DYN, KNOB_FIR_DIRECT_LDS, KNOB_FIR_BLOCK,
+    KNOB_HOST_CHUNK_MB, KNOB_NO_MIXED, KNOB_REAL_PROMOTE, KNOB_ISTFT_OLD, KNOB_MEL_OLD, KNOB_MEL_FUSED, KNOB_CZT_UNFUSED,
+    KNOB_CEPS_UNFUSED,
+    KNOB_COUNT
+};
+long long knob(Knob k, long long dflt);
+// launches of the paths the tests must see taken (vvhip_debug_get("STAT_..."))
+enum Stat : int { STAT_STFT_DYN, STAT_FIR_DYN, STAT_FIR_STATIC, STAT_MEL_FUSED, STAT_MEL_SPLIT, STAT_COUNT };
+void stat_inc(Stat s);
+
 // Device-resident W_N^k = exp(-2*pi*i*k/N) table, k < N, f32 rounded from double.
 // Cached per N for the process lifetime (per device).
 const float2* twiddle_table(int n);
@@ -64,7 +80,9 @@ int mel_chunk_schedule(const int* meta, int n_mels, std::vector<int>* chunks, st
 // with nothing to write, in kernels that hand-count their memory operations.
 constexpr size_t SINK_FLOATS = 1u << 18;   // 1 MiB = 4096 waves x 64 lanes
 float* store_sink();
-// per-(device, stream) zeroed work counters of the dynamic STFT walk (32 streams x 32 words)
+// zeroed work counters of the dynamic walks (32 counter streams x 32 words) for a
+// launch on stream s (tables.hip: per-(device, stream) pool blocks; a private,
+// memset-on-replay block under graph capture); nullptr: take the static walk
 constexpr size_t STFT_CTR_WORDS = 32 * 32;
 unsigned* stream_counters(hipStream_t s);
 // ---- batched framing (framing_kernels.hip), framing.c:58-146 semantics

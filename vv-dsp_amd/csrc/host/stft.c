@@ -158,6 +158,13 @@ vv_dsp_status vv_dsp_stft_reconstruct_device(vv_dsp_stft* h, const vv_dsp_cpx* d
 }
 
 /* ---- multi-GPU layout (vv_dsp_amd.h) ---- */
+vv_dsp_status vv_dsp_stft_get_sizes(const vv_dsp_stft* h, size_t* fft_size, size_t* hop_size) {
+    if (!h) return VV_DSP_ERROR_NULL_POINTER;
+    if (fft_size) *fft_size = h->nfft;
+    if (hop_size) *hop_size = h->hop;
+    return VV_DSP_OK;
+}
+
 vv_dsp_status vv_dsp_shard_range(size_t total, size_t world, size_t rank, size_t* first, size_t* count) {
     if (!first || !count) return VV_DSP_ERROR_NULL_POINTER;
     if (world == 0 || rank >= world) return VV_DSP_ERROR_OUT_OF_RANGE;

@@ -45,6 +45,10 @@ def lib():
     L.vvhip_available.restype = C.c_int
     L.vvhip_last_error.restype = C.c_char_p
     L.vvhip_version.restype = C.c_char_p
+    L.vvhip_debug_set.argtypes = [C.c_char_p, C.c_longlong]
+    L.vvhip_debug_clear.argtypes = [C.c_char_p]
+    L.vvhip_debug_get.argtypes = [C.c_char_p]
+    L.vvhip_debug_get.restype = C.c_longlong
     L.vv_dsp_fft_make_plan_many.argtypes = [_sz, C.c_int, C.c_int, _sz, C.POINTER(_vp)]
     L.vv_dsp_fft_execute_device.argtypes = [_vp, _vp, _vp, _vp]
     L.vv_dsp_fft_destroy.argtypes = [_vp]
@@ -77,6 +81,17 @@ def lib():
     L.vv_dsp_czt_plan_create.argtypes = [_sz, _sz, C.c_float, C.c_float, C.c_float, C.c_float, C.POINTER(_vp)]
     L.vv_dsp_czt_plan_destroy.argtypes = [_vp]
     L.vv_dsp_czt_execute_device.argtypes = [_vp, _vp, C.c_int, _sz, _vp, _vp]
+    L.vv_dsp_dist_init_all.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(_vp)]
+    L.vv_dsp_dist_init_loopback.argtypes = [C.c_int, C.c_int, C.POINTER(_vp)]
+    L.vv_dsp_dist_from_comm.argtypes = [_vp, C.POINTER(_vp)]
+    L.vv_dsp_dist_destroy.argtypes = [_vp]
+    L.vv_dsp_dist_local_ranks.argtypes = [_vp]
+    L.vv_dsp_dist_rank_info.argtypes = [_vp, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.vv_dsp_dist_stft.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, C.c_int, _vp, _vp, C.POINTER(_sz)]
+    L.vv_dsp_dist_gather_rows.argtypes = [_vp, _vp, _sz, _sz, C.c_int, _vp, C.c_int, _vp]
+    L.vv_dsp_dist_fft.argtypes = [_vp, _sz, C.c_int, C.c_int, _sz, _vp, _vp, _vp]
+    L.vv_dsp_dist_fir_apply_fft.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp]
+    L.vv_dsp_stft_get_sizes.argtypes = [_vp, C.POINTER(_sz), C.POINTER(_sz)]
     for f in ("cepstrum_real", "icepstrum_minphase", "minphase_from_cepstrum"):
         getattr(L, f"vv_dsp_{f}_device").argtypes = [_vp, _sz, _sz, _vp, _vp]
     L.vvhip_fir_block_size.argtypes = [_vp, _sz]
@@ -118,6 +133,43 @@ def _expect(t, dtype, numel, what):
         raise VvError(f"{what}: {t.numel()} elements, the plan needs {numel}")
     if not (t.is_cuda and t.is_contiguous()):
         raise VvError(f"{what}: must be a contiguous device tensor")
+
+
+def debug_set(name, value):
+    """Select a launcher alternative (csrc/hip/debug.hip knob, e.g. "STFT_DYN", 0)."""
+    if lib().vvhip_debug_set(name.encode(), int(value)) != 0:
+        raise VvError(f"unknown knob {name!r} or bad value {value!r}")
+
+
+def debug_clear(name=None):
+    """Back to the default path (None: every knob, and every path counter to 0)."""
+    if lib().vvhip_debug_clear(None if name is None else name.encode()) != 0:
+        raise VvError(f"unknown knob {name!r}")
+
+
+def debug_get(name):
+    """A knob's value (-1 = unset) or a path counter ("STAT_FIR_DYN", ...)."""
+    v = lib().vvhip_debug_get(name.encode())
+    if v == -2:
+        raise VvError(f"unknown knob {name!r}")
+    return v
+
+
+class knobs:
+    """with vv.knobs(STFT_DYN=0): ...  -- set knobs for a block, clear them after."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            debug_set(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.kw:
+            debug_clear(k)
+        return False
 
 
 def device_count():
@@ -467,3 +519,75 @@ def icepstrum_minphase(c, stream=None):
 def minphase_from_cepstrum(c, stream=None):
     """minimum-phase spectrum (complex64, imaginary parts 0) from cepstrum rows (minphase.c:7-31)"""
     return _ceps_rows("vv_dsp_minphase_from_cepstrum_device", c, torch.complex64, "minphase_from_cepstrum", stream)
+
+
+def _ptrs(xs):
+    """per-local-rank pointer array (vv_dsp_dist.h): tensors, raw ints or None"""
+    return (_vp * len(xs))(*[None if x is None else (x if isinstance(x, int) else x.data_ptr()) for x in xs])
+
+
+def _streams(streams, n):
+    if streams is None:
+        streams = [torch.cuda.current_stream()] * n
+    return (_vp * n)(*[s if (s is None or isinstance(s, int)) else s.cuda_stream for s in streams])
+
+
+class Dist:
+    """Multi-GPU layout of the spectral path over RCCL (include/vv_dsp/vv_dsp_dist.h):
+    Dist.all([0, 1, ...]) -- every rank in this process (ncclCommInitAll);
+    Dist.from_comm(ptr)   -- one rank of a caller's ncclComm_t;
+    Dist.loopback(world)  -- `world` ranks on one device, transfers as device copies.
+    Per-rank list arguments have one element per local rank (slot)."""
+
+    def __init__(self, handle):
+        self.h = handle
+        self.slots = lib().vv_dsp_dist_local_ranks(self.h)
+
+    @classmethod
+    def all(cls, devices):
+        h = _vp()
+        arr = (C.c_int * len(devices))(*devices)
+        _check(lib().vv_dsp_dist_init_all(len(devices), arr, C.byref(h)), "dist_init_all")
+        return cls(h)
+
+    @classmethod
+    def loopback(cls, world, device=0):
+        h = _vp()
+        _check(lib().vv_dsp_dist_init_loopback(world, device, C.byref(h)), "dist_init_loopback")
+        return cls(h)
+
+    @classmethod
+    def from_comm(cls, comm_ptr):
+        h = _vp()
+        _check(lib().vv_dsp_dist_from_comm(comm_ptr, C.byref(h)), "dist_from_comm")
+        return cls(h)
+
+    def rank_info(self, slot):
+        r, w, d = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().vv_dsp_dist_rank_info(self.h, slot, C.byref(r), C.byref(w), C.byref(d)), "dist_rank_info")
+        return r.value, w.value, d.value
+
+    def stft(self, st, sigs, n, total_ch, ch_stride, rows, out_kind=0, streams=None):
+        nf = _sz(0)
+        _check(lib().vv_dsp_dist_stft(self.h, st.h, _ptrs(sigs), n, total_ch, ch_stride, out_kind, _ptrs(rows),
+                                      _streams(streams, self.slots), C.byref(nf)), "dist_stft")
+        return nf.value
+
+    def gather_rows(self, local, total_rows, row_floats, out, root=0, half=False, streams=None):
+        _check(lib().vv_dsp_dist_gather_rows(self.h, _ptrs(local), total_rows, row_floats, 1 if half else 0,
+                                             None if out is None else _ptr(out), root,
+                                             _streams(streams, self.slots)), "dist_gather_rows")
+
+    def fft(self, n, kind, direction, total_batch, ins, outs, streams=None):
+        _check(lib().vv_dsp_dist_fft(self.h, n, kind, direction, total_batch, _ptrs(ins), _ptrs(outs),
+                                     _streams(streams, self.slots)), "dist_fft")
+
+    def fir(self, plans, n, total_ch, xs, x_stride, ys, y_stride, streams=None):
+        arr = (_vp * len(plans))(*[p.h for p in plans])
+        _check(lib().vv_dsp_dist_fir_apply_fft(self.h, arr, n, total_ch, _ptrs(xs), x_stride, _ptrs(ys), y_stride,
+                                               _streams(streams, self.slots)), "dist_fir_apply_fft")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.vv_dsp_dist_destroy(self.h)
+            self.h = None

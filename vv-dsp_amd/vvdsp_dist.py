@@ -137,9 +137,10 @@ def host_sink(out):
 
 
 def gather_rows_half(local, total, nfft, dst=0, group=None, out=None, pack=None, unpack=None):
-    """gather_rows for magnitude / power rows [ch, frames, nfft] of real frames,
-    sending bins 0..nfft/2 only (SURVEY 8e row note 1: half the xGMI bytes of
-    config 5's gather).  Each rank packs its rows, the packed rows are gathered,
+    """gather_rows for magnitude rows [ch, frames, nfft] of real frames, sending
+    bins 0..nfft/2 only (SURVEY 8e row note 1: half the xGMI bytes of config 5's
+    gather).  The library's power rows are already nfft/2+1 wide: gather those
+    with gather_rows directly.  Each rank packs its rows, the packed rows are gathered,
     and rank `dst` expands them by mirror symmetry.  pack / unpack default to
     the library's device kernels (vv_dsp_spectrogram_{pack,unpack}_half_device);
     for fused-kernel rows the result equals gather_rows bit for bit."""
