@@ -53,18 +53,21 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_rank_info(const vv_dsp_dist* d, int s
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_stft(vv_dsp_dist* d, vv_dsp_stft* h, const vv_dsp_real* const* d_signal,
                                                 size_t n, size_t total_ch, size_t ch_stride, int out_kind,
                                                 void* const* d_rows, void* const* streams, size_t* out_frames);
-/* The gather: every rank's rows d_local[s] = [count_r][row_floats] (count_r
- * from vv_dsp_shard_range(total_rows, world, r)) into d_root_out =
- * [total_rows][row_floats] on rank `root` (ignored on other ranks), in rank =
- * row order, in slabs of at most 256 MiB per rank.  half != 0: the rows are
+/* The gather: every rank's items d_local[s] = [count_r][rows_per_item][row_floats]
+ * (count_r from vv_dsp_shard_range(total_items, world, r): channels of a
+ * spectrogram, rows_per_item = its frames) into d_root_out =
+ * [total_items][rows_per_item][row_floats] on rank `root` (ignored on other
+ * ranks), in rank = item order, in slabs of at most 256 MiB per rank (a slab
+ * may end inside an item).  half != 0: the rows are
  * magnitude (or mirror-symmetric) rows of fft_size = row_floats bins; each rank
  * sends bins 0..fft_size/2 only and the root expands them
  * (vv_dsp_spectrogram_pack/unpack_half_device): the same rows for half the
  * xGMI bytes.  Stream-ordered on streams[s]: returns once everything is
  * enqueued; the sources must be complete in stream order on streams[s]. */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* d_local,
-                                                       size_t total_rows, size_t row_floats, int half,
-                                                       vv_dsp_real* d_root_out, int root, void* const* streams);
+                                                       size_t total_items, size_t rows_per_item, size_t row_floats,
+                                                       int half, vv_dsp_real* d_root_out, int root,
+                                                       void* const* streams);
 /* Config 2: each local rank transforms its batch shard -- transforms
  * vv_dsp_shard_range(total_batch, world, rank) of a [total_batch][n] job, d_in[s]
  * / d_out[s] pointing at the shard's first transform (layout as

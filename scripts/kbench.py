@@ -302,6 +302,12 @@ def case_firreglab(e, nch=8, n=1 << 24):
     return case_firlab(e, nch, n, fn="firreglab_run")
 
 
+def case_firr32lab(e, nch=8, n=1 << 24):
+    """k_fir_r32 (the product's config-4 kernel) with parts switched off (scripts/stftlab.hip
+    firr32lab_run: 2 no FFTs, 4 no stores, 8 no loads)"""
+    return case_firlab(e, nch, n, fn="firr32lab_run")
+
+
 def case_firlab(e, nch=8, n=1 << 24, fn="firlab_run"):
     """k_fir_bulk (config 4's bulk pairs) with parts switched off (scripts/stftlab.hip firlab_run,
     EXP bits: 1 no FFT exchanges, 2 no FFTs, 4 no stores, 8 no span loads); H = a unit impulse's spectrum"""
@@ -538,6 +544,8 @@ CASES = {
     "firspan": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_REG", "0"),
     "firstatic": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_DYN", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
+    "firr16": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_R32", "0"),
+    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12)},
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),
     "logmelold": with_env(lambda: case_mel(0), "VVHIP_MEL_OLD", "1"),

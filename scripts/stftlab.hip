@@ -81,6 +81,22 @@ static hipError_t lab_firreg(const float2* H, const float* x, float* y, long lon
                        pass_twiddles(N), n, (const float*)nullptr, le, qf, ql, ctr);
     return hipGetLastError();
 }
+// config 4 through k_fir_r32<EXP> (every pair, edges included; EXP bits 2 no
+// FFT, 4 no stores, 8 no loads)
+template <int EXP>
+static hipError_t lab_firr32(const float2* H, const float* x, float* y, long long n, long long nch, hipStream_t s) {
+    constexpr int N = 1024;
+    const long long le = 256, lout = N - le, nblk = (n + lout - 1) / lout, ppc = (nblk + 1) / 2;
+    long long qf = (le + 2 * lout - 1) / (2 * lout), ql = n / (2 * lout);
+    if (ql > ppc) ql = ppc;
+    static std::atomic<int> cap;
+    const int capv = cached_grid(cap, (const void*)k_fir_r32<EXP>, 256, 0, 1LL << 40);
+    const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
+    const int grid = (int)(need < capv ? need : capv);
+    hipLaunchKernelGGL((k_fir_r32<EXP>), dim3(grid), dim3(256), 0, s, H, x, y, nch, n, n, ppc, twiddle_table(N), n,
+                       (const float*)nullptr, le, qf, ql);
+    return hipGetLastError();
+}
 template <int EXP>
 static hipError_t lab_c2c(const float2* in, float2* out, long long batch, hipStream_t s) {
     constexpr int N = 1024, F = Wg<N>::F;
@@ -124,7 +140,19 @@ extern "C" int firreglab_run(int exp, const void* H, const float* x, float* y, l
     switch (exp) {
 #define C(E) case E: return (int)vvh::lab_firreg<E>(h, x, y, n, nch, s);
         C(0) C(2) C(4) C(6) C(8) C(10) C(12) C(14) C(16) C(32) C(64) C(80) C(18) C(34) C(66) C(82) C(128) C(144) C(130)
-        C(256) C(258) C(266)
+        C(256) C(258) C(266) C(512) C(768) C(770) C(778) C(1536) C(1792) C(1794)
+#undef C
+        default: return -1;
+    }
+}
+
+extern "C" int firr32lab_run(int exp, const void* H, const float* x, float* y, long long n, long long nch,
+                             void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const float2* h = (const float2*)H;
+    switch (exp) {
+#define C(E) case E: return (int)vvh::lab_firr32<E>(h, x, y, n, nch, s);
+        C(0) C(2) C(4) C(6) C(8) C(10) C(12)
 #undef C
         default: return -1;
     }

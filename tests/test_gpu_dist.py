@@ -60,16 +60,19 @@ def test_rccl_one_rank_stft_and_gather(job):
     assert torch.equal(rows[0], ref)
     for half in (False, True):
         out = torch.full_like(ref, -1.0)
-        d.gather_rows([rows[0]], NCH * ref.shape[1], 1024, out, root=0, half=half)
+        d.gather_rows([rows[0]], NCH, ref.shape[1], 1024, out, root=0, half=half)
         torch.cuda.synchronize()
         assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("world,root", [(2, 0), (3, 0), (3, 2)])
+@pytest.mark.parametrize("world,root,slab_kb", [(2, 0, 0), (3, 0, 0), (3, 2, 0), (3, 1, 1500), (2, 1, 4097)])
 @pytest.mark.parametrize("half", [False, True])
-def test_loopback_gather_uneven(job, world, root, half):
+def test_loopback_gather_uneven(job, knob, world, root, slab_kb, half):
+    """slab_kb: slabs smaller than a channel (15 MB here), ending inside channels"""
     import torch
     sig, st, ref = job
+    if slab_kb:
+        knob("DIST_SLAB_KB", slab_kb)
     d = vv.Dist.loopback(world)
     assert d.slots == world
     rows = _sharded_rows(d, sig, st, world)
@@ -77,7 +80,7 @@ def test_loopback_gather_uneven(job, world, root, half):
     for (f, c), r in zip(_shards(NCH, world), rows):
         assert torch.equal(r, ref[f:f + c])
     out = torch.full_like(ref, -1.0)
-    d.gather_rows(rows, NCH * ref.shape[1], 1024, out, root=root, half=half)
+    d.gather_rows(rows, NCH, ref.shape[1], 1024, out, root=root, half=half)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
 
@@ -94,7 +97,7 @@ def test_loopback_power_and_complex_rows(job):
         # power rows gather as plain rows (513 floats)
         if kind == 2:
             out = torch.full_like(full, -1.0)
-            d.gather_rows(rows, NCH * full.shape[1], 513, out, root=1)
+            d.gather_rows(rows, NCH, full.shape[1], 513, out, root=1)
             torch.cuda.synchronize()
             assert torch.equal(out, full)
 

@@ -355,6 +355,15 @@ __device__ __forceinline__ void stage_twiddles(float2* lds_tab, const float2* gp
     }
 }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 // Barrier between LDS writes and reads of one transform.  A transform owned by
 // threads of a single wave needs no s_barrier: LDS ops of a wave execute in
 // order; only the compiler must not move them (wave_barrier + fence).
@@ -572,29 +581,105 @@ __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
     if constexpr (G::T > 64) xsync<G::T>();
 }
 
+// N = 1024 (passes 16, 16, 4), one wave per transform, not PAIRED: the
+// exchange of whole complex values (b64 LDS accesses, half the LDS instructions
+// of pass_exchange_ri for twice the buffer) with every address a per-lane base
+// plus a compile-time offset.  Layout: element e at e + (e >> 4) (Geo::pad);
+//   p 0 writes  16b + r             -> 17b + r
+//   p 0 reads   b + 64r   (b < 64)  -> (b + (b >> 4)) + 68r
+//   p 1 writes  256(b>>4) + (b&15) + 16r -> (272(b >> 4) + (b & 15)) + 17r
+//   p 1 reads   b + 256r, b = t + 64i   -> (t + (t >> 4)) + 68i + 272r
+// Bit-identical to pass_exchange (a permutation through LDS either way).
+__host__ __device__ constexpr bool c1024_check() {
+    for (int b = 0; b < 64; ++b)
+        for (int r = 0; r < 16; ++r) {
+            if (Geo<1024>::pad(16 * b + r) != 17 * b + r) return false;
+            if (Geo<1024>::pad(b + 64 * r) != b + (b >> 4) + 68 * r) return false;
+            if (Geo<1024>::pad(256 * (b >> 4) + (b & 15) + 16 * r) != 272 * (b >> 4) + (b & 15) + 17 * r) return false;
+        }
+    for (int t = 0; t < 64; ++t)
+        for (int i = 0; i < 4; ++i)
+            for (int r = 0; r < 4; ++r)
+                if (Geo<1024>::pad(t + 64 * i + 256 * r) != t + (t >> 4) + 68 * i + 272 * r) return false;
+    return true;
+}
+static_assert(c1024_check(), "pass_exchange_c1024 offsets");
+
+// One ds_read_b64 at a compile-time byte offset.  Written out because the
+// compiler pairs adjacent b64 reads into ds_read2_b64, which moves the same
+// bytes at half the rate (8 LDS cycles for two, against 2 per ds_read_b64:
+// MI355X_MICROARCH.md, LDS table).  The compiler does not count asm LDS ops:
+// lds_rd_done() waits for them (its own lgkmcnt waits only become stricter).
+template <int OFF>
+__device__ __forceinline__ float2 lds_rd64(unsigned addr) {
+    static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+    vf2_t r;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return upk(r);
+}
+// s_waitcnt lgkmcnt(0), then every value read by lds_rd64 is tied behind it
+template <int K>
+__device__ __forceinline__ void lds_rd_done(float2* v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < K; ++i) asm volatile("" : "+v"(v[i].x), "+v"(v[i].y));
+}
+
+template <int p>
+__device__ __forceinline__ void pass_exchange_c1024(float2* v, int t, float2* lds) {
+    static_assert(p == 0 || p == 1, "N = 1024 has two exchanges");
+    const unsigned q = (unsigned)(uintptr_t)(lds + t + (t >> 4));   // LDS byte address of the read base
+    if constexpr (p == 0) {
+        float2* w = lds + 17 * t;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[r] = v[r];
+        xsync<64>();
+        static_for<0, 16>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            v[r] = lds_rd64<8 * 68 * r>(q);
+        });
+    } else {
+        float2* w = lds + 272 * (t >> 4) + (t & 15);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[17 * r] = v[r];
+        xsync<64>();
+        static_for<0, 16>([&](auto kc) {
+            constexpr int k = decltype(kc)::value, i = k / 4, r = k % 4;
+            v[k] = lds_rd64<8 * (68 * i + 272 * r)>(q);
+        });
+    }
+    lds_rd_done<16>(v);
+    xsync<64>();   // the next exchange's writes must not pass these reads (compiler order only)
+}
+
 // NOX: timing ablation only (scripts/membench.hip) -- the passes without their
 // exchanges, i.e. a wrong transform with the FFT's arithmetic but no LDS traffic.
-template <int N, bool FWD, int p, bool PAIRED, bool RI = false, bool NOX = false>
+// C64: N = 1024 one-wave transforms exchange through pass_exchange_c1024.
+template <int N, bool FWD, int p, bool PAIRED, bool RI = false, bool NOX = false, bool C64 = false>
 struct PassChain {
     template <class TW>
     __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TW& tw) {
         pass_compute<N, FWD, p, PAIRED>(v, t, tw);
         if constexpr (p + 1 < Geo<N>::NPASS) {
             if constexpr (NOX) asm volatile("" ::: "memory");
+            else if constexpr (C64) pass_exchange_c1024<p>(v, t, lds);
             else if constexpr (RI) pass_exchange_ri<N, p, PAIRED>(v, t, reinterpret_cast<float*>(lds));
             else pass_exchange<N, p, PAIRED>(v, t, lds);
-            PassChain<N, FWD, p + 1, PAIRED, RI, NOX>::run(v, t, lds, tw);
+            PassChain<N, FWD, p + 1, PAIRED, RI, NOX, C64>::run(v, t, lds, tw);
         }
     }
 };
 
 // Full transform.  On entry v[r] = x[t + r*T] (r < P).  On exit register q
 // holds X[out_pos<N, PAIRED>(t, q)].  RI: `lds` needs only Geo<N>::LDS floats
-// (pass_exchange_ri) instead of Geo<N>::LDS float2.
-template <int N, bool FWD, bool PAIRED = false, bool RI = false, class TW = TwTab<N>, bool NOX = false>
+// (pass_exchange_ri) instead of Geo<N>::LDS float2.  C64 (N = 1024, T = 64,
+// not PAIRED): the explicit-offset complex exchange, Geo<N>::LDS float2.
+template <int N, bool FWD, bool PAIRED = false, bool RI = false, class TW = TwTab<N>, bool NOX = false,
+          bool C64 = false>
 __device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TW& tw) {
     static_assert(!PAIRED || Geo<N>::CAN_PAIR, "mirror pairing needs >= 2 last-pass butterflies per thread");
-    PassChain<N, FWD, 0, PAIRED, RI, NOX>::run(v, t, lds, tw);
+    static_assert(!C64 || (N == 1024 && !PAIRED && !RI), "pass_exchange_c1024: N = 1024, one wave, not paired");
+    PassChain<N, FWD, 0, PAIRED, RI, NOX, C64>::run(v, t, lds, tw);
 }
 
 // ---- shared pieces of the persistent streaming kernels ---------------------
@@ -687,14 +772,6 @@ __device__ __forceinline__ void st4_sbase(unsigned lane_off, float v, const void
     static_assert(IMM >= -4096 && IMM <= 4095, "global offset range");
     asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(lane_off), "v"(v), "s"(base), "n"(IMM)
                  : "memory");
-}
-// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + 1, E>(f);
-    }
 }
 template <int CNT>
 __device__ __forceinline__ void vm_wait() {

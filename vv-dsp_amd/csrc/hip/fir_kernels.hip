@@ -335,11 +335,16 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
                long long qf, long long ql, unsigned* ctrs) {
     using G = Geo<N>;
     constexpr bool DYN = (EXP & 256) != 0;
+    // EXP bit 9: the FFT exchanges as whole complex values (b64 LDS accesses,
+    // 2x the buffer) instead of real/imaginary halves (b32); bit 10 with it:
+    // through pass_exchange_c1024's explicit offsets instead of pass_exchange
+    constexpr bool B64X = (EXP & 512) != 0;
+    constexpr bool C64 = B64X && (EXP & 1024) != 0;
     static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
     constexpr int F = 4, RL = G::RL;
     constexpr int LE = N / 4, LOUT = N - LE;   // taps <= N/4 + 1
     constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
-    constexpr int XW = ri_floats<N>();
+    constexpr int XW = B64X ? 2 * G::LDS : ri_floats<N>();
     __shared__ __attribute__((aligned(16))) float xch[F * XW];
     __shared__ float2 ltab[TWL];
     __shared__ float2 lH[N / 2 + 1];
@@ -445,7 +450,7 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
         tw.opaque();
-        if constexpr (!(EXP & 2)) fft_regs<N, true, false, true, TwLastReg<N>>(v, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, true, false, !B64X, TwLastReg<N>, false, C64>(v, t, my, tw);
         float2 u[G::P];
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
@@ -454,7 +459,7 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
             else u[m] = cmul(v[q], cconj(lH[N - t - 64 * m]));
         }
         tw.opaque();
-        if constexpr (!(EXP & 2)) fft_regs<N, false, false, true, TwLastReg<N>>(u, t, my, tw);
+        if constexpr (!(EXP & 2)) fft_regs<N, false, false, !B64X, TwLastReg<N>, false, C64>(u, t, my, tw);
         if (more && !is_edge(jn)) {   // ahead of this pair's stores: in flight across them
             load_a(cn, jn);
             load_b(cn, jn);
@@ -519,6 +524,265 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
     }
 }
 
+// ------------------------------------------------------------------------
+// k_fir_r32: config 4's overlap-save (N = 1024, LE = 256, LOUT = 768) with the
+// 1024-point transforms split 32 x 32 instead of 16 x 16 x 4, so each FFT
+// crosses LDS ONCE (a 32 x 32 transpose) instead of twice.  The FFTs of
+// k_fir_bulk_reg are LDS-bound (each exchange moves 8 KB through a ~80 B/clk
+// write path per CU; four exchanges per pair): this halves the exchanges.
+//
+// A transform lives on 32 lanes (32 points per lane), so a wave runs two pairs
+// at once, one per half.  Forward, for z[n] = a[n] + i b[n], n = 32 m1 + m2:
+//   lane m2: DFT_32 over m1 (registers) -> k1, times W_1024^(m2 k1)
+//   transpose through LDS (row k1, column m2; rows padded to 33: conflict-free)
+//   lane k1: DFT_32 over m2 -> X[k1 + 32 k2] in register k2.
+// The product with H (f < 512: H[f], else conj H[1024 - f]) keeps that
+// layout, and the inverse runs the same two steps mirrored:
+//   lane k1: IDFT_32 over k2 -> a, times conj W_1024^(k1 a)
+//   transpose; lane a: IDFT_32 over k1 -> b:  y[a + 32 b] in register b,
+// so the 768 outputs of a block (e = a + 32 b >= 256, b >= 8) leave as 24
+// lane-contiguous dword stores per block.  Each lane keeps its 31 twiddles
+// W_1024^(m r) come from an LDS table [r][m] (consecutive lanes, consecutive
+// words) and the next pair's 64 samples are loaded during the current pair's
+// transforms: two waves per SIMD (launch bounds 256, 2); exchange buffers
+// 66 KB + H 4 KB + twiddles 8 KB per workgroup, two workgroups per CU.
+// Edge pairs (span before sample 0 or past n) load through the prefix / zero
+// rule and store predicated, in the same loop (a wave-uniform branch).
+// EXP (timing ablations, scripts/stftlab.hip; the library uses 0): bit 1 no
+// FFT, bit 2 no stores, bit 3 no loads.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ constexpr float cos32(int m) {
+    constexpr float c1 = 0.98078528040323044913f, c2 = 0.92387953251128675613f, c3 = 0.83146961230254523708f,
+                    c4 = 0.70710678118654752440f, c5 = 0.55557023301960222474f, c6 = 0.38268343236508977173f,
+                    c7 = 0.19509032201612826785f;
+    switch (m & 31) {
+        case 0: return 1.0f;  case 1: return c1;  case 2: return c2;  case 3: return c3;
+        case 4: return c4;    case 5: return c5;  case 6: return c6;  case 7: return c7;
+        case 8: return 0.0f;  case 9: return -c7; case 10: return -c6; case 11: return -c5;
+        case 12: return -c4;  case 13: return -c3; case 14: return -c2; case 15: return -c1;
+        case 16: return -1.0f; case 17: return -c1; case 18: return -c2; case 19: return -c3;
+        case 20: return -c4;  case 21: return -c5; case 22: return -c6; case 23: return -c7;
+        case 24: return 0.0f; case 25: return c7;  case 26: return c6;  case 27: return c5;
+        case 28: return c4;   case 29: return c3;  case 30: return c2;  default: return c1;
+    }
+}
+
+// In-register DFT of length 32 (natural order in and out): two DFT_16 of the
+// even and odd points, combined with W_32^k (exact rotations at k = 0, 8).
+template <bool FWD>
+__device__ __forceinline__ void dft32(float2* v) {
+    float2 e[16], o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        e[i] = v[2 * i];
+        o[i] = v[2 * i + 1];
+    }
+    Dft<16, FWD>::run(e);
+    Dft<16, FWD>::run(o);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (k == 8) {   // o * (-i) forward, (+i) backward: folded into the adds
+            v[k] = FWD ? cadd_i<false>(e[k], o[k]) : cadd_i<true>(e[k], o[k]);
+            v[k + 16] = FWD ? cadd_i<true>(e[k], o[k]) : cadd_i<false>(e[k], o[k]);
+        } else {
+            float2 t = o[k];
+            if (k != 0) {
+                const float c = cos32(k), sn = cos32(k - 8);   // sin(2 pi k / 32)
+                t = cmul(o[k], make_float2(c, FWD ? -sn : sn));
+            }
+            v[k] = cadd(e[k], t);
+            v[k + 16] = csub(e[k], t);
+        }
+    }
+}
+
+// a * conj(w) in two packed instructions (cmul's sequence with the signs of w.y flipped)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 w) {
+    const vf2_t A = pk(a), W = pk(w);
+    vf2_t t, r;
+    // t = a.yy * (w.y, w.x); r = a.xx * (w.x, -w.y) + t = (a.x w.x + a.y w.y, a.y w.x - a.x w.y)
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(A), "v"(W));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(A), "v"(W), "v"(t));
+    return upk(r);
+}
+
+constexpr int R32_ROW = 33;                   // padded row of the 32 x 32 transpose (float2)
+constexpr int R32_BUF = 32 * R32_ROW;         // one transform's exchange buffer (float2)
+
+// register r of every lane -> row r, column `col`; then row `row` -> registers
+__device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int lane32) {
+    float2* w = buf + lane32;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) w[R32_ROW * r] = v[r];
+    xsync<64>();
+    const unsigned q = (unsigned)(uintptr_t)(buf + R32_ROW * lane32);
+    static_for<0, 32>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        v[r] = lds_rd64<8 * r>(q);
+    });
+    lds_rd_done<32>(v);
+    xsync<64>();   // the next transpose's writes must stay behind these reads
+}
+
+template <int EXP = 0>
+__global__ void __launch_bounds__(256, 2)
+k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
+          long long ppc, const float2* tw1024, long long n, const float* prefix, long long lm1, long long qf,
+          long long ql) {
+    constexpr int N = 1024, LE = 256, LOUT = N - LE, F = 4;
+    __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R32_BUF];
+    __shared__ float2 lH[N / 2 + 1];
+    __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r) (row 0 unused)
+    for (int i = threadIdx.x; i <= N / 2; i += 256) lH[i] = Hg[i];
+    for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
+    const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
+    float2* buf = xch + (2 * slot + half) * R32_BUF;
+    const unsigned atw = (unsigned)(uintptr_t)(ltw + m);              // + 256 r: W_1024^(m r)
+    const unsigned ahl = (unsigned)(uintptr_t)(lH + m);               // + 256 k2: H[m + 32 k2], k2 < 16
+    const unsigned ahh = (unsigned)(uintptr_t)(lH + 32 - m);          // + 256 (31 - k2): H[1024 - m - 32 k2]
+    __syncthreads();
+    // v[r] *= W_1024^(m r) (FWD) or its conjugate, r = 1..31, twiddles read 8 at a time
+    auto twiddle = [&](float2* v, auto fwd) {
+        static_for<0, 4>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            float2 w[8];
+            static_for<0, 8>([&](auto kc) {
+                constexpr int r = 8 * g + decltype(kc)::value;
+                if constexpr (r > 0) w[r - 8 * g] = lds_rd64<256 * r>(atw);
+            });
+            lds_rd_done<8>(w);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = 8 * g + k;
+                if (r > 0) v[r] = decltype(fwd)::value ? cmul(v[r], w[k]) : cmulc(v[r], w[k]);
+            }
+        });
+    };
+    const long long pairs = nch * ppc, couples = (pairs + 1) / 2;
+    long long it, it_end, it_step;
+    xcd_walk(couples, F, slot, &it, &it_end, &it_step);
+    it = uni<64>(it);
+    it_end = uni<64>(it_end);
+    it_step = uni<64>(it_step);
+    if (it >= it_end) return;
+    // couple k: pairs 2k (lanes 0..31) and 2k+1 (lanes 32..63); a missing
+    // second pair (odd total) computes pair 2k again and stores nothing
+    auto locate = [&](long long k, long long* c, long long* j, bool* valid, bool* edge_any) {
+        const long long p0 = 2 * k, p1 = p0 + 1 < pairs ? p0 + 1 : p0;
+        const long long pm = half ? p1 : p0;
+        *valid = !half || p0 + 1 < pairs;
+        *c = pm / ppc;
+        const long long q = pm - *c * ppc;
+        *j = 2 * q;
+        const long long q0 = p0 % ppc, q1 = p1 % ppc;
+        *edge_any = q0 < qf || q0 >= ql || q1 < qf || q1 >= ql;
+    };
+    float xa[32], xb[32];
+    auto load_bulk = [&](long long c, long long j) {
+        if constexpr (EXP & 8) return;
+        const float* a = x + c * x_stride + j * LOUT - LE + m;
+        const float* b = a + LOUT;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) xa[r] = __builtin_nontemporal_load(a + 32 * r);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) xb[r] = b[32 * r];   // overlaps the next pair's block a: cached
+    };
+    // edge couples: staged through the (idle) exchange buffer with rolled loops
+    // (the prefix / zero rule per sample), then read back -- no register
+    // array is indexed by a loop variable, and nothing else is live here
+    auto load_edge = [&](long long c, long long j) {
+        const float* xs = x + c * x_stride;
+        const float* pre = prefix ? prefix + c * lm1 : nullptr;
+        float* sf = reinterpret_cast<float*>(buf);
+        const long long s0 = j * LOUT - LE;
+#pragma unroll 1
+        for (int k = m; k < 2 * N; k += 32) {
+            const long long i = s0 + (k < N ? k : k - N + LOUT);
+            float v = 0.0f;
+            if (i < 0) {
+                if (pre && i >= -lm1) v = pre[lm1 + i];
+            } else if (i < n) {
+                v = xs[i];
+            }
+            sf[k] = v;
+        }
+        xsync<64>();
+#pragma unroll
+        for (int r = 0; r < 32; ++r) xa[r] = sf[m + 32 * r];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) xb[r] = sf[N + m + 32 * r];
+        xsync<64>();
+    };
+    long long c, j;
+    bool valid, edge;
+    locate(it, &c, &j, &valid, &edge);
+    if (!edge) load_bulk(c, j);
+    for (; it < it_end; it += it_step) {
+        if (edge) load_edge(c, j);   // at the top of its own iteration (a bulk couple was prefetched)
+        float2 v[32];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[r] = make_float2(xa[r], xb[r]);
+        const long long itn = it + it_step;
+        long long cn = c, jn = j;
+        bool validn = valid, edgen = edge;
+        if (itn < it_end) {   // the next couple's loads, in flight across this one's transforms
+            locate(itn, &cn, &jn, &validn, &edgen);
+            if (!edgen) load_bulk(cn, jn);
+        }
+        if constexpr (!(EXP & 2)) {
+            // forward: DFT over m1, twiddle, transpose, DFT over m2 -> X[m + 32 k2] in v[k2]
+            dft32<true>(v);
+            twiddle(v, std::true_type{});
+            r32_transpose(v, buf, m);
+            dft32<true>(v);
+            // times H: bin f = m + 32 k2 (H[f] for f < 512, conj H[1024 - f] above), 8 reads at a time
+            static_for<0, 4>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                float2 h[8];
+                static_for<0, 8>([&](auto kc) {
+                    constexpr int k2 = 8 * g + decltype(kc)::value;
+                    if constexpr (k2 < 16) h[k2 - 8 * g] = lds_rd64<256 * k2>(ahl);
+                    else h[k2 - 8 * g] = lds_rd64<256 * (31 - k2)>(ahh);
+                });
+                lds_rd_done<8>(h);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int k2 = 8 * g + k;
+                    v[k2] = k2 < 16 ? cmul(v[k2], h[k]) : cmulc(v[k2], h[k]);
+                }
+            });
+            // inverse: IDFT over k2, conj twiddle, transpose, IDFT over k1 -> y[m + 32 b] in v[b]
+            dft32<false>(v);
+            twiddle(v, std::false_type{});
+            r32_transpose(v, buf, m);
+            dft32<false>(v);
+        }
+        if constexpr (!(EXP & 4)) {
+            float* ya = y + c * y_stride + j * LOUT - LE + m;   // + 32 b: block j's output (b >= 8)
+            if (!edge) {
+                if (valid) {
+#pragma unroll
+                    for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].x, ya + 32 * b);
+#pragma unroll
+                    for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].y, ya + LOUT + 32 * b);
+                }
+            } else if (valid) {   // outputs past n are not stored
+                const long long rem = n - (j * LOUT - LE + m);
+                const int rm = (int)(rem < (1 << 30) ? rem : (1 << 30));
+#pragma unroll
+                for (int b = 8; b < 32; ++b) {
+                    if (32 * b < rm) ya[32 * b] = v[b].x;
+                    if (32 * b + LOUT < rm) ya[LOUT + 32 * b] = v[b].y;
+                }
+            }
+        }
+        c = cn;
+        j = jn;
+        valid = validn;
+        edge = edgen;
+    }
+}
+
 // Effective history of the block geometry (see the header comment).
 long long fir_effective_history(long long nfft, long long taps) {
     long long le = taps - 1;
@@ -563,6 +827,30 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     const bool old = knob(KNOB_FIR_OLD, 0) == 1;   // A/B knob (scripts/kbench.py)
     // le == N/4 holds for every filter fir_block gives N = 1024 (taps <= 257)
     const bool reg = knob(KNOB_FIR_REG, 1) != 0;   // A/B knob: 0 = LDS-span k_fir_bulk
+    if constexpr (N == 1024) {
+        // the 32 x 32 transform split (k_fir_r32): one LDS transpose per FFT instead
+        // of two; every pair, edges included, in one launch.  Knob FIR_R32 = 0: the
+        // 16 x 16 x 4 kernels below (A/B)
+        if (le == N / 4 && knob(KNOB_FIR_R32, 1) != 0) {
+            // bulk pairs need no alignment here (dword loads): [qf, ql) from the geometry alone
+            long long qf32 = (le + 2 * lout - 1) / (2 * lout), ql32 = n / (2 * lout);
+            if (ql32 > ppc) ql32 = ppc;
+            if (qf32 >= ql32) qf32 = ql32 = ppc;
+            qf = qf32;
+            ql = ql32;
+            static std::atomic<int> capc_32;
+            const int cap = cached_grid(capc_32, (const void*)k_fir_r32<0>, 256, 0, 1LL << 40);
+            const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
+            const int grid = (int)(need < cap ? need : cap);
+            const float2* t1024 = twiddle_table(1024);
+            if (!t1024) return hipErrorOutOfMemory;
+            if (grid < 1) return hipSuccess;
+            stat_inc(STAT_FIR_R32);
+            hipLaunchKernelGGL((k_fir_r32<0>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, ppc,
+                               t1024, n, prefix, lm1, qf, ql);
+            return hipGetLastError();
+        }
+    }
     if (ql > qf && le == N / 4 && !old && reg) {
         // every pair of every channel in one launch: the edge pairs [0, qf) and
         // [ql, ppc) take the kernel's bounds-checked branch (round 2 ran them as a

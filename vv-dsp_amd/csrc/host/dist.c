@@ -280,36 +280,41 @@ vv_dsp_status vv_dsp_dist_fir_apply_fft(vv_dsp_dist* d, vv_dsp_fir_plan* const* 
 }
 
 /* ---- the gather ---- */
-vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* d_local, size_t total_rows,
-                                      size_t row_floats, int half, vv_dsp_real* d_root_out, int root,
-                                      void* const* streams) {
+/* rank r's rows: items vv_dsp_shard_range(total_items, world, r), rows_per_item each */
+static size_t rows_first(size_t total_items, size_t rpi, int world, int r) { return shard_first(total_items, world, r) * rpi; }
+static size_t rows_count(size_t total_items, size_t rpi, int world, int r) { return shard_count(total_items, world, r) * rpi; }
+
+vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* d_local, size_t total_items,
+                                      size_t rows_per_item, size_t row_floats, int half, vv_dsp_real* d_root_out,
+                                      int root, void* const* streams) {
     if (!d || !d_local || !streams) return VV_DSP_ERROR_NULL_POINTER;
-    if (row_floats == 0) return VV_DSP_ERROR_INVALID_SIZE;
+    if (row_floats == 0 || rows_per_item == 0) return VV_DSP_ERROR_INVALID_SIZE;
     if (root < 0 || root >= d->world) return VV_DSP_ERROR_OUT_OF_RANGE;
     if (!d->loopback && !rccl_ready()) return VV_DSP_ERROR_UNSUPPORTED;
     const int world = d->world, rs = slot_of_rank(d, root);
     if (rs >= 0 && !d_root_out) return VV_DSP_ERROR_NULL_POINTER;
     for (int s = 0; s < d->nslots; ++s)
-        if (!d_local[s] && shard_count(total_rows, world, d->rank[s]) > 0) return VV_DSP_ERROR_NULL_POINTER;
+        if (!d_local[s] && rows_count(total_items, rows_per_item, world, d->rank[s]) > 0) return VV_DSP_ERROR_NULL_POINTER;
     const size_t w = half ? row_floats / 2 + 1 : row_floats;   /* floats sent per row */
     size_t cmax = 0;
     for (int r = 0; r < world; ++r) {
-        const size_t c = shard_count(total_rows, world, r);
+        const size_t c = rows_count(total_items, rows_per_item, world, r);
         if (c > cmax) cmax = c;
     }
     if (cmax == 0) return VV_DSP_OK;
-    size_t slab = DIST_SLAB_BYTES / (sizeof(float) * w);
+    const long long kb = vvhip_debug_get("DIST_SLAB_KB");   /* knob (tests): a smaller slab */
+    size_t slab = (kb > 0 ? (size_t)kb << 10 : DIST_SLAB_BYTES) / (sizeof(float) * w);
     if (slab < 1) slab = 1;
     if (slab > cmax) slab = cmax;
 
     vv_dsp_status st = VV_DSP_OK;
     /* the root's own rows: one device copy to their place (no-op in place) */
     if (rs >= 0) {
-        const size_t c = shard_count(total_rows, world, root);
+        const size_t c = rows_count(total_items, rows_per_item, world, root);
         dev_scope g;
         st = dev_enter(&g, d->dev[rs]);
         if (st == VV_DSP_OK && c)
-            st = vvhip_memcpy_d2d_async(d_root_out + shard_first(total_rows, world, root) * row_floats, d_local[rs],
+            st = vvhip_memcpy_d2d_async(d_root_out + rows_first(total_items, rows_per_item, world, root) * row_floats, d_local[rs],
                                         sizeof(float) * c * row_floats, streams[rs]) == 0
                      ? VV_DSP_OK
                      : VV_DSP_ERROR_INTERNAL;
@@ -325,7 +330,7 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
     void* const rstream = rs >= 0 ? streams[rs] : NULL;
     if (half) {
         for (int s = 0; s < d->nslots && st == VV_DSP_OK; ++s) {
-            if (d->rank[s] == root || shard_count(total_rows, world, d->rank[s]) == 0) continue;
+            if (d->rank[s] == root || rows_count(total_items, rows_per_item, world, d->rank[s]) == 0) continue;
             dev_scope g;
             st = dev_enter(&g, d->dev[s]);
             void* sp = d->loopback ? rstream : streams[s];
@@ -347,7 +352,7 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
         if (half)
             for (int s = 0; s < d->nslots && st == VV_DSP_OK; ++s) {
                 const int r = d->rank[s];
-                const size_t c = shard_count(total_rows, world, r);
+                const size_t c = rows_count(total_items, rows_per_item, world, r);
                 if (r == root || i0 >= c) continue;
                 const size_t cnt = c - i0 < slab ? c - i0 : slab;
                 dev_scope g;
@@ -361,13 +366,13 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
         /* 2. the transfers of this slab: peer r's rows [i0, i0 + cnt) */
         if (d->loopback) {
             for (int r = 0; r < world && st == VV_DSP_OK; ++r) {
-                const size_t c = shard_count(total_rows, world, r);
+                const size_t c = rows_count(total_items, rows_per_item, world, r);
                 if (r == root || i0 >= c) continue;
                 const size_t cnt = c - i0 < slab ? c - i0 : slab;
                 const int s = slot_of_rank(d, r);
                 const float* src = half ? pack[s] : d_local[s] + i0 * row_floats;
                 float* dst = half ? stage + (size_t)r * slab * w
-                                  : d_root_out + (shard_first(total_rows, world, r) + i0) * row_floats;
+                                  : d_root_out + (rows_first(total_items, rows_per_item, world, r) + i0) * row_floats;
                 if (vvhip_memcpy_d2d_async(dst, src, sizeof(float) * cnt * w, rstream) != 0) st = VV_DSP_ERROR_INTERNAL;
             }
         } else {
@@ -379,16 +384,16 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
                 const int r = d->rank[s];
                 if (r == root) {
                     for (int p = 0; p < world && e == ncclSuccess; ++p) {
-                        const size_t c = shard_count(total_rows, world, p);
+                        const size_t c = rows_count(total_items, rows_per_item, world, p);
                         if (p == root || i0 >= c) continue;
                         const size_t cnt = c - i0 < slab ? c - i0 : slab;
                         float* dst = half ? stage + (size_t)p * slab * w
-                                          : d_root_out + (shard_first(total_rows, world, p) + i0) * row_floats;
+                                          : d_root_out + (rows_first(total_items, rows_per_item, world, p) + i0) * row_floats;
                         e = R.recv(dst, cnt * w, ncclFloat32, p, d->comm[s], (hipStream_t)streams[s]);
                         what = "ncclRecv";
                     }
                 } else {
-                    const size_t c = shard_count(total_rows, world, r);
+                    const size_t c = rows_count(total_items, rows_per_item, world, r);
                     if (i0 >= c) continue;
                     const size_t cnt = c - i0 < slab ? c - i0 : slab;
                     const float* src = half ? pack[s] : d_local[s] + i0 * row_floats;
@@ -406,7 +411,7 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
         /* 3. the root expands the half rows to their place */
         if (half && rs >= 0)
             for (int r = 0; r < world && st == VV_DSP_OK; ++r) {
-                const size_t c = shard_count(total_rows, world, r);
+                const size_t c = rows_count(total_items, rows_per_item, world, r);
                 if (r == root || i0 >= c) continue;
                 const size_t cnt = c - i0 < slab ? c - i0 : slab;
                 dev_scope g;
@@ -414,7 +419,7 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
                 if (st == VV_DSP_OK)
                     st = vv_dsp_spectrogram_unpack_half_device(
                         stage + (size_t)r * slab * w, cnt, row_floats,
-                        d_root_out + (shard_first(total_rows, world, r) + i0) * row_floats, rstream);
+                        d_root_out + (rows_first(total_items, rows_per_item, world, r) + i0) * row_floats, rstream);
                 st = dev_leave(&g, st);
             }
     }

@@ -88,7 +88,7 @@ def lib():
     L.vv_dsp_dist_local_ranks.argtypes = [_vp]
     L.vv_dsp_dist_rank_info.argtypes = [_vp, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.vv_dsp_dist_stft.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, C.c_int, _vp, _vp, C.POINTER(_sz)]
-    L.vv_dsp_dist_gather_rows.argtypes = [_vp, _vp, _sz, _sz, C.c_int, _vp, C.c_int, _vp]
+    L.vv_dsp_dist_gather_rows.argtypes = [_vp, _vp, _sz, _sz, _sz, C.c_int, _vp, C.c_int, _vp]
     L.vv_dsp_dist_fft.argtypes = [_vp, _sz, C.c_int, C.c_int, _sz, _vp, _vp, _vp]
     L.vv_dsp_dist_fir_apply_fft.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp]
     L.vv_dsp_stft_get_sizes.argtypes = [_vp, C.POINTER(_sz), C.POINTER(_sz)]
@@ -573,8 +573,11 @@ class Dist:
                                       _streams(streams, self.slots), C.byref(nf)), "dist_stft")
         return nf.value
 
-    def gather_rows(self, local, total_rows, row_floats, out, root=0, half=False, streams=None):
-        _check(lib().vv_dsp_dist_gather_rows(self.h, _ptrs(local), total_rows, row_floats, 1 if half else 0,
+    def gather_rows(self, local, total_items, rows_per_item, row_floats, out, root=0, half=False, streams=None):
+        """items (channels) of rows_per_item rows of row_floats floats; rank r's
+        items from vv_dsp_shard_range(total_items, world, r)"""
+        _check(lib().vv_dsp_dist_gather_rows(self.h, _ptrs(local), total_items, rows_per_item, row_floats,
+                                             1 if half else 0,
                                              None if out is None else _ptr(out), root,
                                              _streams(streams, self.slots)), "dist_gather_rows")
 
