@@ -249,6 +249,23 @@ def case_wr(mode, nt, rows=3600000, blocks=2048):
     return (lambda: lib.membench_write(out.data_ptr(), rows, mode, nt, blocks, s)), rows * 4096, (out, lib)
 
 
+def case_wprobe(w, pol, band, rd, blocks=2048, items=3599936):
+    """write-ceiling probe (membench.hip k_wprobe): items x 4 KB written (the
+    headline's 14.7 GB of rows), + 1 KB read per item with rd; one buffer pair
+    shared by every probe case (same placement)"""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libmembench.so"))
+    lib.membench_wprobe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong] + [ctypes.c_int] * 5 + \
+        [ctypes.c_void_p]
+    if ("wprobe", items) not in _SHARED:
+        _SHARED[("wprobe", items)] = (torch.rand(items * 256, device="cuda"), torch.empty(items * 1024, device="cuda"))
+    a, b = _SHARED[("wprobe", items)]
+    s = torch.cuda.current_stream().cuda_stream
+    f = (lambda: lib.membench_wprobe(a.data_ptr(), b.data_ptr(), items, w, pol, band, rd, blocks, s))
+    assert f() == 0
+    return f, items * 4096 + (items * 1024 if rd else 0), (a, b, lib)
+
+
 def case_stft_exp(e, nch=32, seconds=600):
     """STFT kernel with parts switched off (scripts/membench.hip k_stft_exp)"""
     import ctypes
@@ -327,17 +344,19 @@ def case_firlab(e, nch=8, n=1 << 24, fn="firlab_run"):
         (x, y, H, lib)
 
 
-def case_c2clab(e, batch=65536):
-    """k_c2c<1024> forward with parts switched off (scripts/stftlab.hip c2clab_run: 1 no exchanges, 2 no FFT)"""
+def case_c2clab(e, batch=65536, fn="c2clab_run"):
+    """k_c2c<1024> forward with parts switched off (scripts/stftlab.hip c2clab_run: 1 no exchanges, 2 no FFT;
+    c2cr32lab_run: k_c2c_r32, 2 no FFT)"""
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
-    lib.c2clab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
+    run = getattr(lib, fn)
+    run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
     if ("c2clab", batch) not in _SHARED:   # one buffer pair for every c2c lab case (same placement)
         x = torch.rand(batch, 1024, dtype=torch.complex64, device="cuda")
         _SHARED[("c2clab", batch)] = (x, torch.empty_like(x))
     x, y = _SHARED[("c2clab", batch)]
     s = torch.cuda.current_stream().cuda_stream
-    return (lambda: lib.c2clab_run(e, x.data_ptr(), y.data_ptr(), batch, s)), 2 * batch * 1024 * 8, (x, y, lib)
+    return (lambda: run(e, x.data_ptr(), y.data_ptr(), batch, s)), 2 * batch * 1024 * 8, (x, y, lib)
 
 
 def case_rw(w, in_bytes=3686400000, blocks=4096):
@@ -418,6 +437,10 @@ CASES = {
     **{f"ex{e}": (lambda e=e: case_stft_exp(e)) for e in range(8)},
     "rw1": lambda: case_rw(1), "rw4": lambda: case_rw(4),
     **{f"rw{w}b{b}": (lambda w=w, b=b: case_rw(w, blocks=b)) for w in (1, 4) for b in (256, 512, 1024, 2048, 16384)},
+    **{f"wp{w}p{p}b{b}r{r}": (lambda w=w, p=p, b=b, r=r: case_wprobe(w, p, b, r))
+       for w in (1, 4) for p in (0, 1, 2, 3) for b in (0, 1, 2) for r in (0, 1)},
+    **{f"wp{w}p{p}b{b}r{r}g{g}": (lambda w=w, p=p, b=b, r=r, g=g: case_wprobe(w, p, b, r, blocks=g))
+       for w in (1, 4) for p in (0, 1) for b in (0, 1, 2) for r in (0, 1) for g in (1024, 4096, 16384)},
     "wr4": lambda: case_wr(0, 0), "wr4nt": lambda: case_wr(0, 1),
     "wrpat": lambda: case_wr(1, 0), "wrpatnt": lambda: case_wr(1, 1),
     "wr8nt": lambda: case_wr(2, 1), "wr16": lambda: case_wr(3, 0), "wr16nt": lambda: case_wr(3, 1),
@@ -453,6 +476,9 @@ CASES = {
     "blue48000unf": with_env(lambda: case_c2c(48000, 1024), "VVHIP_BLUE_UNFUSED", "1"),
     "blue48000old": with_env(lambda: case_c2c(48000, 1024), "VVHIP_FS_OLD", "1"),
     "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),
+    "c2c1024r16": with_env(lambda: case_c2c(1024, 65536), "VVHIP_C2C_R32", "0"),
+    "c2c1024br16": with_env(lambda: case_c2c(1024, 65536, fwd=False), "VVHIP_C2C_R32", "0"),
+    **{f"c2cr32lab{e}": (lambda e=e: case_c2clab(e, fn="c2cr32lab_run")) for e in (0, 2)},
     # mixed-radix (7-smooth non-power-of-two) lengths; *nomix: the f64 DFT kernel / Bluestein
     **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
     **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
@@ -570,7 +596,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--mark", action="store_true",
                     help="launch a tiny torch fill kernel before each case's runs (splits a rocprofv3 trace per case)")
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "ex", "rw", "lab", "model", "firlab", "c2clab"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "wp", "ex", "rw", "lab", "model", "firlab", "c2clab"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

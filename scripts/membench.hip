@@ -407,3 +407,80 @@ extern "C" int membench_model(const float* sig, float* out, long long pairs, lon
 #undef MODEL_LD4
     return -1;
 }
+
+// ---- write-ceiling probe (round 4): pure streams of 4 KB items (the headline's
+// 14.7 GB of magnitude rows), or the 1:4 read:write mix, in the shapes the STFT
+// kernel could use.  W: 1 dword / 4 dwordx4 per lane; POL: 0 plain, 1 nt,
+// 2 sc1, 3 sc0 sc1 nt; BAND: 0 one grid-wide interleaved front, 1 one
+// contiguous eighth of the buffer per XCD group (block % 8), 2 per-XCD-group
+// 2 MB chunks dealt round robin; RD: also read 1 KB per item (16 B/lane nt).
+template <int POL>
+__device__ __forceinline__ void wst4(float* p, vf4 v) {
+    if constexpr (POL == 0) *reinterpret_cast<vf4*>(p) = v;
+    else if constexpr (POL == 1) __builtin_nontemporal_store(v, reinterpret_cast<vf4*>(p));
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+template <int POL>
+__device__ __forceinline__ void wst1(float* p, float v) {
+    if constexpr (POL == 0) *p = v;
+    else if constexpr (POL == 1) __builtin_nontemporal_store(v, p);
+    else if constexpr (POL == 2) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+template <int W, int POL, int BAND, int RD>
+__global__ void __launch_bounds__(256) k_wprobe(const float* in, float* out, long long items) {
+    const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr long long CH = 512;   // 2 MB of output = 512 items
+    long long first, step;
+    const long long nb = gridDim.x, b = blockIdx.x, g = b % 8, nbg = (nb - g + 7) / 8;
+    long long lo = 0, hi = items;
+    if constexpr (BAND == 0) {
+        first = b * 4 + wv;
+        step = nb * 4;
+    } else {
+        first = (b / 8) * 4 + wv;
+        step = nbg * 4;
+        if constexpr (BAND == 1) {
+            lo = g * items / 8;
+            hi = (g + 1) * items / 8;
+        } else {
+            hi = (items / CH + 7 - g) / 8 * CH;   // this group's chunks g, g+8, ... (whole chunks)
+        }
+    }
+    float acc = (float)t;
+    for (long long s = first; lo + s < hi; s += step) {
+        long long it = lo + s;
+        if constexpr (BAND == 2) it = ((s / CH) * 8 + g) * CH + s % CH;
+        if (it >= items) break;
+        if constexpr (RD) {
+            const vf4 x = __builtin_nontemporal_load(reinterpret_cast<const vf4*>(in + it * 256) + t);
+            acc += x.x + x.y + x.z + x.w;
+        }
+        float* o = out + it * 1024;
+        if constexpr (W == 4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wst4<POL>(o + 4 * (t + 64 * j), vf4{acc, acc, acc, acc});
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) wst1<POL>(o + t + 64 * j, acc);
+        }
+    }
+}
+
+extern "C" int membench_wprobe(const float* in, float* out, long long items, int w, int pol, int band, int rd,
+                               int blocks, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int key = ((w == 4 ? 1 : 0) * 4 + pol) * 6 + band * 2 + (rd ? 1 : 0);
+#define L(W, P, B, R)                                                                                  \
+    case ((W == 4 ? 1 : 0) * 4 + P) * 6 + B * 2 + R:                                                    \
+        hipLaunchKernelGGL((k_wprobe<W, P, B, R>), dim3(blocks), dim3(256), 0, s, in, out, items); break;
+#define LB(W, P) L(W, P, 0, 0) L(W, P, 0, 1) L(W, P, 1, 0) L(W, P, 1, 1) L(W, P, 2, 0) L(W, P, 2, 1)
+    switch (key) {
+        LB(1, 0) LB(1, 1) LB(1, 2) LB(1, 3) LB(4, 0) LB(4, 1) LB(4, 2) LB(4, 3)
+        default: return -1;
+    }
+#undef LB
+#undef L
+    return (int)hipGetLastError();
+}

@@ -108,7 +108,26 @@ static hipError_t lab_c2c(const float2* in, float2* out, long long batch, hipStr
                        pass_twiddles(N), twiddle_table(N), 1.0f);
     return hipGetLastError();
 }
+template <int EXP>
+static hipError_t lab_c2c_r32(const float2* in, float2* out, long long batch, hipStream_t s) {
+    static std::atomic<int> cap;
+    const int grid_cap = cached_grid(cap, (const void*)k_c2c_r32<true, EXP>, 256, 0, 1LL << 40);
+    const long long need = ((batch + 1) / 2 + 3) / 4;
+    const int grid = (int)(need < grid_cap ? need : grid_cap);
+    hipLaunchKernelGGL((k_c2c_r32<true, EXP>), dim3(grid), dim3(256), 0, s, in, out, batch, 1024LL, 1024LL,
+                       twiddle_table(1024), 1.0f);
+    return hipGetLastError();
+}
 }  // namespace vvh
+
+extern "C" int c2cr32lab_run(int exp, const void* in, void* out, long long batch, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (exp) {
+        case 0: return (int)vvh::lab_c2c_r32<0>((const float2*)in, (float2*)out, batch, s);
+        case 2: return (int)vvh::lab_c2c_r32<2>((const float2*)in, (float2*)out, batch, s);
+        default: return -1;
+    }
+}
 
 extern "C" int c2clab_run(int exp, const void* in, void* out, long long batch, void* stream) {
     hipStream_t s = (hipStream_t)stream;

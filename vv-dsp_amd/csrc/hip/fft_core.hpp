@@ -652,6 +652,101 @@ __device__ __forceinline__ void pass_exchange_c1024(float2* v, int t, float2* ld
     xsync<64>();   // the next exchange's writes must not pass these reads (compiler order only)
 }
 
+// ---- 1024 = 32 x 32 transforms on half-waves (k_fir_r32, k_c2c_r32) -------
+__device__ __forceinline__ constexpr float cos32(int m) {
+    constexpr float c1 = 0.98078528040323044913f, c2 = 0.92387953251128675613f, c3 = 0.83146961230254523708f,
+                    c4 = 0.70710678118654752440f, c5 = 0.55557023301960222474f, c6 = 0.38268343236508977173f,
+                    c7 = 0.19509032201612826785f;
+    switch (m & 31) {
+        case 0: return 1.0f;  case 1: return c1;  case 2: return c2;  case 3: return c3;
+        case 4: return c4;    case 5: return c5;  case 6: return c6;  case 7: return c7;
+        case 8: return 0.0f;  case 9: return -c7; case 10: return -c6; case 11: return -c5;
+        case 12: return -c4;  case 13: return -c3; case 14: return -c2; case 15: return -c1;
+        case 16: return -1.0f; case 17: return -c1; case 18: return -c2; case 19: return -c3;
+        case 20: return -c4;  case 21: return -c5; case 22: return -c6; case 23: return -c7;
+        case 24: return 0.0f; case 25: return c7;  case 26: return c6;  case 27: return c5;
+        case 28: return c4;   case 29: return c3;  case 30: return c2;  default: return c1;
+    }
+}
+
+// In-register DFT of length 32 (natural order in and out): two DFT_16 of the
+// even and odd points, combined with W_32^k (exact rotations at k = 0, 8).
+template <bool FWD>
+__device__ __forceinline__ void dft32(float2* v) {
+    float2 e[16], o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        e[i] = v[2 * i];
+        o[i] = v[2 * i + 1];
+    }
+    Dft<16, FWD>::run(e);
+    Dft<16, FWD>::run(o);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (k == 8) {   // o * (-i) forward, (+i) backward: folded into the adds
+            v[k] = FWD ? cadd_i<false>(e[k], o[k]) : cadd_i<true>(e[k], o[k]);
+            v[k + 16] = FWD ? cadd_i<true>(e[k], o[k]) : cadd_i<false>(e[k], o[k]);
+        } else {
+            float2 t = o[k];
+            if (k != 0) {
+                const float c = cos32(k), sn = cos32(k - 8);   // sin(2 pi k / 32)
+                t = cmul(o[k], make_float2(c, FWD ? -sn : sn));
+            }
+            v[k] = cadd(e[k], t);
+            v[k + 16] = csub(e[k], t);
+        }
+    }
+}
+
+// a * conj(w) in two packed instructions (cmul's sequence with the signs of w.y flipped)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 w) {
+    const vf2_t A = pk(a), W = pk(w);
+    vf2_t t, r;
+    // t = a.yy * (w.y, w.x); r = a.xx * (w.x, -w.y) + t = (a.x w.x + a.y w.y, a.y w.x - a.x w.y)
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(A), "v"(W));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(A), "v"(W), "v"(t));
+    return upk(r);
+}
+
+constexpr int R32_ROW = 33;                   // padded row of the 32 x 32 transpose (float2)
+constexpr int R32_BUF = 32 * R32_ROW;         // one transform's exchange buffer (float2)
+
+// register r of every lane -> row r, column `col`; then row `row` -> registers
+__device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int lane32) {
+    float2* w = buf + lane32;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) w[R32_ROW * r] = v[r];
+    xsync<64>();
+    const unsigned q = (unsigned)(uintptr_t)(buf + R32_ROW * lane32);
+    static_for<0, 32>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        v[r] = lds_rd64<8 * r>(q);
+    });
+    lds_rd_done<32>(v);
+    xsync<64>();   // the next transpose's writes must stay behind these reads
+}
+
+
+// v[r] *= W_1024^(m r) (FWD) or its conjugate, r = 1..31, from an LDS table
+// laid out [r][m] (atw: byte address of entry [0][m]); eight ds_read_b64 at a time
+template <bool FWD>
+__device__ __forceinline__ void r32_twiddle(float2* v, unsigned atw) {
+    static_for<0, 4>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        float2 w[8];
+        static_for<0, 8>([&](auto kc) {
+            constexpr int r = 8 * g + decltype(kc)::value;
+            if constexpr (r > 0) w[r - 8 * g] = lds_rd64<256 * r>(atw);
+        });
+        lds_rd_done<8>(w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = 8 * g + k;
+            if (r > 0) v[r] = FWD ? cmul(v[r], w[k]) : cmulc(v[r], w[k]);
+        }
+    });
+}
+
 // NOX: timing ablation only (scripts/membench.hip) -- the passes without their
 // exchanges, i.e. a wrong transform with the FFT's arithmetic but no LDS traffic.
 // C64: N = 1024 one-wave transforms exchange through pass_exchange_c1024.

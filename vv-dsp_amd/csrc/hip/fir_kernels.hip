@@ -551,79 +551,6 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // EXP (timing ablations, scripts/stftlab.hip; the library uses 0): bit 1 no
 // FFT, bit 2 no stores, bit 3 no loads.
 // ------------------------------------------------------------------------
-__device__ __forceinline__ constexpr float cos32(int m) {
-    constexpr float c1 = 0.98078528040323044913f, c2 = 0.92387953251128675613f, c3 = 0.83146961230254523708f,
-                    c4 = 0.70710678118654752440f, c5 = 0.55557023301960222474f, c6 = 0.38268343236508977173f,
-                    c7 = 0.19509032201612826785f;
-    switch (m & 31) {
-        case 0: return 1.0f;  case 1: return c1;  case 2: return c2;  case 3: return c3;
-        case 4: return c4;    case 5: return c5;  case 6: return c6;  case 7: return c7;
-        case 8: return 0.0f;  case 9: return -c7; case 10: return -c6; case 11: return -c5;
-        case 12: return -c4;  case 13: return -c3; case 14: return -c2; case 15: return -c1;
-        case 16: return -1.0f; case 17: return -c1; case 18: return -c2; case 19: return -c3;
-        case 20: return -c4;  case 21: return -c5; case 22: return -c6; case 23: return -c7;
-        case 24: return 0.0f; case 25: return c7;  case 26: return c6;  case 27: return c5;
-        case 28: return c4;   case 29: return c3;  case 30: return c2;  default: return c1;
-    }
-}
-
-// In-register DFT of length 32 (natural order in and out): two DFT_16 of the
-// even and odd points, combined with W_32^k (exact rotations at k = 0, 8).
-template <bool FWD>
-__device__ __forceinline__ void dft32(float2* v) {
-    float2 e[16], o[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        e[i] = v[2 * i];
-        o[i] = v[2 * i + 1];
-    }
-    Dft<16, FWD>::run(e);
-    Dft<16, FWD>::run(o);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (k == 8) {   // o * (-i) forward, (+i) backward: folded into the adds
-            v[k] = FWD ? cadd_i<false>(e[k], o[k]) : cadd_i<true>(e[k], o[k]);
-            v[k + 16] = FWD ? cadd_i<true>(e[k], o[k]) : cadd_i<false>(e[k], o[k]);
-        } else {
-            float2 t = o[k];
-            if (k != 0) {
-                const float c = cos32(k), sn = cos32(k - 8);   // sin(2 pi k / 32)
-                t = cmul(o[k], make_float2(c, FWD ? -sn : sn));
-            }
-            v[k] = cadd(e[k], t);
-            v[k + 16] = csub(e[k], t);
-        }
-    }
-}
-
-// a * conj(w) in two packed instructions (cmul's sequence with the signs of w.y flipped)
-__device__ __forceinline__ float2 cmulc(float2 a, float2 w) {
-    const vf2_t A = pk(a), W = pk(w);
-    vf2_t t, r;
-    // t = a.yy * (w.y, w.x); r = a.xx * (w.x, -w.y) + t = (a.x w.x + a.y w.y, a.y w.x - a.x w.y)
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(A), "v"(W));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(A), "v"(W), "v"(t));
-    return upk(r);
-}
-
-constexpr int R32_ROW = 33;                   // padded row of the 32 x 32 transpose (float2)
-constexpr int R32_BUF = 32 * R32_ROW;         // one transform's exchange buffer (float2)
-
-// register r of every lane -> row r, column `col`; then row `row` -> registers
-__device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int lane32) {
-    float2* w = buf + lane32;
-#pragma unroll
-    for (int r = 0; r < 32; ++r) w[R32_ROW * r] = v[r];
-    xsync<64>();
-    const unsigned q = (unsigned)(uintptr_t)(buf + R32_ROW * lane32);
-    static_for<0, 32>([&](auto rc) {
-        constexpr int r = decltype(rc)::value;
-        v[r] = lds_rd64<8 * r>(q);
-    });
-    lds_rd_done<32>(v);
-    xsync<64>();   // the next transpose's writes must stay behind these reads
-}
-
 template <int EXP = 0>
 __global__ void __launch_bounds__(256, 2)
 k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
@@ -641,23 +568,6 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     const unsigned ahl = (unsigned)(uintptr_t)(lH + m);               // + 256 k2: H[m + 32 k2], k2 < 16
     const unsigned ahh = (unsigned)(uintptr_t)(lH + 32 - m);          // + 256 (31 - k2): H[1024 - m - 32 k2]
     __syncthreads();
-    // v[r] *= W_1024^(m r) (FWD) or its conjugate, r = 1..31, twiddles read 8 at a time
-    auto twiddle = [&](float2* v, auto fwd) {
-        static_for<0, 4>([&](auto gc) {
-            constexpr int g = decltype(gc)::value;
-            float2 w[8];
-            static_for<0, 8>([&](auto kc) {
-                constexpr int r = 8 * g + decltype(kc)::value;
-                if constexpr (r > 0) w[r - 8 * g] = lds_rd64<256 * r>(atw);
-            });
-            lds_rd_done<8>(w);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int r = 8 * g + k;
-                if (r > 0) v[r] = decltype(fwd)::value ? cmul(v[r], w[k]) : cmulc(v[r], w[k]);
-            }
-        });
-    };
     const long long pairs = nch * ppc, couples = (pairs + 1) / 2;
     long long it, it_end, it_step;
     xcd_walk(couples, F, slot, &it, &it_end, &it_step);
@@ -732,7 +642,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         if constexpr (!(EXP & 2)) {
             // forward: DFT over m1, twiddle, transpose, DFT over m2 -> X[m + 32 k2] in v[k2]
             dft32<true>(v);
-            twiddle(v, std::true_type{});
+            r32_twiddle<true>(v, atw);
             r32_transpose(v, buf, m);
             dft32<true>(v);
             // times H: bin f = m + 32 k2 (H[f] for f < 512, conj H[1024 - f] above), 8 reads at a time
@@ -753,7 +663,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             });
             // inverse: IDFT over k2, conj twiddle, transpose, IDFT over k1 -> y[m + 32 b] in v[b]
             dft32<false>(v);
-            twiddle(v, std::false_type{});
+            r32_twiddle<false>(v, atw);
             r32_transpose(v, buf, m);
             dft32<false>(v);
         }
