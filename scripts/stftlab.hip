@@ -4,6 +4,7 @@
 // library's k_stft_pair<1024, 0, 0, EXP>; EXP bits (stft_kernels.hip): 1 FFT
 // without LDS exchanges, 2 no FFT, 4 no row stores, 8 no span loads,
 // 16 rows as 16 B/lane stores (garbage values), 32 plain instead of streaming stores.
+#include "../vv-dsp_amd/csrc/hip/debug.hip"
 #include "../vv-dsp_amd/csrc/hip/tables.hip"
 #include "../vv-dsp_amd/csrc/hip/stft_kernels.hip"
 #include "../vv-dsp_amd/csrc/hip/fir_kernels.hip"

@@ -205,9 +205,14 @@ def test_czt_fused_equals_unfused(vdev, knob, n, m):
         knob("CZT_UNFUSED", "0")
         a = plan(x)
         knob("CZT_UNFUSED", "1")
+        knob("C2C_R32", "0")   # the chain's P = 1024 FFTs as 16 x 16 x 4, the fused kernel's split
         b = plan(x)
+        knob("C2C_R32", "")
+        c = plan(x)            # the chain with the library's default 1024-point kernel (32 x 32)
+        knob("CZT_UNFUSED", "")
         torch.cuda.synchronize()
         assert torch.equal(a, b)
+        assert _normwise(c.cpu().numpy(), a.cpu().numpy()) <= 2e-6
 
 
 @pytest.mark.parametrize("n", [2, 16, 256, 1024, 4096])

@@ -13,7 +13,10 @@ import vvdsp_amd as vv
 pytestmark = pytest.mark.gpu
 
 NCH = 7
-N = 7 * 60 * 48000 + 333   # 78,749 frames per channel (1 + (n - 1024 + 256) // 256): odd, zero-padded tail
+# 78,749 frames per channel (1 + (n - 1024 + 256) // 256): odd, zero-padded tail;
+# n a multiple of 4, so the channels are 16 B aligned: the LDS-DMA kernels and
+# their dynamic walks (with an odd stride every launch is the register-load VAR 1/2)
+N = 7 * 60 * 48000 + 336
 
 
 @pytest.fixture(scope="module")
@@ -38,8 +41,10 @@ def test_dynamic_walk_equals_chunked(job):
     out = torch.full_like(ref, -1.0)
     for _ in range(3):   # the counters are reset by each launch's last waves
         out.fill_(-1.0)
+        d0 = vv.debug_get("STAT_STFT_DYN")
         st.spectrogram(sig, out=out)
         torch.cuda.synchronize()
+        assert vv.debug_get("STAT_STFT_DYN") - d0 == 1   # the dynamic walk ran
         assert torch.equal(out, ref)
 
 
@@ -156,7 +161,7 @@ def test_dynamic_walks_under_graph_capture(job, vdev, orc):
     sig, st, ref = job
     h = orc.fir_design_lowpass(257, 0.25, 2)
     plan = vdev.FirPlan(torch.from_numpy(h))
-    x = torch.rand(6, 9_000_001, device="cuda") * 2 - 1
+    x = torch.rand(6, 9_000_004, device="cuda") * 2 - 1   # aligned channels: the bulk kernel's dynamic walk
     with vv.knobs(FIR_R32=0):
         yref = plan(x).clone()
     out, y = torch.empty_like(ref), torch.empty_like(x)

@@ -30,9 +30,11 @@ def _walks(fn):
     return vv.debug_get("STAT_FIR_DYN") - d0, vv.debug_get("STAT_FIR_STATIC") - s0
 
 
-# (nch, n, dynamic walk expected): >= 8 pairs per wave slot of the 256-CU x 16-wave grid
-@pytest.mark.parametrize("nch,n,dyn", [(8, 1 << 24, True), (6, 9_000_001, True), (3, 5_000_001, False),
-                                       (1, 777_777, False), (5, 1537, False)])
+# (nch, n, dynamic walk expected): >= 8 pairs per wave slot of the 256-CU x 16-wave
+# grid; n a multiple of 4 (16 B aligned channels: the bulk kernel; other strides
+# run every pair through the bounds-checked k_fir_pair)
+@pytest.mark.parametrize("nch,n,dyn", [(8, 1 << 24, True), (6, 9_000_004, True), (3, 5_000_004, False),
+                                       (1, 777_780, False), (5, 1540, False)])
 def test_fir_dynamic_walk_equals_static(vdev, orc, nch, n, dyn):
     import torch
     h = orc.fir_design_lowpass(257, 0.25, 2)

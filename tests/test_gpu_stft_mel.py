@@ -38,9 +38,10 @@ def test_stft_mel_equals_two_step(vdev, nfft, hop, sr, n_mels, n_coeffs, nch, n,
     f0, s0 = vv.debug_get("STAT_MEL_FUSED"), vv.debug_get("STAT_MEL_SPLIT")
     got = mf.from_signal(st, sig, log_mel=log_mel)
     torch.cuda.synchronize()
-    # the path that ran (vv_dsp_amd.h: one kernel for nfft 1024, hop <= 256, and
+    # the path that ran (vv_dsp_amd.h: one kernel for nfft 1024, hop <= 256 and a
+    # multiple of 4, a 16 B aligned signal with a channel stride of 4k floats, and
     # for MFCC at most 60 mel bands; otherwise the two launches)
-    fused = nfft == 1024 and hop <= 256 and (log_mel or n_mels <= 60)
+    fused = nfft == 1024 and hop <= 256 and hop % 4 == 0 and n % 4 == 0 and (log_mel or n_mels <= 60)
     assert (vv.debug_get("STAT_MEL_FUSED") - f0, vv.debug_get("STAT_MEL_SPLIT") - s0) == \
         ((1, 0) if fused else (0, 1))
     assert got.shape == ref.shape

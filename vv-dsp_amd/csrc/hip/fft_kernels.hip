@@ -92,7 +92,7 @@ k_c2c_r32(const float2* in, float2* out, long long batch, long long in_dist, lon
     for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & 1023];
     const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
     float2* buf = xch + (2 * slot + half) * R32_BUF;
-    const unsigned atw = (unsigned)(uintptr_t)(ltw + m);
+    const float2* atw = ltw + m;
     __syncthreads();
     const long long couples = (batch + 1) / 2, stride = (long long)gridDim.x * F;
     long long cp = uni<64>((long long)blockIdx.x * F + slot);

@@ -564,9 +564,9 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
     const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
     float2* buf = xch + (2 * slot + half) * R32_BUF;
-    const unsigned atw = (unsigned)(uintptr_t)(ltw + m);              // + 256 r: W_1024^(m r)
-    const unsigned ahl = (unsigned)(uintptr_t)(lH + m);               // + 256 k2: H[m + 32 k2], k2 < 16
-    const unsigned ahh = (unsigned)(uintptr_t)(lH + 32 - m);          // + 256 (31 - k2): H[1024 - m - 32 k2]
+    const float2* atw = ltw + m;        // + 32 r: W_1024^(m r)
+    const float2* ahl = lH + m;         // + 32 k2: H[m + 32 k2], k2 < 16
+    const float2* ahh = lH + 32 - m;    // + 32 (31 - k2): H[1024 - m - 32 k2]
     __syncthreads();
     const long long pairs = nch * ppc, couples = (pairs + 1) / 2;
     long long it, it_end, it_step;
@@ -645,22 +645,16 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             r32_twiddle<true>(v, atw);
             r32_transpose(v, buf, m);
             dft32<true>(v);
-            // times H: bin f = m + 32 k2 (H[f] for f < 512, conj H[1024 - f] above), 8 reads at a time
-            static_for<0, 4>([&](auto gc) {
-                constexpr int g = decltype(gc)::value;
-                float2 h[8];
-                static_for<0, 8>([&](auto kc) {
-                    constexpr int k2 = 8 * g + decltype(kc)::value;
-                    if constexpr (k2 < 16) h[k2 - 8 * g] = lds_rd64<256 * k2>(ahl);
-                    else h[k2 - 8 * g] = lds_rd64<256 * (31 - k2)>(ahh);
-                });
-                lds_rd_done<8>(h);
+            // times H: bin f = m + 32 k2 (H[f] for f < 512, conj H[1024 - f] above)
+            {
+                float2 h[16];
+                lds_rd64x16<0, 256>(ahl, h);   // H[m + 32 k2], k2 < 16
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int k2 = 8 * g + k;
-                    v[k2] = k2 < 16 ? cmul(v[k2], h[k]) : cmulc(v[k2], h[k]);
-                }
-            });
+                for (int k2 = 0; k2 < 16; ++k2) v[k2] = cmul(v[k2], h[k2]);
+                lds_rd64x16<15 * 256, -256>(ahh, h);   // h[i] = H[1024 - m - 32 (16 + i)]
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[16 + i] = cmulc(v[16 + i], h[i]);
+            }
             // inverse: IDFT over k2, conj twiddle, transpose, IDFT over k1 -> y[m + 32 b] in v[b]
             dft32<false>(v);
             r32_twiddle<false>(v, atw);

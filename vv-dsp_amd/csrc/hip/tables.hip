@@ -159,6 +159,7 @@ unsigned* stream_counters(hipStream_t s) {
     if (capturing) {
         if (p.used >= CTR_POOL_BLOCKS) return nullptr;
         unsigned* b = p.base + (size_t)p.used * STFT_CTR_WORDS;
+        (void)hipGetLastError();   // a stale error must not read as this launch's
         hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, b, (int)STFT_CTR_WORDS);
         if (hipGetLastError() != hipSuccess) return nullptr;
         ++p.used;
