@@ -158,9 +158,10 @@ def fir_roofline(reps=50):
             "achieved_GBs": round(byts / (avg * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
             "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "samples_per_s": round(nch * n / (avg * 1e-3), 1),
-            "kernel": "vvh::k_fir_bulk_reg<1024, 256> (every pair of every channel in one launch: persistent grid, "
-                      "dynamic band walk, the edge pairs bounds-checked in the same loop), one step",
-            **dict(zip(("traffic", "traffic_source"), kernel_traffic(["vvh::k_fir_bulk_reg<1024", "vvh::k_fir_pair<1024"])))}
+            "kernel": "vvh::k_fir_r32<0> (1024-point blocks as 32 x 32 on half-waves: one LDS transpose per FFT; "
+                      "two blocks per complex FFT, two pairs per wave, every pair of every channel in one persistent "
+                      "launch, the edge pairs bounds-checked in the same loop), one step",
+            **dict(zip(("traffic", "traffic_source"), kernel_traffic(["vvh::k_fir_r32"])))}
 
 
 def host_cpu_share():

@@ -20,6 +20,6 @@ for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_V
 done
 BOX="$(rocm-smi --showproductname 2>/dev/null | grep -m1 -o 'MI3[0-9A-Z]*' || echo MI355X)"
 python3 scripts/pmc_summary.py $O --json $O/bench_pmc.json --channels 256 --box "$BOX, $(date -u +%F)" \
-  --tail vvh::k_stft_pair=20 --tail vvh::k_c2c=50 --tail vvh::k_fir=50 > $O/summary.txt
+  --tail vvh::k_stft_pair=20 --tail vvh::k_c2c=50 --tail vvh::k_fir_r32=50 > $O/summary.txt
 find $O/trace -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
 head -40 $O/summary.txt

@@ -476,8 +476,8 @@ CASES = {
     "blue48000unf": with_env(lambda: case_c2c(48000, 1024), "VVHIP_BLUE_UNFUSED", "1"),
     "blue48000old": with_env(lambda: case_c2c(48000, 1024), "VVHIP_FS_OLD", "1"),
     "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),
-    "c2c1024r16": with_env(lambda: case_c2c(1024, 65536), "VVHIP_C2C_R32", "0"),
-    "c2c1024br16": with_env(lambda: case_c2c(1024, 65536, fwd=False), "VVHIP_C2C_R32", "0"),
+    "c2c1024r32": with_env(lambda: case_c2c(1024, 65536), "VVHIP_C2C_R32", "1"),
+    "c2c1024br32": with_env(lambda: case_c2c(1024, 65536, fwd=False), "VVHIP_C2C_R32", "1"),
     **{f"c2cr32lab{e}": (lambda e=e: case_c2clab(e, fn="c2cr32lab_run")) for e in (0, 2)},
     # mixed-radix (7-smooth non-power-of-two) lengths; *nomix: the f64 DFT kernel / Bluestein
     **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
@@ -522,7 +522,7 @@ CASES = {
     **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2, 4, 6)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
-                                                                          256, 258, 266)},
+                                                                          256, 258, 266, 512, 768, 1536, 1792)},
     **{f"lab60_{e}": (lambda e=e: case_lab(e, nch=1, seconds=60)) for e in (0, 2, 4, 6, 8, 10, 14, 32782, 65550, 98318)},
     **{f"empty{g}": (lambda g=g: case_empty(g)) for g in (703, 2048)},
     **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
@@ -571,7 +571,7 @@ CASES = {
     "firstatic": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_DYN", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "firr16": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_R32", "0"),
-    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12)},
+    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 16, 32, 64, 128, 96, 192, 18, 34)},
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),
     "logmelold": with_env(lambda: case_mel(0), "VVHIP_MEL_OLD", "1"),

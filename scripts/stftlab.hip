@@ -93,9 +93,12 @@ static hipError_t lab_firr32(const float2* H, const float* x, float* y, long lon
     static std::atomic<int> cap;
     const int capv = cached_grid(cap, (const void*)k_fir_r32<EXP>, 256, 0, 1LL << 40);
     const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
-    const int grid = (int)(need < capv ? need : capv);
+    int grid = (int)(need < capv ? need : capv);
+    if (EXP & 16) grid = (int)((couples + 31) / 32);   // chunks of 8 couples per wave
+    if (EXP & 32) grid = capv / 8 * 8;
+    unsigned* ctr = (EXP & 32) ? stream_counters(s) : nullptr;
     hipLaunchKernelGGL((k_fir_r32<EXP>), dim3(grid), dim3(256), 0, s, H, x, y, nch, n, n, ppc, twiddle_table(N), n,
-                       (const float*)nullptr, le, qf, ql);
+                       (const float*)nullptr, le, qf, ql, ctr);
     return hipGetLastError();
 }
 template <int EXP>
@@ -172,7 +175,7 @@ extern "C" int firr32lab_run(int exp, const void* H, const float* x, float* y, l
     const float2* h = (const float2*)H;
     switch (exp) {
 #define C(E) case E: return (int)vvh::lab_firr32<E>(h, x, y, n, nch, s);
-        C(0) C(2) C(4) C(6) C(8) C(10) C(12)
+        C(0) C(2) C(4) C(6) C(8) C(10) C(12) C(16) C(32) C(64) C(128) C(96) C(192) C(18) C(34)
 #undef C
         default: return -1;
     }

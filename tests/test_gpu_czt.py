@@ -205,10 +205,10 @@ def test_czt_fused_equals_unfused(vdev, knob, n, m):
         knob("CZT_UNFUSED", "0")
         a = plan(x)
         knob("CZT_UNFUSED", "1")
-        knob("C2C_R32", "0")   # the chain's P = 1024 FFTs as 16 x 16 x 4, the fused kernel's split
-        b = plan(x)
+        b = plan(x)            # the chain's P = 1024 FFTs as 16 x 16 x 4, the fused kernel's split
+        knob("C2C_R32", 1)
+        c = plan(x)            # the chain with the 32 x 32 kernel: the same values up to rounding
         knob("C2C_R32", "")
-        c = plan(x)            # the chain with the library's default 1024-point kernel (32 x 32)
         knob("CZT_UNFUSED", "")
         torch.cuda.synchronize()
         assert torch.equal(a, b)

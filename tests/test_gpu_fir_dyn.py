@@ -34,7 +34,7 @@ def _walks(fn):
 # grid; n a multiple of 4 (16 B aligned channels: the bulk kernel; other strides
 # run every pair through the bounds-checked k_fir_pair)
 @pytest.mark.parametrize("nch,n,dyn", [(8, 1 << 24, True), (6, 9_000_004, True), (3, 5_000_004, False),
-                                       (1, 777_780, False), (5, 1540, False)])
+                                       (1, 777_780, False), (5, 1540, None)])
 def test_fir_dynamic_walk_equals_static(vdev, orc, nch, n, dyn):
     import torch
     h = orc.fir_design_lowpass(257, 0.25, 2)
@@ -47,7 +47,8 @@ def test_fir_dynamic_walk_equals_static(vdev, orc, nch, n, dyn):
         with vv.knobs(FIR_R32=0):
             walks = _walks(lambda: got.append(plan(x)))
         torch.cuda.synchronize()
-        assert walks == ((1, 0) if dyn else (0, 1)), walks
+        # dyn None: every pair is an edge pair (k_fir_pair alone, neither bulk walk)
+        assert walks == ((0, 0) if dyn is None else (1, 0) if dyn else (0, 1)), walks
         assert torch.equal(got[0], ref)
 
 

@@ -78,7 +78,8 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
 // lane-contiguous 8 B loads), DFT_32 over m1 in registers, twiddle W_1024^(m2 k1),
 // ONE LDS transpose, DFT_32 over m2 -> X[k1 + 32 k2] in register k2 of lane k1
 // (lane-contiguous stores).  One exchange per transform instead of k_c2c's two
-// (each 8 KB through the LDS write path).  Two transforms per wave, the next
+// (each 8 KB through the LDS write path).  Kept as the A/B alternative (knob
+// C2C_R32 = 1): it measured slower than k_c2c.  Two transforms per wave, the next
 // couple's 64 points prefetched into registers: two waves per SIMD, 2 x 72 KB
 // of LDS per CU.  EXP (scripts/stftlab.hip only): bit 1 no FFT.
 // ------------------------------------------------------------------------
@@ -137,8 +138,12 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     const float2* pas = pass_twiddles(N);
     if (!tab || !pas) return hipErrorOutOfMemory;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
-    if constexpr (N == 1024) {   // the 32 x 32 split (k_c2c_r32); knob C2C_R32 = 0: k_c2c (A/B)
-        if (knob(KNOB_C2C_R32, 1) != 0) {
+    if constexpr (N == 1024) {
+        // the 32 x 32 split (k_c2c_r32) on knob C2C_R32 = 1 only: same buffers, k_c2c
+        // 0.1878 / 0.1847 ms (fwd / bwd) against 0.1943 / 0.1953 -- the FFT hides under
+        // k_c2c's memory pattern (0.1796 ms without it) and k_c2c_r32's own pattern is
+        // slower at two waves per SIMD (0.1945 ms) (profiles/r04_kbench_r32.jsonl)
+        if (knob(KNOB_C2C_R32, 0) != 0) {
             static std::atomic<int> capr;
             const int cap = cached_grid(capr, (const void*)k_c2c_r32<FWD>, 256, 0, 1LL << 40);
             const long long need = ((batch + 1) / 2 + 3) / 4;

@@ -549,14 +549,18 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // Edge pairs (span before sample 0 or past n) load through the prefix / zero
 // rule and store predicated, in the same loop (a wave-uniform branch).
 // EXP (timing ablations, scripts/stftlab.hip; the library uses 0): bit 1 no
-// FFT, bit 2 no stores, bit 3 no loads.
+// FFT, bit 2 no stores, bit 3 no loads; walks: bit 4 non-persistent chunks of 8
+// couples per wave (the launcher sizes the grid), bit 5 the dynamic band walk
+// of k_fir_bulk_reg (counters in `ctrs`); bit 6 plain output stores, bit 7
+// plain block-a loads.
 // ------------------------------------------------------------------------
 template <int EXP = 0>
 __global__ void __launch_bounds__(256, 2)
 k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
           long long ppc, const float2* tw1024, long long n, const float* prefix, long long lm1, long long qf,
-          long long ql) {
+          long long ql, unsigned* ctrs) {
     constexpr int N = 1024, LE = 256, LOUT = N - LE, F = 4;
+    constexpr bool DYN = (EXP & 32) != 0;
     __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R32_BUF];
     __shared__ float2 lH[N / 2 + 1];
     __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r) (row 0 unused)
@@ -570,11 +574,29 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     __syncthreads();
     const long long pairs = nch * ppc, couples = (pairs + 1) / 2;
     long long it, it_end, it_step;
-    xcd_walk(couples, F, slot, &it, &it_end, &it_step);
-    it = uni<64>(it);
-    it_end = uni<64>(it_end);
-    it_step = uni<64>(it_step);
-    if (it >= it_end) return;
+    // DYN: counter value k of stream s (= XCD group, slot) is couple
+    // (k / 64) * 8 F 64 + s * 64 + k % 64: the chip sweeps one moving band
+    const int stream = __builtin_amdgcn_readfirstlane((int)(blockIdx.x & 7) * F + slot);
+    unsigned* const ctr = DYN ? ctrs + 32 * stream : nullptr;
+    auto band_item = [&](unsigned k) -> long long {
+        return (long long)(k >> 6) * (8 * F * 64) + (long long)stream * 64 + (long long)(k & 63);
+    };
+    unsigned rk = 0;   // lane 0: the counter value of the couple after `it`
+    if constexpr (DYN) {
+        unsigned r0 = 0;
+        if (lane == 0) r0 = atomicAdd(ctr, 1u);
+        it = band_item(__builtin_amdgcn_readfirstlane(r0));
+        it_end = couples;
+        it_step = 0;
+        if (it < it_end && lane == 0) rk = atomicAdd(ctr, 1u);
+    } else {
+        if constexpr (EXP & 16) work_walk(couples, F, slot, 8 * F, &it, &it_end, &it_step);
+        else xcd_walk(couples, F, slot, &it, &it_end, &it_step);
+        it = uni<64>(it);
+        it_end = uni<64>(it_end);
+        it_step = uni<64>(it_step);
+    }
+    if (it < it_end) {
     // couple k: pairs 2k (lanes 0..31) and 2k+1 (lanes 32..63); a missing
     // second pair (odd total) computes pair 2k again and stores nothing
     auto locate = [&](long long k, long long* c, long long* j, bool* valid, bool* edge_any) {
@@ -593,7 +615,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         const float* a = x + c * x_stride + j * LOUT - LE + m;
         const float* b = a + LOUT;
 #pragma unroll
-        for (int r = 0; r < 32; ++r) xa[r] = __builtin_nontemporal_load(a + 32 * r);
+        for (int r = 0; r < 32; ++r) xa[r] = (EXP & 128) ? a[32 * r] : __builtin_nontemporal_load(a + 32 * r);
 #pragma unroll
         for (int r = 0; r < 32; ++r) xb[r] = b[32 * r];   // overlaps the next pair's block a: cached
     };
@@ -628,11 +650,15 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     locate(it, &c, &j, &valid, &edge);
     if (!edge) load_bulk(c, j);
     for (; it < it_end; it += it_step) {
+        if constexpr (DYN) it_step = band_item(__builtin_amdgcn_readfirstlane(rk)) - it;
         if (edge) load_edge(c, j);   // at the top of its own iteration (a bulk couple was prefetched)
         float2 v[32];
 #pragma unroll
         for (int r = 0; r < 32; ++r) v[r] = make_float2(xa[r], xb[r]);
         const long long itn = it + it_step;
+        if constexpr (DYN) {
+            if (itn < it_end && lane == 0) rk = atomicAdd(ctr, 1u);   // -> the couple after itn
+        }
         long long cn = c, jn = j;
         bool validn = valid, edgen = edge;
         if (itn < it_end) {   // the next couple's loads, in flight across this one's transforms
@@ -665,10 +691,17 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             float* ya = y + c * y_stride + j * LOUT - LE + m;   // + 32 b: block j's output (b >= 8)
             if (!edge) {
                 if (valid) {
+                    if constexpr (EXP & 64) {
 #pragma unroll
-                    for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].x, ya + 32 * b);
+                        for (int b = 8; b < 32; ++b) ya[32 * b] = v[b].x;
 #pragma unroll
-                    for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].y, ya + LOUT + 32 * b);
+                        for (int b = 8; b < 32; ++b) ya[LOUT + 32 * b] = v[b].y;
+                    } else {
+#pragma unroll
+                        for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].x, ya + 32 * b);
+#pragma unroll
+                        for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].y, ya + LOUT + 32 * b);
+                    }
                 }
             } else if (valid) {   // outputs past n are not stored
                 const long long rem = n - (j * LOUT - LE + m);
@@ -684,6 +717,16 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         j = jn;
         valid = validn;
         edge = edgen;
+    }
+    }
+    if constexpr (DYN) {   // the XCD group's last wave out resets its counters for the next launch
+        if (lane == 0) {
+            const unsigned nw = (unsigned)((gridDim.x - (blockIdx.x & 7) + 7) / 8);
+            if (atomicAdd(ctr + 16, 1u) == nw - 1) {
+                atomicExch(ctr, 0u);
+                atomicExch(ctr + 16, 0u);
+            }
+        }
     }
 }
 
@@ -751,7 +794,7 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
             if (grid < 1) return hipSuccess;
             stat_inc(STAT_FIR_R32);
             hipLaunchKernelGGL((k_fir_r32<0>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, ppc,
-                               t1024, n, prefix, lm1, qf, ql);
+                               t1024, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
             return hipGetLastError();
         }
     }
