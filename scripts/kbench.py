@@ -476,15 +476,11 @@ CASES = {
     "blue48000unf": with_env(lambda: case_c2c(48000, 1024), "VVHIP_BLUE_UNFUSED", "1"),
     "blue48000old": with_env(lambda: case_c2c(48000, 1024), "VVHIP_FS_OLD", "1"),
     "c2c1024b": lambda: case_c2c(1024, 65536, fwd=False),
-    "c2c1024r32": with_env(lambda: case_c2c(1024, 65536), "VVHIP_C2C_R32", "1"),
-    "c2c1024br32": with_env(lambda: case_c2c(1024, 65536, fwd=False), "VVHIP_C2C_R32", "1"),
     **{f"c2cr32lab{e}": (lambda e=e: case_c2clab(e, fn="c2cr32lab_run")) for e in (0, 2)},
     # mixed-radix (7-smooth non-power-of-two) lengths; *nomix: the f64 DFT kernel / Bluestein
     **{f"mix{n}": (lambda n=n: case_c2c(n, (1 << 26) // n)) for n in (400, 480, 1000, 2000, 3000, 4000)},
     **{f"mix{n}nomix": with_env(lambda n=n: case_c2c(n, (1 << 22) // n), "VVHIP_NO_MIXED", "1") for n in (400, 3000)},
     "stft400": lambda: case_stft_n(32, 600, 400, 160),
-    "stftp256half": with_env(lambda: case_stft_n(8, 600, 256, 64, sr=48000), "VVHIP_STFT_HALF", "1"),
-    "stftp4096half": with_env(lambda: case_stft_n(8, 600, 4096, 1024, sr=48000), "VVHIP_STFT_HALF", "1"),
     "stftp128": lambda: case_stft_n(8, 600, 128, 32, sr=48000),
     "stftp256": lambda: case_stft_n(8, 600, 256, 64, sr=48000),
     "stftp512": lambda: case_stft_n(8, 600, 512, 128, sr=48000),
@@ -567,15 +563,12 @@ CASES = {
     "firdirectlds": with_env(lambda: case_fir_direct(8, 1 << 24), "VVHIP_FIR_DIRECT_LDS", "1"),
     "filtfilt": lambda: case_fir_direct(8, 1 << 24, filtfilt=True),
     "filtfiltlds": with_env(lambda: case_fir_direct(8, 1 << 24, filtfilt=True), "VVHIP_FIR_DIRECT_LDS", "1"),
-    "firspan": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_REG", "0"),
     "firstatic": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_DYN", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "firr16": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_R32", "0"),
-    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 16, 32, 64, 128, 96, 192, 18, 34)},
+    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 16, 32, 64, 128, 96, 192, 18, 34, 256, 258, 288, 290)},
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),
-    "logmelold": with_env(lambda: case_mel(0), "VVHIP_MEL_OLD", "1"),
-    "mfccold": with_env(lambda: case_mel(1), "VVHIP_MEL_OLD", "1"),
     "ola": lambda: case_ola(),
     "olaold": with_env(lambda: case_ola(), "VVHIP_ISTFT_OLD", "1"),
     "dct1024": lambda: case_dct(1024, 131072),

@@ -12,6 +12,31 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vv-dsp_amd"))
 import vvdsp_amd as vv  # noqa: E402
 
+if sys.argv[1] == "firr32":   # python scripts/labcheck.py firr32 <EXP>: k_fir_r32 variant vs EXP 0 (every output)
+    e = int(sys.argv[2])
+    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
+    lib.firr32lab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_longlong, ctypes.c_longlong, ctypes.c_void_p]
+    worst = 0.0
+    for nch, n in ((3, (1 << 20) + 12346), (1, 768 * 6), (2, 700), (5, 1540), (7, 768 * 41 + 2)):
+        x = torch.rand(nch, n, device="cuda") * 2 - 1
+        H = torch.complex(torch.rand(1024, device="cuda"), torch.rand(1024, device="cuda"))
+        s = torch.cuda.current_stream().cuda_stream
+        ref = torch.full_like(x, -2.0)
+        assert lib.firr32lab_run(0, H.data_ptr(), x.data_ptr(), ref.data_ptr(), n, nch, s) == 0
+        for rep in range(2):
+            out = torch.full_like(x, -1.0)
+            assert lib.firr32lab_run(e, H.data_ptr(), x.data_ptr(), out.data_ptr(), n, nch, s) == 0
+            torch.cuda.synchronize()
+            ne = out != ref
+            bad = ne.sum().item()
+            d = (out - ref).abs().max().item()
+            worst = max(worst, d / ref.abs().max().item())
+            print(f"firr32lab{e} ({nch} x {n}) launch {rep}: {bad} of {out.numel()} values differ, max |diff| {d:.3g} "
+                  f"(max |y| {ref.abs().max().item():.3g}), first at {ne.nonzero()[:5].tolist()}")
+    assert worst <= 1e-5, worst
+    sys.exit(0)
+
 if sys.argv[1] == "fir":   # python scripts/labcheck.py fir <EXP>: k_fir_bulk_reg variant vs EXP 0
     e = int(sys.argv[2])
     lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))

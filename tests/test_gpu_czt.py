@@ -206,13 +206,9 @@ def test_czt_fused_equals_unfused(vdev, knob, n, m):
         a = plan(x)
         knob("CZT_UNFUSED", "1")
         b = plan(x)            # the chain's P = 1024 FFTs as 16 x 16 x 4, the fused kernel's split
-        knob("C2C_R32", 1)
-        c = plan(x)            # the chain with the 32 x 32 kernel: the same values up to rounding
-        knob("C2C_R32", "")
         knob("CZT_UNFUSED", "")
         torch.cuda.synchronize()
         assert torch.equal(a, b)
-        assert _normwise(c.cpu().numpy(), a.cpu().numpy()) <= 2e-6
 
 
 @pytest.mark.parametrize("n", [2, 16, 256, 1024, 4096])

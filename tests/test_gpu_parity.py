@@ -981,28 +981,3 @@ def test_device_wrappers_check_shapes(vdev):
                        torch.zeros(100, device="cuda"))
     with pytest.raises(vdev.VvError):
         st.spectrogram(torch.zeros(2, 4096, device="cuda"), out=torch.zeros(2, 3, 1024, device="cuda"))
-
-
-@pytest.mark.parametrize("batch", [1, 2, 7, 4099])
-def test_c2c_1024_r32_vs_previous(vdev, knob, batch):
-    """k_c2c_r32 (1024 = 32 x 32 on half-waves, knob C2C_R32 = 1) against NumPy
-    f64 at the harness tolerance and against the default 16 x 16 x 4 kernel
-    within 2x that bound: odd batches (a wave's second half idle), both
-    directions, and in place."""
-    import torch
-    rng = np.random.default_rng(batch)
-    x = (rng.random((batch, 1024)) - 0.5 + 1j * (rng.random((batch, 1024)) - 0.5)).astype(np.complex64)
-    xd = torch.from_numpy(x).cuda()
-    r, a = tolerances()
-    for d in (vdev.FWD, vdev.BWD):
-        plan = vdev.FftPlan(1024, vdev.C2C, d, batch=batch)
-        knob("C2C_R32", 1)
-        y = plan(xd).cpu().numpy()
-        ref = (np.fft.fft if d == vdev.FWD else np.fft.ifft)(x.astype(np.complex128), axis=1)
-        np.testing.assert_allclose(y, ref, rtol=r, atol=a)
-        xi = xd.clone()
-        plan(xi, out=xi)
-        assert np.array_equal(xi.cpu().numpy(), y)
-        knob("C2C_R32", "")
-        yo = plan(xd).cpu().numpy()
-        np.testing.assert_allclose(y, yo, rtol=2 * r, atol=2 * a)

@@ -24,11 +24,11 @@ namespace vvh {
 namespace {
 // knob names without the VVHIP_ prefix, in enum Knob order
 constexpr const char* KNOB_NAMES[KNOB_COUNT] = {
-    "STFT_CPS",   "STFT_RUN",     "STFT_DBS",      "POW_OLD",     "STFT_RING",   "STFT_DYN",        "STFT_HALF",
-    "FS_VAR",     "FS_CHUNK_MB",  "FS_OLD",        "BLUE_UNFUSED", "C2C_MAX",    "STFT_SQ",         "MIX_VAR",
-    "MIX_CHUNK_MB", "MIX_R2C_FULL", "FIR_OLD",     "FIR_REG",     "FIR_DYN",     "FIR_DIRECT_LDS",  "FIR_BLOCK",
-    "HOST_CHUNK_MB", "NO_MIXED",  "REAL_PROMOTE",  "ISTFT_OLD",   "MEL_OLD",     "MEL_FUSED",       "CZT_UNFUSED",
-    "CEPS_UNFUSED", "FIR_R32", "DIST_SLAB_KB", "C2C_R32",
+    "STFT_CPS",      "STFT_RUN",     "STFT_DBS",     "POW_OLD",     "STFT_RING",   "STFT_DYN",
+    "FS_VAR",        "FS_CHUNK_MB",  "FS_OLD",       "BLUE_UNFUSED", "C2C_MAX",    "STFT_SQ",     "MIX_VAR",
+    "MIX_CHUNK_MB",  "MIX_R2C_FULL", "FIR_OLD",      "FIR_DYN",     "FIR_DIRECT_LDS", "FIR_BLOCK",
+    "HOST_CHUNK_MB", "NO_MIXED",     "REAL_PROMOTE", "ISTFT_OLD",   "MEL_FUSED",   "CZT_UNFUSED",
+    "CEPS_UNFUSED",  "FIR_R32",      "DIST_SLAB_KB",
 };
 constexpr const char* STAT_NAMES[STAT_COUNT] = {
     "STAT_STFT_DYN", "STAT_FIR_DYN", "STAT_FIR_STATIC", "STAT_MEL_FUSED", "STAT_MEL_SPLIT", "STAT_FIR_R32",

@@ -769,13 +769,28 @@ constexpr int R32_ROW = 33;                   // padded row of the 32 x 32 trans
 constexpr int R32_BUF = 32 * R32_ROW;         // one transform's exchange buffer (float2)
 
 // register r of every lane -> row r, column `col`; then row `row` -> registers
-__device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int lane32) {
-    float2* w = buf + lane32;
+// (col = row = the lane's index in its half for the plain split)
+__device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int col, int row) {
+    float2* w = buf + col;
 #pragma unroll
     for (int r = 0; r < 32; ++r) w[R32_ROW * r] = v[r];
     xsync<64>();
-    lds_rd64x32(buf + R32_ROW * lane32, v);
+    lds_rd64x32(buf + R32_ROW * row, v);
     xsync<64>();   // the next transpose's writes must stay behind these reads
+}
+__device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int lane32) { r32_transpose(v, buf, lane32, lane32); }
+
+// Lanes l and l + 16 of each half-wave trade a <-> b (v_permlane16_swap: rows
+// 1 and 3 of `a` with rows 0 and 2 of `b`): afterwards lane l < 16 holds (its a,
+// lane l+16's a) and lane l + 16 (lane l's b, its b).  Two dwords loaded as one
+// 8 B pair per lane (samples 2l, 2l+1 of 64) become samples 2l, 2l + 32 in lane
+// l < 16 and 2l + 1, 2l + 33 in lane l + 16: the r32 layout (one residue mod 32
+// per lane) with residue 2 (l & 15) + (l >> 4).  The same swap turns two r32
+// registers (rows b, b + 1 of that residue layout) back into 8 B pairs.
+__device__ __forceinline__ void r32_pairswap(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
 }
 
 

@@ -72,65 +72,6 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
     }
 }
 
-// ------------------------------------------------------------------------
-// k_c2c_r32: 1024-point C2C with the transform split 32 x 32 on half a wave
-// (fft_core.hpp dft32 / r32_transpose): lane m2 loads x[32 m1 + m2] (m1 = 0..31,
-// lane-contiguous 8 B loads), DFT_32 over m1 in registers, twiddle W_1024^(m2 k1),
-// ONE LDS transpose, DFT_32 over m2 -> X[k1 + 32 k2] in register k2 of lane k1
-// (lane-contiguous stores).  One exchange per transform instead of k_c2c's two
-// (each 8 KB through the LDS write path).  Kept as the A/B alternative (knob
-// C2C_R32 = 1): it measured slower than k_c2c.  Two transforms per wave, the next
-// couple's 64 points prefetched into registers: two waves per SIMD, 2 x 72 KB
-// of LDS per CU.  EXP (scripts/stftlab.hip only): bit 1 no FFT.
-// ------------------------------------------------------------------------
-template <bool FWD, int EXP = 0>
-__global__ void __launch_bounds__(256, 2)
-k_c2c_r32(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
-          const float2* tw1024, float scale) {
-    constexpr int F = 4;
-    __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R32_BUF];
-    __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r)
-    for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & 1023];
-    const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
-    float2* buf = xch + (2 * slot + half) * R32_BUF;
-    const float2* atw = ltw + m;
-    __syncthreads();
-    const long long couples = (batch + 1) / 2, stride = (long long)gridDim.x * F;
-    long long cp = uni<64>((long long)blockIdx.x * F + slot);
-    // transform of this half in couple k (a missing second transform recomputes the first, stores nothing)
-    auto tf = [&](long long k) { return 2 * k + half < batch ? 2 * k + half : 2 * k; };
-    float2 nx[32];
-    if (cp < couples) {
-        const float2* src = in + tf(cp) * in_dist + m;
-#pragma unroll
-        for (int r = 0; r < 32; ++r) nx[r] = ld_nt(src + 32 * r);
-    }
-    for (; cp < couples; cp += stride) {
-        float2 v[32];
-#pragma unroll
-        for (int r = 0; r < 32; ++r) v[r] = nx[r];
-        const long long f = tf(cp);
-        const bool valid = 2 * cp + half < batch;
-        const long long cn = cp + stride;
-        if (cn < couples) {
-            const float2* src = in + tf(cn) * in_dist + m;
-#pragma unroll
-            for (int r = 0; r < 32; ++r) nx[r] = ld_nt(src + 32 * r);
-        }
-        if constexpr (!(EXP & 2)) {
-            dft32<FWD>(v);
-            r32_twiddle<FWD>(v, atw);
-            r32_transpose(v, buf, m);
-            dft32<FWD>(v);
-        }
-        if (valid) {
-            float2* dst = out + f * out_dist + m;
-#pragma unroll
-            for (int k2 = 0; k2 < 32; ++k2) st_nt(FWD ? v[k2] : cscale(v[k2], scale), dst + 32 * k2);
-        }
-    }
-}
-
 template <int N, bool FWD>
 static hipError_t run_c2c(const float2* in, float2* out, long long batch, long long in_dist,
                           long long out_dist, float scale, hipStream_t s) {
@@ -138,22 +79,6 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     const float2* pas = pass_twiddles(N);
     if (!tab || !pas) return hipErrorOutOfMemory;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
-    if constexpr (N == 1024) {
-        // the 32 x 32 split (k_c2c_r32) on knob C2C_R32 = 1 only: same buffers, k_c2c
-        // 0.1878 / 0.1847 ms (fwd / bwd) against 0.1943 / 0.1953 -- the FFT hides under
-        // k_c2c's memory pattern (0.1796 ms without it) and k_c2c_r32's own pattern is
-        // slower at two waves per SIMD (0.1945 ms) (profiles/r04_kbench_r32.jsonl)
-        if (knob(KNOB_C2C_R32, 0) != 0) {
-            static std::atomic<int> capr;
-            const int cap = cached_grid(capr, (const void*)k_c2c_r32<FWD>, 256, 0, 1LL << 40);
-            const long long need = ((batch + 1) / 2 + 3) / 4;
-            const int grid = (int)(need < cap ? need : cap);
-            if (grid < 1) return hipSuccess;
-            hipLaunchKernelGGL((k_c2c_r32<FWD>), dim3(grid), dim3(256), 0, s, in, out, batch, in_dist, out_dist, tab,
-                               scale);
-            return hipGetLastError();
-        }
-    }
     static std::atomic<int> capc;
     const int grid_cap = cached_grid(capc, (const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;

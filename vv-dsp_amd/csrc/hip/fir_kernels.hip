@@ -191,131 +191,10 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
 }
 
 // ------------------------------------------------------------------------
-// k_fir_bulk<N, LQ>: the bulk pairs at three workgroups per CU (12 waves)
-// instead of two.  LDS per workgroup of four transforms: the FFT exchange
-// through the half-size real/imaginary buffer (pass_exchange_ri, conflict-free
-// for N = 1024), H for bins 0..N/2 only (h is real, so H[N-k] = conj H[k]),
-// the last pass' twiddles in registers (a thread's last-pass butterflies are
-// the same for every pair: j = t + T*i) and only the earlier passes' table in
-// LDS -- 52 KB instead of 80 KB.
-// LQ (le == N/4, e.g. taps <= N/4 + 1): the outputs below le are exactly the
-// registers q with q % RL == 0, so those stores are dropped at compile time
-// (no sink stores: 3/4 of the store instructions of the general variant).
-// ------------------------------------------------------------------------
-// EXP: timing ablations for scripts/stftlab.hip only (the library instantiates
-// EXP = 0): bit 0 FFTs without their LDS exchanges, bit 1 no FFTs, bit 2 no
-// output stores, bit 3 no span loads.  Results are wrong under any of them.
-template <int N, bool LQ, int EXP = 0>
-__global__ void __launch_bounds__(256, 3)   // 3 waves per SIMD: the LDS allows 3 workgroups per CU
-k_fir_bulk(long long le, const float2* Hg, const float* x, float* y, long long nch, long long x_stride,
-           long long y_stride, long long cnt, long long q0, const float2* gpass, float* sink) {
-    using G = Geo<N>;
-    static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
-    constexpr int F = 4, RL = G::RL;
-    constexpr int SPAN = N + (3 * N) / 4;
-    constexpr int NST = (EXP & 4) ? 0 : LQ ? 2 * (G::P - G::P / RL) : 2 * G::P;   // stores per pair
-    constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
-    constexpr int XW = ri_floats<N>();   // exchange floats per transform (a multiple of 4)
-    __shared__ __attribute__((aligned(16))) float xch[F * XW];   // 16 B: pass_exchange_ri's b128 writes
-    __shared__ float2 ltab[TWL];
-    __shared__ float2 lH[N / 2 + 1];
-    __shared__ float span_all[F * SPAN];
-    for (int i = threadIdx.x; i < G::tw_off(G::NPASS - 1); i += 256) ltab[i] = gpass[i];
-    for (int i = threadIdx.x; i <= N / 2; i += 256) lH[i] = Hg[i];
-    const int lt = threadIdx.x, slot = lt >> 6, t = lt & 63;
-    TwLastReg<N> tw;
-    tw.tab = ltab;
-    tw.load(gpass, t);
-    __syncthreads();
-    float2* my = reinterpret_cast<float2*>(xch + slot * XW);
-    float* span = span_all + slot * SPAN;
-    const long long lout = N - le;
-    long long p, p_end, p_step;
-    xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
-    p = uni<64>(p);
-    p_end = uni<64>(p_end);
-    p_step = uni<64>(p_step);
-    if (p >= p_end) return;
-    auto locate = [&](long long it, long long* cc, long long* jj) {
-        *cc = it / cnt;
-        *jj = 2 * (q0 + (it - *cc * cnt));
-    };
-    long long c, j;
-    locate(p, &c, &j);
-    float* snk = sink + ((((long long)blockIdx.x * F + slot) * 64) % SINK_FLOATS) + t;
-    auto issue_span = [&](long long cc, long long jj) {
-        if constexpr (EXP & 8) return;
-        const float* s0 = x + cc * x_stride + jj * lout - le;
-        const int len = (int)(N + lout);
-#pragma unroll
-        for (int u = 0; u < SPAN / 256; ++u) {
-            const int e = u * 256 + t * 4;
-            glds16(s0 + (e < len ? e : 0), span + u * 256);
-        }
-    };
-    issue_span(c, j);
-    vm_wait<0>();
-    for (; p < p_end; p += p_step) {
-        const bool more = p + p_step < p_end;
-        long long cn = c, jn = j;
-        if (more) locate(p + p_step, &cn, &jn);
-        vm_wait<NST>();   // this pair's span; the previous pair's stores may still fly
-        float2 v[G::P];
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) v[r] = make_float2(span[t + r * 64], span[lout + t + r * 64]);
-        lgkm_wait0();
-        if (more) issue_span(cn, jn);
-        tw.opaque();
-        if constexpr (!(EXP & 2)) fft_regs<N, true, false, true, TwLastReg<N>, (EXP & 1) != 0>(v, t, my, tw);
-        float2 u[G::P];
-#pragma unroll
-        for (int q = 0; q < G::P; ++q) {
-            const int m = q / RL + G::NPT * (q % RL);   // out_pos<N>(t, q) = t + 64*m
-            if (m < G::P / 2) u[m] = cmul(v[q], lH[t + 64 * m]);
-            else u[m] = cmul(v[q], cconj(lH[N - t - 64 * m]));
-        }
-        tw.opaque();
-        if constexpr (!(EXP & 2)) fft_regs<N, false, false, true, TwLastReg<N>, (EXP & 1) != 0>(u, t, my, tw);
-        float* ya = y + c * y_stride + j * lout - le;   // + e: block j output (e >= le)
-        if constexpr (LQ) {
-            // le = N/4, lout = 3N/4: register q (q % RL != 0) holds outputs
-            // e = t + 64 m of both blocks, m = out_pos' slot; streaming dword
-            // stores at the wave-uniform row base + 4t + immediate (block b's
-            // from a second base 4 KB on, the immediate is 13-bit)
-            const unsigned lo = 4u * (unsigned)t;
-            const float* yb = ya + 1024;
-            if constexpr (EXP & 4) {
-#pragma unroll
-                for (int q = 0; q < G::P; ++q) asm volatile("" ::"v"(u[q].x), "v"(u[q].y));
-            }
-            static_for<0, G::P>([&](auto qc) {
-                constexpr int q = decltype(qc)::value;
-                constexpr int m = q / RL + G::NPT * (q % RL);
-                if constexpr ((EXP & 4) == 0 && q % RL != 0) {
-                    st4_nt_sbase<256 * m>(lo, u[q].x, ya);
-                    st4_nt_sbase<256 * m + 4 * (3 * N / 4) - 4096>(lo, u[q].y, yb);
-                }
-            });
-        } else {
-#pragma unroll
-        for (int q = 0; q < G::P; ++q) {
-            const long long e = out_pos<N>(t, q);
-            {
-                const bool ok = e >= le;
-                st4_counted(ok ? ya + e : snk, u[q].x);
-                st4_counted(ok ? ya + e + lout : snk, u[q].y);
-            }
-        }
-        }
-        c = cn;
-        j = jn;
-    }
-}
-
-// ------------------------------------------------------------------------
-// k_fir_bulk_reg<N>: k_fir_bulk's LQ case with the pair's two blocks loaded
-// straight into registers (coalesced dword loads, the LE overlap re-read from
-// L1/L2) instead of an LDS span.  Without the 28 KB of spans a workgroup needs
+// k_fir_bulk_reg<N>: the bulk pairs (le == N/4) with the pair's two blocks
+// loaded straight into registers (coalesced dword loads, the LE overlap re-read
+// from L1/L2) instead of round 2's LDS span (k_fir_bulk, now in
+// scripts/stftlab.hip only).  Without the 28 KB of spans a workgroup needs
 // 24 KB of LDS, so four workgroups fit per CU (16 waves instead of 12): the
 // kernel is latency-bound on its LDS exchanges (scripts/kbench.py firlab*).
 // The next pair's loads are issued after the inverse FFT, ahead of this
@@ -552,7 +431,14 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // FFT, bit 2 no stores, bit 3 no loads; walks: bit 4 non-persistent chunks of 8
 // couples per wave (the launcher sizes the grid), bit 5 the dynamic band walk
 // of k_fir_bulk_reg (counters in `ctrs`); bit 6 plain output stores, bit 7
-// plain block-a loads.
+// plain block-a loads; bit 8 PAIRED (below).
+// PAIRED: bulk samples move as 8 B per lane -- a block's 1024 inputs as 16
+// dwordx2 loads (rows 0..7 of block b are rows 24..31 of block a: 12 more), its
+// 768 outputs as 12 dwordx2 stores -- each pair of dwords re-laid by one
+// v_permlane16_swap (r32_pairswap): lane l of a half works on residue
+// 2 (l & 15) + (l >> 4) instead of l, which only moves its forward-twiddle column
+// and the rows the transposes use.  Needs 8 B aligned channels (x, y and
+// their strides even).
 // ------------------------------------------------------------------------
 template <int EXP = 0>
 __global__ void __launch_bounds__(256, 2)
@@ -561,6 +447,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
           long long ql, unsigned* ctrs) {
     constexpr int N = 1024, LE = 256, LOUT = N - LE, F = 4;
     constexpr bool DYN = (EXP & 32) != 0;
+    constexpr bool PAIRED = (EXP & 256) != 0;
     __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R32_BUF];
     __shared__ float2 lH[N / 2 + 1];
     __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r) (row 0 unused)
@@ -568,7 +455,10 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
     const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
     float2* buf = xch + (2 * slot + half) * R32_BUF;
-    const float2* atw = ltw + m;        // + 32 r: W_1024^(m r)
+    // the lane's residue: input / output samples 32 r + mr in register r
+    const int mr = PAIRED ? 2 * (m & 15) + (m >> 4) : m;
+    const float2* atwf = ltw + mr;      // + 32 r: W_1024^(mr r), forward (lane = input residue)
+    const float2* atw = ltw + m;        // + 32 r: W_1024^(m r), inverse (lane = bin residue)
     const float2* ahl = lH + m;         // + 32 k2: H[m + 32 k2], k2 < 16
     const float2* ahh = lH + 32 - m;    // + 32 (31 - k2): H[1024 - m - 32 k2]
     __syncthreads();
@@ -612,12 +502,30 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     float xa[32], xb[32];
     auto load_bulk = [&](long long c, long long j) {
         if constexpr (EXP & 8) return;
-        const float* a = x + c * x_stride + j * LOUT - LE + m;
-        const float* b = a + LOUT;
+        if constexpr (PAIRED) {
+            // 8 B pairs (samples 64 i + 2m, +1), swapped into the residue layout at use
+            const float2* a = reinterpret_cast<const float2*>(x + c * x_stride + j * LOUT - LE) + m;
+            const float2* b = a + LOUT / 2;
 #pragma unroll
-        for (int r = 0; r < 32; ++r) xa[r] = (EXP & 128) ? a[32 * r] : __builtin_nontemporal_load(a + 32 * r);
+            for (int i = 0; i < 16; ++i) {
+                const float2 u = ld_nt(a + 32 * i);
+                xa[2 * i] = u.x;
+                xa[2 * i + 1] = u.y;
+            }
 #pragma unroll
-        for (int r = 0; r < 32; ++r) xb[r] = b[32 * r];   // overlaps the next pair's block a: cached
+            for (int i = 4; i < 16; ++i) {   // rows 0..7 of block b = rows 24..31 of block a
+                const float2 u = b[32 * i];    // overlaps the next pair's block a: cached
+                xb[2 * i] = u.x;
+                xb[2 * i + 1] = u.y;
+            }
+        } else {
+            const float* a = x + c * x_stride + j * LOUT - LE + m;
+            const float* b = a + LOUT;
+#pragma unroll
+            for (int r = 0; r < 32; ++r) xa[r] = (EXP & 128) ? a[32 * r] : __builtin_nontemporal_load(a + 32 * r);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) xb[r] = b[32 * r];   // overlaps the next pair's block a: cached
+        }
     };
     // edge couples: staged through the (idle) exchange buffer with rolled loops
     // (the prefix / zero rule per sample), then read back -- no register
@@ -640,9 +548,9 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         }
         xsync<64>();
 #pragma unroll
-        for (int r = 0; r < 32; ++r) xa[r] = sf[m + 32 * r];
+        for (int r = 0; r < 32; ++r) xa[r] = sf[mr + 32 * r];
 #pragma unroll
-        for (int r = 0; r < 32; ++r) xb[r] = sf[N + m + 32 * r];
+        for (int r = 0; r < 32; ++r) xb[r] = sf[N + mr + 32 * r];
         xsync<64>();
     };
     long long c, j;
@@ -651,7 +559,16 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     if (!edge) load_bulk(c, j);
     for (; it < it_end; it += it_step) {
         if constexpr (DYN) it_step = band_item(__builtin_amdgcn_readfirstlane(rk)) - it;
-        if (edge) load_edge(c, j);   // at the top of its own iteration (a bulk couple was prefetched)
+        if (edge) {
+            load_edge(c, j);   // at the top of its own iteration (a bulk couple was prefetched)
+        } else if constexpr (PAIRED) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) r32_pairswap(xa[2 * i], xa[2 * i + 1]);
+#pragma unroll
+            for (int i = 4; i < 16; ++i) r32_pairswap(xb[2 * i], xb[2 * i + 1]);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) xb[r] = xa[24 + r];
+        }
         float2 v[32];
 #pragma unroll
         for (int r = 0; r < 32; ++r) v[r] = make_float2(xa[r], xb[r]);
@@ -668,8 +585,8 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         if constexpr (!(EXP & 2)) {
             // forward: DFT over m1, twiddle, transpose, DFT over m2 -> X[m + 32 k2] in v[k2]
             dft32<true>(v);
-            r32_twiddle<true>(v, atw);
-            r32_transpose(v, buf, m);
+            r32_twiddle<true>(v, atwf);
+            r32_transpose(v, buf, mr, m);
             dft32<true>(v);
             // times H: bin f = m + 32 k2 (H[f] for f < 512, conj H[1024 - f] above)
             {
@@ -684,13 +601,28 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             // inverse: IDFT over k2, conj twiddle, transpose, IDFT over k1 -> y[m + 32 b] in v[b]
             dft32<false>(v);
             r32_twiddle<false>(v, atw);
-            r32_transpose(v, buf, m);
+            r32_transpose(v, buf, m, mr);
             dft32<false>(v);
         }
         if constexpr (!(EXP & 4)) {
-            float* ya = y + c * y_stride + j * LOUT - LE + m;   // + 32 b: block j's output (b >= 8)
+            float* ya = y + c * y_stride + j * LOUT - LE + mr;   // + 32 b: block j's output (b >= 8)
             if (!edge) {
-                if (valid) {
+                if constexpr (PAIRED) {
+                    // rows b, b + 1 -> 8 B pairs: lane l < 16 stores samples 32 b + 2l, +1,
+                    // lane l + 16 samples 32 (b + 1) + 2l, +1
+#pragma unroll
+                    for (int b = 8; b < 32; b += 2) {
+                        r32_pairswap(v[b].x, v[b + 1].x);
+                        r32_pairswap(v[b].y, v[b + 1].y);
+                    }
+                    float2* yp = reinterpret_cast<float2*>(y + c * y_stride + j * LOUT - LE) + (m & 15) + 16 * (m >> 4);
+                    if (valid) {
+#pragma unroll
+                        for (int b = 8; b < 32; b += 2) st_nt(make_float2(v[b].x, v[b + 1].x), yp + 16 * b);
+#pragma unroll
+                        for (int b = 8; b < 32; b += 2) st_nt(make_float2(v[b].y, v[b + 1].y), yp + LOUT / 2 + 16 * b);
+                    }
+                } else if (valid) {
                     if constexpr (EXP & 64) {
 #pragma unroll
                         for (int b = 8; b < 32; ++b) ya[32 * b] = v[b].x;
@@ -704,7 +636,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
                     }
                 }
             } else if (valid) {   // outputs past n are not stored
-                const long long rem = n - (j * LOUT - LE + m);
+                const long long rem = n - (j * LOUT - LE + mr);
                 const int rm = (int)(rem < (1 << 30) ? rem : (1 << 30));
 #pragma unroll
                 for (int b = 8; b < 32; ++b) {
@@ -770,10 +702,9 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
     // below (2q+2)*lout without bounds checks: verify the range on the host
     if (ql > qf && (2 * qf * lout < le || 2 * ql * lout > n || N + lout > N + (3 * N) / 4))
         return hipErrorInvalidValue;
-    static std::atomic<int> capc_b, capc_e, capc_v2;
+    static std::atomic<int> capc_b, capc_e;
     const bool old = knob(KNOB_FIR_OLD, 0) == 1;   // A/B knob (scripts/kbench.py)
     // le == N/4 holds for every filter fir_block gives N = 1024 (taps <= 257)
-    const bool reg = knob(KNOB_FIR_REG, 1) != 0;   // A/B knob: 0 = LDS-span k_fir_bulk
     if constexpr (N == 1024) {
         // the 32 x 32 transform split (k_fir_r32): one LDS transpose per FFT instead
         // of two; every pair, edges included, in one launch.  Knob FIR_R32 = 0: the
@@ -798,7 +729,7 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
             return hipGetLastError();
         }
     }
-    if (ql > qf && le == N / 4 && !old && reg) {
+    if (ql > qf && le == N / 4 && !old) {
         // every pair of every channel in one launch: the edge pairs [0, qf) and
         // [ql, ppc) take the kernel's bounds-checked branch (round 2 ran them as a
         // second, latency-bound launch: 11 us of config 4's 237)
@@ -828,14 +759,6 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
                                0LL, pN, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
         }
         return hipGetLastError();
-    } else if (ql > qf && le == N / 4 && !old) {
-        if constexpr (FIR_BULK<N>) {
-            const int cap_v2 = cached_grid(capc_v2, (const void*)k_fir_bulk<N, true>, 256, 0, 1LL << 40);
-            const long long cnt = ql - qf, need = (nch * cnt + 3) / 4;
-            const int grid = (int)(need < cap_v2 ? need : cap_v2);
-            hipLaunchKernelGGL((k_fir_bulk<N, true>), dim3(grid), dim3(256), 0, s, le, H, x, y, nch, x_stride,
-                               y_stride, cnt, qf, pN, sink);
-        }
     } else if (ql > qf) {
         if constexpr (FIR_BULK<N>) {
             const int cap_b = cached_grid(capc_b, (const void*)k_fir_pair<N, true>, WG, 0, 1LL << 40);

@@ -1317,7 +1317,6 @@ struct vvhip_mel {
     int n_mels = 0, nbins = 0, n_coeffs = 0, nnz = 0;
     float eps = 0.0f;
     float* W = nullptr;     // non-zero weight ranges of every filter, packed
-    int* meta = nullptr;    // per filter: lo, len, offset into W
     int* chunks = nullptr;  // balanced chunk schedule of the filters (mel_chunk_schedule)
     int* cbeg = nullptr;    // first chunk of each filter, [n_mels + 1]
     int nc = 0;
@@ -1337,7 +1336,6 @@ void vvhip_mel_destroy(vvhip_mel* m) {
         (void)hipStreamDestroy(m->stream);
     }
     if (m->W) (void)hipFree(m->W);
-    if (m->meta) (void)hipFree(m->meta);
     if (m->chunks) (void)hipFree(m->chunks);
     if (m->cbeg) (void)hipFree(m->cbeg);
     if (m->D) (void)hipFree(m->D);
@@ -1360,7 +1358,7 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
     m->n_coeffs = (int)n_coeffs;
     m->eps = eps;
     std::vector<float> w;
-    std::vector<int> meta(3 * n_mels, 0);
+    std::vector<int> meta(3 * n_mels, 0);   // per filter: lo, len, offset into W (host: the chunk schedule)
     if (fb) {
         for (size_t f = 0; f < n_mels; ++f) {
             const float* r = fb + f * nbins;
@@ -1388,9 +1386,7 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
     if (lifter > 0.0f)
         for (size_t i = 1; i < n_coeffs; ++i)
             L[i] = 1.0f + (lifter / 2.0f) * sinf((float)M_PI * (float)i / lifter);
-    bool ok = hipMalloc(&m->meta, sizeof(int) * meta.size()) == hipSuccess &&
-              hipMemcpy(m->meta, meta.data(), sizeof(int) * meta.size(), hipMemcpyHostToDevice) == hipSuccess &&
-              hipMalloc(&m->chunks, sizeof(int) * (chunks.size() + 1)) == hipSuccess &&
+    bool ok = hipMalloc(&m->chunks, sizeof(int) * (chunks.size() + 1)) == hipSuccess &&
               (chunks.empty() ||
                hipMemcpy(m->chunks, chunks.data(), sizeof(int) * chunks.size(), hipMemcpyHostToDevice) == hipSuccess) &&
               hipMalloc(&m->cbeg, sizeof(int) * cbeg.size()) == hipSuccess &&
@@ -1417,14 +1413,9 @@ int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_ou
     if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
     if ((kind != 2 && m->nbins == 0) || (kind != 0 && m->n_coeffs == 0)) return fail(ST_RANGE, "mel plan lacks tables");
     if (frames == 0) return ST_OK;
-    if (knob(KNOB_MEL_OLD, 0) == 1)   // A/B knob (scripts/kbench.py): one wave per frame
-        HIPCHK(launch_mel(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->meta, m->nnz,
-                          m->D, m->lift, m->eps, d_out, (hipStream_t)stream),
-               ST_INTERNAL);
-    else
-        HIPCHK(launch_mel_grp(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->nnz,
-                              m->chunks, m->nc, m->cbeg, m->D, m->lift, m->eps, d_out, (hipStream_t)stream),
-               ST_INTERNAL);
+    HIPCHK(launch_mel_grp(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->nnz, m->chunks,
+                          m->nc, m->cbeg, m->D, m->lift, m->eps, d_out, (hipStream_t)stream),
+           ST_INTERNAL);
     return ST_OK;
 }
 

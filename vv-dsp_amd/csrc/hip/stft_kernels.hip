@@ -12,8 +12,8 @@
 // come straight from registers -- no split twiddles, no LDS post pass -- and
 // every bin 0..N-1 of both rows is produced in place (Hermitian symmetry is
 // automatic).  Used when Geo<N>::CAN_PAIR.
-// k_stft_half<M>: one frame per M = nfft/2 point complex FFT plus the real
-// split step (nfft = 256 and 4096, where N cannot be mirror-paired).
+// k_stft_pair_lds<N>: the same frame pairs where the last pass cannot be
+// mirror-paired (nfft = 256 and 4096): the mirror bins are read back through LDS.
 //
 // Scheduling: the bulk variant (VAR 0) is launched non-persistently, one
 // workgroup per 16 consecutive frame pairs per transform slot, the slots of a
@@ -1038,120 +1038,10 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
     }
 }
 
-template <int M, int MODE>
-__global__ void __launch_bounds__(Wg<M>::value)
-k_stft_half(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
-            long long hop, const float* win, void* out, long long out_ch_stride, const float2* gpass,
-            const float2* gtabM, const float2* gtab2M) {
-    using G = Geo<M>;
-    constexpr bool PAIR = G::CAN_PAIR;
-    constexpr int WG = Wg<M>::value, F = Wg<M>::F;
-    constexpr int NR = 2 * M;
-    __shared__ float2 lds[F * G::LDS];
-    __shared__ float2 ltab[TwLayout<M>::ENTRIES];
-    __shared__ float2 lpost[PostLayout<M>::ENTRIES];
-    stage_twiddles<M, WG>(ltab, gpass, gtabM);
-    stage_post<M, WG>(lpost, gtab2M);
-    __syncthreads();
-    const TwTab<M> tw{ltab};
-    const PostTab<M> pw{lpost};
-    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
-    float2* my = lds + slot * G::LDS;
-    float2 w[G::P];
-#pragma unroll
-    for (int r = 0; r < G::P; ++r) w[r] = make_float2(win[2 * (t + r * G::T)], win[2 * (t + r * G::T) + 1]);
-    const long long items = nch * frames;
-    long long it, it_end, it_step;
-    xcd_walk(items, F, slot, &it, &it_end, &it_step);
-    it = uni<G::T>(it);
-    it_end = uni<G::T>(it_end);
-    it_step = uni<G::T>(it_step);
-    float2 nx[G::P];
-    auto load = [&](long long i2) {
-        const long long c = i2 / frames, fr = i2 - c * frames;
-        const float* s = sig + c * ch_stride;
-        const long long start = fr * hop;
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) {
-            const long long e = start + 2 * (t + r * G::T);
-            nx[r] = make_float2(e < n ? s[e] : 0.0f, e + 1 < n ? s[e + 1] : 0.0f);
-        }
-    };
-    if (it < it_end) load(it);
-    for (; it < it_end; it += it_step) {
-        const long long c = it / frames, fr = it - c * frames;
-        float2 v[G::P];
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) v[r] = make_float2(nx[r].x * w[r].x, nx[r].y * w[r].y);
-        if (it + it_step < it_end) load(it + it_step);
-        fft_regs<M, true, PAIR>(v, t, my, tw);
-        const long long row = c * out_ch_stride + fr * (long long)(MODE == 2 ? M + 1 : NR);
-        float2 A[G::P], B[G::P];
-        int K[G::P];
-        if constexpr (PAIR) {
-#pragma unroll
-            for (int q = 0; q < G::P; ++q) {
-                K[q] = out_pos<M, true>(t, q);
-                A[q] = v[q];
-                B[q] = mirror_of<M, true>(v, t, q);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<M>(t, q))] = v[q];
-            xsync<G::T>();
-#pragma unroll
-            for (int q = 0; q < G::P; ++q) {
-                K[q] = t + G::T * q;
-                A[q] = my[G::pad(K[q])];
-                B[q] = my[G::pad((M - K[q]) & (M - 1))];
-            }
-            xsync<G::T>();
-        }
-#pragma unroll
-        for (int q = 0; q < G::P; ++q) {
-            const int k = K[q];
-            if (MODE == 0) {
-                float* o = reinterpret_cast<float*>(out) + row;
-                if (k == 0) {
-                    const float x0 = A[q].x + A[q].y, xm = A[q].x - A[q].y;
-                    *(o) = fabsf(x0);
-                    *(o + M) = fabsf(xm);
-                } else {
-                    const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
-                    const float mag = cmag(X.x, X.y);
-                    *(o + k) = mag;
-                    *(o + (NR - k)) = mag;
-                }
-            } else if (MODE == 2) {   // power of bins 0..M
-                float* o = reinterpret_cast<float*>(out) + row;
-                if (k == 0) {
-                    const float x0 = A[q].x + A[q].y, xm = A[q].x - A[q].y;
-                    *(o) = x0 * x0;
-                    *(o + M) = xm * xm;
-                } else {
-                    const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
-                    *(o + k) = __builtin_fmaf(X.x, X.x, X.y * X.y);
-                }
-            } else {
-                float2* o = reinterpret_cast<float2*>(out) + row;
-                if (k == 0) {
-                    *(o) = make_float2(A[q].x + A[q].y, 0.0f);
-                    *(o + M) = make_float2(A[q].x - A[q].y, 0.0f);
-                } else {
-                    const float2 X = split_fwd(A[q], cconj(B[q]), pw(k));
-                    *(o + k) = X;
-                    *(o + (NR - k)) = cconj(X);
-                }
-            }
-        }
-    }
-}
-
 template <int N, int MODE>
 static hipError_t run_stft(const float* sig, long long n, long long nch, long long ch_stride,
                            long long frames, long long hop, const float* win, void* out,
                            long long out_ch_stride, hipStream_t s) {
-    const long long items = nch * frames;
     if constexpr (Geo<N>::CAN_PAIR) {
         const float2* tN = twiddle_table(N);
         const float2* pN = pass_twiddles(N);
@@ -1270,9 +1160,9 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             }
             if (tpc > 0) launch(k_stft_pair<N, MODE, 2>, 2, mpc, tpc);
         }
-    } else if (knob(KNOB_STFT_HALF, 0) != 1) {
-        // frame pairs with the mirror read through LDS (knob STFT_HALF = 1: the
-        // one-frame-per-half-length-FFT kernel below, A/B)
+    } else {
+        // frame pairs with the mirror bins read back through LDS (k_stft_pair_lds;
+        // it replaced round 1's one-frame-per-half-length-FFT kernel, now gone)
         const float2* tN = twiddle_table(N);
         const float2* pN = pass_twiddles(N);
         if (!tN || !pN) return hipErrorOutOfMemory;
@@ -1284,20 +1174,6 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         if (grid < 1) return hipSuccess;
         hipLaunchKernelGGL((k_stft_pair_lds<N, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
                            hop, win, out, out_ch_stride, pN, tN);
-    } else {
-        constexpr int M = N / 2;
-        const float2* tM = twiddle_table(M);
-        const float2* pM = pass_twiddles(M);
-        const float2* t2M = twiddle_table(N);
-        if (!tM || !pM || !t2M) return hipErrorOutOfMemory;
-        constexpr int WG = Wg<M>::value, F = Wg<M>::F;
-        static std::atomic<int> capc1;
-        const int cap = cached_grid(capc1, (const void*)k_stft_half<M, MODE>, WG, 0, 1LL << 40);
-        const long long need = (items + F - 1) / F;
-        const int grid = (int)(need < cap ? need : cap);
-        if (grid < 1) return hipSuccess;
-        hipLaunchKernelGGL((k_stft_half<M, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
-                           hop, win, out, out_ch_stride, pM, tM, t2M);
     }
     return hipGetLastError();
 }

@@ -13,11 +13,11 @@ namespace vvh {
 // Knob values come from vvhip_debug_set (or, with VVHIP_AB=1, from the
 // environment read once per process); knob(k, dflt) returns dflt when unset.
 enum Knob : int {
-    KNOB_STFT_CPS, KNOB_STFT_RUN, KNOB_STFT_DBS, KNOB_POW_OLD, KNOB_STFT_RING, KNOB_STFT_DYN, KNOB_STFT_HALF,
+    KNOB_STFT_CPS, KNOB_STFT_RUN, KNOB_STFT_DBS, KNOB_POW_OLD, KNOB_STFT_RING, KNOB_STFT_DYN,
     KNOB_FS_VAR, KNOB_FS_CHUNK_MB, KNOB_FS_OLD, KNOB_BLUE_UNFUSED, KNOB_C2C_MAX, KNOB_STFT_SQ, KNOB_MIX_VAR,
-    KNOB_MIX_CHUNK_MB, KNOB_MIX_R2C_FULL, KNOB_FIR_OLD, KNOB_FIR_REG, KNOB_FIR_DYN, KNOB_FIR_DIRECT_LDS, KNOB_FIR_BLOCK,
-    KNOB_HOST_CHUNK_MB, KNOB_NO_MIXED, KNOB_REAL_PROMOTE, KNOB_ISTFT_OLD, KNOB_MEL_OLD, KNOB_MEL_FUSED, KNOB_CZT_UNFUSED,
-    KNOB_CEPS_UNFUSED, KNOB_FIR_R32, KNOB_DIST_SLAB_KB, KNOB_C2C_R32,
+    KNOB_MIX_CHUNK_MB, KNOB_MIX_R2C_FULL, KNOB_FIR_OLD, KNOB_FIR_DYN, KNOB_FIR_DIRECT_LDS, KNOB_FIR_BLOCK,
+    KNOB_HOST_CHUNK_MB, KNOB_NO_MIXED, KNOB_REAL_PROMOTE, KNOB_ISTFT_OLD, KNOB_MEL_FUSED, KNOB_CZT_UNFUSED,
+    KNOB_CEPS_UNFUSED, KNOB_FIR_R32, KNOB_DIST_SLAB_KB,
     KNOB_COUNT
 };
 long long knob(Knob k, long long dflt);
@@ -66,9 +66,6 @@ hipError_t launch_promote_real(const float* in, float2* out, long long count, hi
 // ---- mel / MFCC (mel_kernels.hip) ---------------------------------------
 // mode 0: power rows [frames][nbins] -> log-mel [frames][n_mels]
 //      1: power rows -> MFCC [frames][n_coeffs];  2: log-mel rows -> MFCC
-hipError_t launch_mel(int mode, const float* in, long long frames, int nbins, int n_mels, int n_coeffs,
-                      const float* W, const int* meta, int nnz, const float* D, const float* lift, float eps,
-                      float* out, hipStream_t s);
 hipError_t launch_mel_grp(int mode, const float* in, long long frames, int nbins, int n_mels, int n_coeffs,
                           const float* W, int nnz, const int* chunks, int nc, const int* cbeg, const float* D,
                           const float* lift, float eps, float* out, hipStream_t s);
