@@ -266,8 +266,8 @@ static hipError_t lab_firreg(const float2* H, const float* x, float* y, long lon
                        pass_twiddles(N), n, (const float*)nullptr, le, qf, ql, ctr);
     return hipGetLastError();
 }
-// config 4 through k_fir_r32<EXP> (every pair, edges included; EXP bits 2 no
-// FFT, 4 no stores, 8 no loads)
+// config 4 through k_fir_r32<PAIRED, EXP> (every pair, edges included; EXP bits 2 no
+// FFT, 4 no stores, 8 no loads; lab bit 8 = PAIRED)
 template <int EXP>
 static hipError_t lab_firr32(const float2* H, const float* x, float* y, long long n, long long nch, hipStream_t s) {
     constexpr int N = 1024;
@@ -275,13 +275,15 @@ static hipError_t lab_firr32(const float2* H, const float* x, float* y, long lon
     long long qf = (le + 2 * lout - 1) / (2 * lout), ql = n / (2 * lout);
     if (ql > ppc) ql = ppc;
     static std::atomic<int> cap;
-    const int capv = cached_grid(cap, (const void*)k_fir_r32<EXP>, 256, 0, 1LL << 40);
+    constexpr bool PAIRED = (EXP & 256) != 0;   // lab bit 8: the paired 8 B loads / stores
+    constexpr int E = EXP & ~256;
+    const int capv = cached_grid(cap, (const void*)k_fir_r32<PAIRED, E>, 256, 0, 1LL << 40);
     const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
     int grid = (int)(need < capv ? need : capv);
     if (EXP & 16) grid = (int)((couples + 31) / 32);   // chunks of 8 couples per wave
     if (EXP & 32) grid = capv / 8 * 8;
     unsigned* ctr = (EXP & 32) ? stream_counters(s) : nullptr;
-    hipLaunchKernelGGL((k_fir_r32<EXP>), dim3(grid), dim3(256), 0, s, H, x, y, nch, n, n, ppc, twiddle_table(N), n,
+    hipLaunchKernelGGL((k_fir_r32<PAIRED, E>), dim3(grid), dim3(256), 0, s, H, x, y, nch, n, n, ppc, twiddle_table(N), n,
                        (const float*)nullptr, le, qf, ql, ctr);
     return hipGetLastError();
 }

@@ -746,8 +746,11 @@ __device__ __forceinline__ void dft32(float2* v) {
         } else {
             float2 t = o[k];
             if (k != 0) {
-                const float c = cos32(k), sn = cos32(k - 8);   // sin(2 pi k / 32)
-                t = cmul(o[k], make_float2(c, FWD ? -sn : sn));
+                // o * (c, s): cmul's roundings (fma(o.x, c, -o.y s), fma(o.x, s, o.y c)) with
+                // the constants as SGPR operands (cmul's asm would copy them into VGPRs)
+                const float c = cos32(k), sn = FWD ? -cos32(k - 8) : cos32(k - 8);   // -+sin(2 pi k / 32)
+                const vf2_t O = pk(o[k]);
+                t = upk(__builtin_elementwise_fma(O.xx, vf2_t{c, sn}, O.yy * vf2_t{-sn, c}));
             }
             v[k] = cadd(e[k], t);
             v[k + 16] = csub(e[k], t);

@@ -431,8 +431,8 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // FFT, bit 2 no stores, bit 3 no loads; walks: bit 4 non-persistent chunks of 8
 // couples per wave (the launcher sizes the grid), bit 5 the dynamic band walk
 // of k_fir_bulk_reg (counters in `ctrs`); bit 6 plain output stores, bit 7
-// plain block-a loads; bit 8 PAIRED (below).
-// PAIRED: bulk samples move as 8 B per lane -- a block's 1024 inputs as 16
+// plain block-a loads.
+// PAIRED (the launcher's choice for 8 B aligned channels): bulk samples move as 8 B per lane -- a block's 1024 inputs as 16
 // dwordx2 loads (rows 0..7 of block b are rows 24..31 of block a: 12 more), its
 // 768 outputs as 12 dwordx2 stores -- each pair of dwords re-laid by one
 // v_permlane16_swap (r32_pairswap): lane l of a half works on residue
@@ -440,14 +440,13 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // and the rows the transposes use.  Needs 8 B aligned channels (x, y and
 // their strides even).
 // ------------------------------------------------------------------------
-template <int EXP = 0>
+template <bool PAIRED, int EXP = 0>
 __global__ void __launch_bounds__(256, 2)
 k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
           long long ppc, const float2* tw1024, long long n, const float* prefix, long long lm1, long long qf,
           long long ql, unsigned* ctrs) {
     constexpr int N = 1024, LE = 256, LOUT = N - LE, F = 4;
     constexpr bool DYN = (EXP & 32) != 0;
-    constexpr bool PAIRED = (EXP & 256) != 0;
     __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R32_BUF];
     __shared__ float2 lH[N / 2 + 1];
     __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r) (row 0 unused)
@@ -488,17 +487,40 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     }
     if (it < it_end) {
     // couple k: pairs 2k (lanes 0..31) and 2k+1 (lanes 32..63); a missing
-    // second pair (odd total) computes pair 2k again and stores nothing
+    // second pair (odd total) computes pair 2k again and stores nothing.
+    // Pair 2k = (channel c0, pair q0 of it), kept incrementally for the static
+    // walk (one division per wave, not three per couple).
+    long long c0 = 0, q0 = 0, dc = 0, dq = 0;
+    auto seek = [&](long long k) {
+        c0 = (2 * k) / ppc;
+        q0 = 2 * k - c0 * ppc;
+    };
     auto locate = [&](long long k, long long* c, long long* j, bool* valid, bool* edge_any) {
-        const long long p0 = 2 * k, p1 = p0 + 1 < pairs ? p0 + 1 : p0;
-        const long long pm = half ? p1 : p0;
-        *valid = !half || p0 + 1 < pairs;
-        *c = pm / ppc;
-        const long long q = pm - *c * ppc;
-        *j = 2 * q;
-        const long long q0 = p0 % ppc, q1 = p1 % ppc;
+        const bool two = 2 * k + 1 < pairs;
+        const bool wrap = q0 + 1 == ppc;
+        const long long c1 = two ? c0 + (wrap ? 1 : 0) : c0, q1 = two ? (wrap ? 0 : q0 + 1) : q0;
+        *valid = !half || two;
+        *c = half ? c1 : c0;
+        *j = 2 * (half ? q1 : q0);
         *edge_any = q0 < qf || q0 >= ql || q1 < qf || q1 >= ql;
     };
+    auto advance = [&](long long k) {   // (c0, q0) of couple k from those of k - it_step
+        if constexpr (DYN) {
+            seek(k);
+        } else {
+            q0 += dq;
+            c0 += dc;
+            if (q0 >= ppc) {
+                q0 -= ppc;
+                ++c0;
+            }
+        }
+    };
+    if constexpr (!DYN) {
+        dc = (2 * it_step) / ppc;
+        dq = 2 * it_step - dc * ppc;
+    }
+    seek(it);
     float xa[32], xb[32];
     auto load_bulk = [&](long long c, long long j) {
         if constexpr (EXP & 8) return;
@@ -579,6 +601,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         long long cn = c, jn = j;
         bool validn = valid, edgen = edge;
         if (itn < it_end) {   // the next couple's loads, in flight across this one's transforms
+            advance(itn);
             locate(itn, &cn, &jn, &validn, &edgen);
             if (!edgen) load_bulk(cn, jn);
         }
@@ -716,16 +739,23 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
             if (qf32 >= ql32) qf32 = ql32 = ppc;
             qf = qf32;
             ql = ql32;
+            // 8 B pairs (PAIRED) for 8 B aligned channels; dword loads and stores otherwise
+            const bool paired = ((uintptr_t)x & 7) == 0 && ((uintptr_t)y & 7) == 0 && (x_stride & 1) == 0 &&
+                                (y_stride & 1) == 0;
             static std::atomic<int> capc_32;
-            const int cap = cached_grid(capc_32, (const void*)k_fir_r32<0>, 256, 0, 1LL << 40);
+            const int cap = cached_grid(capc_32, (const void*)k_fir_r32<true>, 256, 0, 1LL << 40);
             const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
             const int grid = (int)(need < cap ? need : cap);
             const float2* t1024 = twiddle_table(1024);
             if (!t1024) return hipErrorOutOfMemory;
             if (grid < 1) return hipSuccess;
             stat_inc(STAT_FIR_R32);
-            hipLaunchKernelGGL((k_fir_r32<0>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, ppc,
-                               t1024, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
+            if (paired)
+                hipLaunchKernelGGL((k_fir_r32<true>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride,
+                                   ppc, t1024, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
+            else
+                hipLaunchKernelGGL((k_fir_r32<false>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride,
+                                   ppc, t1024, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
             return hipGetLastError();
         }
     }
