@@ -726,35 +726,42 @@ __device__ __forceinline__ constexpr float cos32(int m) {
     }
 }
 
-// In-register DFT of length 32 (natural order in and out): two DFT_16 of the
-// even and odd points, combined with W_32^k (exact rotations at k = 0, 8).
+// In-register DFT of length 32 (natural order in and out) as radix 4 x 8:
+// DFT_8 of each residue class x[4 m + j], twiddle W_32^(j k1), then a DFT_4
+// over j -> X[k1 + 8 k2].  20 non-trivial twiddles plus 2 per DFT_8 (28
+// complex multiplies; the radix-2 split takes 34), the same 160 complex adds.
+// The twiddle constants are SGPR operands of the packed FMA (cmul's asm would
+// copy each into VGPRs first); cmul's roundings.
+template <bool FWD>
+__device__ __forceinline__ float2 tw32(float2 o, int e) {
+    e &= 31;
+    if (e == 0) return o;
+    if (e == 16) return upk(-pk(o));
+    if (e == 8) return FWD ? cmul_mi(o) : cmul_pi(o);
+    if (e == 24) return FWD ? cmul_pi(o) : cmul_mi(o);
+    const float c = cos32(e), sn = FWD ? -cos32(e - 8) : cos32(e - 8);   // -+sin(2 pi e / 32)
+    const vf2_t O = pk(o);
+    return upk(__builtin_elementwise_fma(O.xx, vf2_t{c, sn}, O.yy * vf2_t{-sn, c}));
+}
 template <bool FWD>
 __device__ __forceinline__ void dft32(float2* v) {
-    float2 e[16], o[16];
+    float2 y[4][8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        e[i] = v[2 * i];
-        o[i] = v[2 * i + 1];
-    }
-    Dft<16, FWD>::run(e);
-    Dft<16, FWD>::run(o);
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (k == 8) {   // o * (-i) forward, (+i) backward: folded into the adds
-            v[k] = FWD ? cadd_i<false>(e[k], o[k]) : cadd_i<true>(e[k], o[k]);
-            v[k + 16] = FWD ? cadd_i<true>(e[k], o[k]) : cadd_i<false>(e[k], o[k]);
-        } else {
-            float2 t = o[k];
-            if (k != 0) {
-                // o * (c, s): cmul's roundings (fma(o.x, c, -o.y s), fma(o.x, s, o.y c)) with
-                // the constants as SGPR operands (cmul's asm would copy them into VGPRs)
-                const float c = cos32(k), sn = FWD ? -cos32(k - 8) : cos32(k - 8);   // -+sin(2 pi k / 32)
-                const vf2_t O = pk(o[k]);
-                t = upk(__builtin_elementwise_fma(O.xx, vf2_t{c, sn}, O.yy * vf2_t{-sn, c}));
-            }
-            v[k] = cadd(e[k], t);
-            v[k + 16] = csub(e[k], t);
-        }
+        for (int m = 0; m < 8; ++m) y[j][m] = v[4 * m + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Dft<8, FWD>::run(y[j]);
+#pragma unroll
+    for (int k1 = 0; k1 < 8; ++k1) {
+        const float2 a0 = y[0][k1], a1 = tw32<FWD>(y[1][k1], k1), a2 = tw32<FWD>(y[2][k1], 2 * k1),
+                     a3 = tw32<FWD>(y[3][k1], 3 * k1);
+        const float2 s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
+        v[k1] = cadd(s02, s13);
+        v[k1 + 16] = csub(s02, s13);
+        // d13 * W_4^1 (forward -i, backward +i) folded into the adds, as Dft<4>
+        v[k1 + 8] = FWD ? cadd_i<false>(d02, d13) : cadd_i<true>(d02, d13);
+        v[k1 + 24] = FWD ? cadd_i<true>(d02, d13) : cadd_i<false>(d02, d13);
     }
 }
 
@@ -790,6 +797,15 @@ __device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int lane32
 // l < 16 and 2l + 1, 2l + 33 in lane l + 16: the r32 layout (one residue mod 32
 // per lane) with residue 2 (l & 15) + (l >> 4).  The same swap turns two r32
 // registers (rows b, b + 1 of that residue layout) back into 8 B pairs.
+// (a.lo, b.lo) (SEL 0) or (a.hi, b.hi) (SEL 1) as one v_pk_mov_b32: two
+// registers from two different pairs without a v_mov per half
+template <int SEL>
+__device__ __forceinline__ vf2_t pk_pair(vf2_t a, vf2_t b) {
+    vf2_t r;
+    if constexpr (SEL) asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    else asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ void r32_pairswap(float& a, float& b) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
     a = __uint_as_float(r[0]);

@@ -588,12 +588,22 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             for (int i = 0; i < 16; ++i) r32_pairswap(xa[2 * i], xa[2 * i + 1]);
 #pragma unroll
             for (int i = 4; i < 16; ++i) r32_pairswap(xb[2 * i], xb[2 * i + 1]);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) xb[r] = xa[24 + r];
         }
         float2 v[32];
+        if constexpr (PAIRED) {
+            // v[r] = (block a row r, block b row r); block b's rows 0..7 are block a's
+            // rows 24..31 (edge couples too: the same sample indices)
 #pragma unroll
-        for (int r = 0; r < 32; ++r) v[r] = make_float2(xa[r], xb[r]);
+            for (int i = 0; i < 16; ++i) {
+                const vf2_t A = {xa[2 * i], xa[2 * i + 1]};
+                const vf2_t B = i < 4 ? vf2_t{xa[24 + 2 * i], xa[25 + 2 * i]} : vf2_t{xb[2 * i], xb[2 * i + 1]};
+                v[2 * i] = upk(pk_pair<0>(A, B));
+                v[2 * i + 1] = upk(pk_pair<1>(A, B));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) v[r] = make_float2(xa[r], xb[r]);
+        }
         const long long itn = it + it_step;
         if constexpr (DYN) {
             if (itn < it_end && lane == 0) rk = atomicAdd(ctr, 1u);   // -> the couple after itn
@@ -633,17 +643,20 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
                 if constexpr (PAIRED) {
                     // rows b, b + 1 -> 8 B pairs: lane l < 16 stores samples 32 b + 2l, +1,
                     // lane l + 16 samples 32 (b + 1) + 2l, +1
+                    float2 oa[12], ob[12];   // (row b, row b + 1) of block a / block b
 #pragma unroll
-                    for (int b = 8; b < 32; b += 2) {
-                        r32_pairswap(v[b].x, v[b + 1].x);
-                        r32_pairswap(v[b].y, v[b + 1].y);
+                    for (int i = 0; i < 12; ++i) {
+                        oa[i] = upk(pk_pair<0>(pk(v[8 + 2 * i]), pk(v[9 + 2 * i])));
+                        ob[i] = upk(pk_pair<1>(pk(v[8 + 2 * i]), pk(v[9 + 2 * i])));
+                        r32_pairswap(oa[i].x, oa[i].y);
+                        r32_pairswap(ob[i].x, ob[i].y);
                     }
                     float2* yp = reinterpret_cast<float2*>(y + c * y_stride + j * LOUT - LE) + (m & 15) + 16 * (m >> 4);
                     if (valid) {
 #pragma unroll
-                        for (int b = 8; b < 32; b += 2) st_nt(make_float2(v[b].x, v[b + 1].x), yp + 16 * b);
+                        for (int i = 0; i < 12; ++i) st_nt(oa[i], yp + 16 * (8 + 2 * i));
 #pragma unroll
-                        for (int b = 8; b < 32; b += 2) st_nt(make_float2(v[b].y, v[b + 1].y), yp + LOUT / 2 + 16 * b);
+                        for (int i = 0; i < 12; ++i) st_nt(ob[i], yp + LOUT / 2 + 16 * (8 + 2 * i));
                     }
                 } else if (valid) {
                     if constexpr (EXP & 64) {
