@@ -283,7 +283,7 @@ def case_stft_exp(e, nch=32, seconds=600):
         byts, (sig, win, out, lib)
 
 
-def case_lab(e, nch=32, seconds=600, fn="stftlab_run"):
+def case_lab(e, nch=32, seconds=600, fn="stftlab_run", row=1024):
     """the product STFT kernel with parts switched off (scripts/stftlab.hip, EXP bits:
     1 no FFT exchanges, 2 no FFT, 4 no row stores, 8 no span loads); bytes = the real job's"""
     import ctypes
@@ -298,7 +298,7 @@ def case_lab(e, nch=32, seconds=600, fn="stftlab_run"):
     sig, out = _SHARED[("lab", nch, n)]
     win = torch.hann_window(1024, periodic=False, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    byts = nch * n * 4 + nch * fr * 1024 * 4
+    byts = nch * n * 4 + nch * fr * row * 4
     return (lambda: run(e, sig.data_ptr(), n, nch, win.data_ptr(), out.data_ptr(), s)), \
         byts, (sig, win, out, lib)
 
@@ -522,7 +522,8 @@ CASES = {
     **{f"lab60_{e}": (lambda e=e: case_lab(e, nch=1, seconds=60)) for e in (0, 2, 4, 6, 8, 10, 14, 32782, 65550, 98318)},
     **{f"empty{g}": (lambda g=g: case_empty(g)) for g in (703, 2048)},
     **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
-       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026, 128, 256)},
+       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026, 128, 256, 131072)},
+    **{f"powlab{e}": (lambda e=e: case_lab(e, fn="stftpowlab_run", row=513)) for e in (0, 2, 4, 131072)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152,
                                                                          2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194,
@@ -589,7 +590,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--mark", action="store_true",
                     help="launch a tiny torch fill kernel before each case's runs (splits a rocprofv3 trace per case)")
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "wp", "ex", "rw", "lab", "model", "firlab", "c2clab"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "wp", "ex", "rw", "lab", "model", "firlab", "c2clab", "powlab"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

@@ -63,17 +63,24 @@ if sys.argv[1] == "fir":   # python scripts/labcheck.py fir <EXP>: k_fir_bulk_re
               f"(max |y| {ref.abs().max().item():.3g}), first at {idx}")
         assert d <= 1e-5 * ref.abs().max().item()   # same arithmetic, possibly other contractions
     sys.exit(0)
+# python scripts/labcheck.py [pow|lab5] <EXP> [nch] [seconds]: the power-row (stftpowlab_run) or
+# VAR 5 magnitude (stftlab5_run) lab launch instead of stftlab_run
+fn, row = "stftlab_run", 1024
+if sys.argv[1] in ("pow", "lab5"):
+    fn, row = ("stftpowlab_run", 513) if sys.argv[1] == "pow" else ("stftlab5_run", 1024)
+    sys.argv.pop(1)
 e = int(sys.argv[1])
 nch = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 sec = int(sys.argv[3]) if len(sys.argv) > 3 else 60
 lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
-lib.stftlab_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
-                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+getattr(lib, fn).argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
+                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+lib.stftlab_run = getattr(lib, fn)
 n = sec * 48000
 sig = torch.rand(nch, n, device="cuda") * 2 - 1
 win = torch.hann_window(1024, periodic=False, device="cuda")
 frames = (n - 1024 + 256) // 256 + 1
-ref = torch.full((nch, frames, 1024), -2.0, device="cuda")
+ref = torch.full((nch, frames, row), -2.0, device="cuda")
 assert lib.stftlab_run(0, sig.data_ptr(), n, nch, win.data_ptr(), ref.data_ptr(),
                        torch.cuda.current_stream().cuda_stream) == 0
 out = torch.full_like(ref, -1.0)

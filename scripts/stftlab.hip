@@ -233,6 +233,24 @@ static hipError_t lab_launch5(const float* sig, long long n, long long nch, cons
                        store_sink(), ctr, MelArgs{});
     return hipGetLastError();
 }
+// the product's power-row launch for hop % 256 == 0: k_stft_pair<1024, 2, 3, EXP> (the ring
+// walk, one workgroup per cps pairs per slot, runs of cps pairs); rows of n/2+1 floats
+template <int EXP>
+static hipError_t lab_launch_pow(const float* sig, long long n, long long nch, const float* win, float* out,
+                                 hipStream_t s) {
+    constexpr int N = 1024, F = Wg<N>::F;
+    const long long hop = 256, frames = n < N ? 1 : 1 + (n - N + hop) / hop, ppc = (frames + 1) / 2;
+    static std::atomic<int> cap;
+    const int cap0 = cached_grid(cap, (const void*)k_stft_pair<N, 2, 3, EXP>, 256, 0, 1LL << 40);
+    const long long pairs = nch * ppc;
+    long long cps = (pairs + (long long)F * cap0 - 1) / ((long long)F * cap0);
+    cps = cps < 1 ? 1 : (cps > 16 ? 16 : cps);
+    const long long chunk = cps * F, grid = (pairs + chunk - 1) / chunk;
+    hipLaunchKernelGGL((k_stft_pair<N, 2, 3, EXP>), dim3((unsigned)grid), dim3(256), 0, s, sig, n, nch, n, frames, hop,
+                       0LL, ppc, win, (void*)out, frames * (N / 2 + 1), pass_twiddles(N), twiddle_table(N),
+                       chunk | (cps << 40), store_sink(), (unsigned*)nullptr, MelArgs{});
+    return hipGetLastError();
+}
 // config 4's bulk launch (8 ch x 2^24, 257 taps: N 1024, le 256) of k_fir_bulk<1024, true, EXP>
 template <int EXP>
 static hipError_t lab_fir(const float2* H, const float* x, float* y, long long n, long long nch, hipStream_t s) {
@@ -382,12 +400,24 @@ extern "C" int stftlab_run(int exp, const float* sig, long long n, long long nch
     }
 }
 
+extern "C" int stftpowlab_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
+                              void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (exp) {
+#define C(E) case E: return (int)vvh::lab_launch_pow<E>(sig, n, nch, win, out, s);
+        C(0) C(2) C(4) C(131072)
+#undef C
+        default: return -1;
+    }
+}
+
 extern "C" int stftlab5_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
                             void* stream) {
     hipStream_t s = (hipStream_t)stream;
     switch (exp) {
 #define C(E) case E: return (int)vvh::lab_launch5<E>(sig, n, nch, win, out, s);
         C(0) C(2) C(4) C(6) C(8) C(10) C(16) C(18) C(32) C(34) C(512) C(514) C(1024) C(1026) C(128) C(256)
+        C(131072)
 #undef C
         default: return -1;
     }

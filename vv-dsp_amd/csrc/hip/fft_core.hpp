@@ -504,9 +504,58 @@ __host__ __device__ constexpr bool ri1024_check() {
 }
 static_assert(ri1024_check(), "Ri1024 decomposition of ri_pad");
 
-template <int N, int p, bool PAIRED>
+template <int BASE, int STEP>
+__device__ __forceinline__ void lds_rd32x16(const float* base, float* o);
+template <int STEP>
+__device__ __forceinline__ void lds_rd32x4x4(const float* b0, const float* b1, const float* b2, const float* b3,
+                                             float* o);
+// RIV 1 (N = 1024): the reads as single ds_read_b32 (lds_rd32x16 /
+// lds_rd32x4x4) so each real part and its imaginary part land straight in one
+// complex register pair (RIV 0: the compiler's ds_read2 pairs, then v_movs).
+template <int N, int p, bool PAIRED, int RIV = 0>
 __device__ __forceinline__ void pass_exchange_ri(float2* v, int t, float* lds) {
     using G = Geo<N>;
+    if constexpr (N == 1024 && RIV == 1) {
+        constexpr int R = G::radix(p), R2 = G::radix(p + 1);
+        static_assert(R == 16 && G::P / R == 1, "N = 1024: one radix-16 butterfly per thread before the exchange");
+        const int wb = Ri1024::wbase<p>(bfly<N, p, PAIRED>(t, 0));
+        int rb[G::P / R2];
+#pragma unroll
+        for (int i = 0; i < G::P / R2; ++i) rb[i] = Ri1024::rbase<p>(bfly<N, p + 1, PAIRED>(t, i));
+        auto write = [&](auto part) {
+            constexpr int Y = decltype(part)::value;
+            if constexpr (p == 0 && VVH_RI_B128) {   // 16 contiguous floats: four 16 B stores
+#pragma unroll
+                for (int u = 0; u < R / 4; ++u)
+                    *reinterpret_cast<vf4_t*>(lds + wb + 4 * u) =
+                        Y ? vf4_t{v[4 * u].y, v[4 * u + 1].y, v[4 * u + 2].y, v[4 * u + 3].y}
+                          : vf4_t{v[4 * u].x, v[4 * u + 1].x, v[4 * u + 2].x, v[4 * u + 3].x};
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) lds[wb + Ri1024::woff<p>(r)] = Y ? v[r].y : v[r].x;
+            }
+        };
+        auto read = [&](float* o) {
+            if constexpr (p == 0) {
+                static_assert(G::P / R2 == 1 && R2 == 16, "pass 1 reads: one radix-16 butterfly");
+                lds_rd32x16<0, 4 * Ri1024::roff<0>(1)>(lds + rb[0], o);
+            } else {
+                static_assert(G::P / R2 == 4 && R2 == 4, "pass 2 reads: four radix-4 butterflies");
+                lds_rd32x4x4<4 * Ri1024::roff<1>(1)>(lds + rb[0], lds + rb[1], lds + rb[2], lds + rb[3], o);
+            }
+        };
+        float re[G::P], im[G::P];
+        write(std::integral_constant<int, 0>{});
+        xsync<G::T>();
+        read(re);
+        xsync<G::T>();
+        write(std::integral_constant<int, 1>{});
+        xsync<G::T>();
+        read(im);
+#pragma unroll
+        for (int k = 0; k < G::P; ++k) v[k] = make_float2(re[k], im[k]);
+        return;
+    }
     if constexpr (N == 1024) {
         constexpr int R = G::radix(p), R2 = G::radix(p + 1);
         static_assert(R == 16 && G::P / R == 1, "N = 1024: one radix-16 butterfly per thread before the exchange");
@@ -640,6 +689,62 @@ __device__ __forceinline__ void lds_rd64x16(const float2* base, float2* out) {
                  : "v"(a), "n"(BASE + 0 * STEP), "n"(BASE + 1 * STEP), "n"(BASE + 2 * STEP), "n"(BASE + 3 * STEP), "n"(BASE + 4 * STEP), "n"(BASE + 5 * STEP), "n"(BASE + 6 * STEP), "n"(BASE + 7 * STEP), "n"(BASE + 8 * STEP), "n"(BASE + 9 * STEP), "n"(BASE + 10 * STEP), "n"(BASE + 11 * STEP), "n"(BASE + 12 * STEP), "n"(BASE + 13 * STEP), "n"(BASE + 14 * STEP), "n"(BASE + 15 * STEP));
 #pragma unroll
     for (int i = 0; i < 16; ++i) out[i] = upk(o[i]);
+}
+// 16 single-dword reads (b32, never merged into ds_read2) at byte offsets
+// BASE + i * STEP from `base`, then the wait -- one asm statement as above.
+// The outputs are 16 independent registers, so the caller can pair each with
+// another value into one complex register pair without a move (the compiler's
+// ds_read2 merging fixes each destination pair, and re-pairing costs v_movs).
+template <int BASE, int STEP>
+__device__ __forceinline__ void lds_rd32x16(const float* base, float* o) {
+    static_assert(BASE >= 0 && BASE + 15 * STEP < 65536, "ds offset range");
+    const unsigned a = (unsigned)(uintptr_t)base;
+    asm volatile("ds_read_b32 %0, %16 offset:%17\n\t"
+                 "ds_read_b32 %1, %16 offset:%18\n\t"
+                 "ds_read_b32 %2, %16 offset:%19\n\t"
+                 "ds_read_b32 %3, %16 offset:%20\n\t"
+                 "ds_read_b32 %4, %16 offset:%21\n\t"
+                 "ds_read_b32 %5, %16 offset:%22\n\t"
+                 "ds_read_b32 %6, %16 offset:%23\n\t"
+                 "ds_read_b32 %7, %16 offset:%24\n\t"
+                 "ds_read_b32 %8, %16 offset:%25\n\t"
+                 "ds_read_b32 %9, %16 offset:%26\n\t"
+                 "ds_read_b32 %10, %16 offset:%27\n\t"
+                 "ds_read_b32 %11, %16 offset:%28\n\t"
+                 "ds_read_b32 %12, %16 offset:%29\n\t"
+                 "ds_read_b32 %13, %16 offset:%30\n\t"
+                 "ds_read_b32 %14, %16 offset:%31\n\t"
+                 "ds_read_b32 %15, %16 offset:%32\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7]), "=&v"(o[8]), "=&v"(o[9]), "=&v"(o[10]), "=&v"(o[11]), "=&v"(o[12]), "=&v"(o[13]), "=&v"(o[14]), "=&v"(o[15])
+                 : "v"(a), "n"(BASE + 0 * STEP), "n"(BASE + 1 * STEP), "n"(BASE + 2 * STEP), "n"(BASE + 3 * STEP), "n"(BASE + 4 * STEP), "n"(BASE + 5 * STEP), "n"(BASE + 6 * STEP), "n"(BASE + 7 * STEP), "n"(BASE + 8 * STEP), "n"(BASE + 9 * STEP), "n"(BASE + 10 * STEP), "n"(BASE + 11 * STEP), "n"(BASE + 12 * STEP), "n"(BASE + 13 * STEP), "n"(BASE + 14 * STEP), "n"(BASE + 15 * STEP));
+}
+// 4 x 4 single-dword reads: o[4 i + r] from base i at byte offset r * STEP
+template <int STEP>
+__device__ __forceinline__ void lds_rd32x4x4(const float* b0, const float* b1, const float* b2, const float* b3,
+                                             float* o) {
+    static_assert(3 * STEP < 65536, "ds offset range");
+    const unsigned a0 = (unsigned)(uintptr_t)b0, a1 = (unsigned)(uintptr_t)b1, a2 = (unsigned)(uintptr_t)b2,
+                   a3 = (unsigned)(uintptr_t)b3;
+    asm volatile("ds_read_b32 %0, %16 offset:%20\n\t"
+                 "ds_read_b32 %1, %16 offset:%21\n\t"
+                 "ds_read_b32 %2, %16 offset:%22\n\t"
+                 "ds_read_b32 %3, %16 offset:%23\n\t"
+                 "ds_read_b32 %4, %17 offset:%20\n\t"
+                 "ds_read_b32 %5, %17 offset:%21\n\t"
+                 "ds_read_b32 %6, %17 offset:%22\n\t"
+                 "ds_read_b32 %7, %17 offset:%23\n\t"
+                 "ds_read_b32 %8, %18 offset:%20\n\t"
+                 "ds_read_b32 %9, %18 offset:%21\n\t"
+                 "ds_read_b32 %10, %18 offset:%22\n\t"
+                 "ds_read_b32 %11, %18 offset:%23\n\t"
+                 "ds_read_b32 %12, %19 offset:%20\n\t"
+                 "ds_read_b32 %13, %19 offset:%21\n\t"
+                 "ds_read_b32 %14, %19 offset:%22\n\t"
+                 "ds_read_b32 %15, %19 offset:%23\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7]), "=&v"(o[8]), "=&v"(o[9]), "=&v"(o[10]), "=&v"(o[11]), "=&v"(o[12]), "=&v"(o[13]), "=&v"(o[14]), "=&v"(o[15])
+                 : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "n"(0 * STEP), "n"(1 * STEP), "n"(2 * STEP), "n"(3 * STEP));
 }
 // 32 reads of consecutive float2 (byte offsets 8 i, i < 32) from `base`
 __device__ __forceinline__ void lds_rd64x32(const float2* base, float2* out) {
@@ -829,7 +934,7 @@ __device__ __forceinline__ void r32_twiddle(float2* v, const float2* atw) {
 // NOX: timing ablation only (scripts/membench.hip) -- the passes without their
 // exchanges, i.e. a wrong transform with the FFT's arithmetic but no LDS traffic.
 // C64: N = 1024 one-wave transforms exchange through pass_exchange_c1024.
-template <int N, bool FWD, int p, bool PAIRED, bool RI = false, bool NOX = false, bool C64 = false>
+template <int N, bool FWD, int p, bool PAIRED, bool RI = false, bool NOX = false, bool C64 = false, int RIV = 0>
 struct PassChain {
     template <class TW>
     __device__ __forceinline__ static void run(float2* v, int t, float2* lds, const TW& tw) {
@@ -837,9 +942,9 @@ struct PassChain {
         if constexpr (p + 1 < Geo<N>::NPASS) {
             if constexpr (NOX) asm volatile("" ::: "memory");
             else if constexpr (C64) pass_exchange_c1024<p>(v, t, lds);
-            else if constexpr (RI) pass_exchange_ri<N, p, PAIRED>(v, t, reinterpret_cast<float*>(lds));
+            else if constexpr (RI) pass_exchange_ri<N, p, PAIRED, RIV>(v, t, reinterpret_cast<float*>(lds));
             else pass_exchange<N, p, PAIRED>(v, t, lds);
-            PassChain<N, FWD, p + 1, PAIRED, RI, NOX, C64>::run(v, t, lds, tw);
+            PassChain<N, FWD, p + 1, PAIRED, RI, NOX, C64, RIV>::run(v, t, lds, tw);
         }
     }
 };
@@ -849,11 +954,11 @@ struct PassChain {
 // (pass_exchange_ri) instead of Geo<N>::LDS float2.  C64 (N = 1024, T = 64,
 // not PAIRED): the explicit-offset complex exchange, Geo<N>::LDS float2.
 template <int N, bool FWD, bool PAIRED = false, bool RI = false, class TW = TwTab<N>, bool NOX = false,
-          bool C64 = false>
+          bool C64 = false, int RIV = 0>
 __device__ __forceinline__ void fft_regs(float2* v, int t, float2* lds, const TW& tw) {
     static_assert(!PAIRED || Geo<N>::CAN_PAIR, "mirror pairing needs >= 2 last-pass butterflies per thread");
     static_assert(!C64 || (N == 1024 && !PAIRED && !RI), "pass_exchange_c1024: N = 1024, one wave, not paired");
-    PassChain<N, FWD, 0, PAIRED, RI, NOX, C64>::run(v, t, lds, tw);
+    PassChain<N, FWD, 0, PAIRED, RI, NOX, C64, RIV>::run(v, t, lds, tw);
 }
 
 // ---- shared pieces of the persistent streaming kernels ---------------------

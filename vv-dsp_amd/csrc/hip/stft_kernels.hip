@@ -856,10 +856,26 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (more) load_pair(cn, fn);
         }
         float2 v[G::P];
+        if constexpr (!(EXP & 131072) && BULK && G::T == 64) {
+            // the span reads come in pairs (r, r + 1) of one frame (ds_read2st64: adjacent
+            // registers); one v_pk_mov_b32 per (frame a, frame b) register pair instead of
+            // two v_mov_b32.  With the exchange reads as single ds_read_b32 (RIV 1) the
+            // loop's v_movs drop from 87 to 27 (power rows; VALU 419 -> 370 per pair),
+            // bit-identical, 2.766 -> 2.741 ms power / 3.410 -> 3.399 ms magnitude
+            // (profiles/r04_kbench_stft_movefree.jsonl).  EXP bit 17 (lab): round 3's
+            // read2 pairing and v_movs.
 #pragma unroll
-        for (int r = 0; r < G::P; ++r) {
-            const vf2_t x = {xa[r], xb[r]};
-            v[r] = upk((r & 1) ? pk_mul_bcast<1>(x, wp[r / 2]) : pk_mul_bcast<0>(x, wp[r / 2]));
+            for (int i = 0; i < G::P / 2; ++i) {
+                const vf2_t A = {xa[2 * i], xa[2 * i + 1]}, B = {xb[2 * i], xb[2 * i + 1]};
+                v[2 * i] = upk(pk_mul_bcast<0>(pk_pair<0>(A, B), wp[i]));
+                v[2 * i + 1] = upk(pk_mul_bcast<1>(pk_pair<1>(A, B), wp[i]));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const vf2_t x = {xa[r], xb[r]};
+                v[r] = upk((r & 1) ? pk_mul_bcast<1>(x, wp[r / 2]) : pk_mul_bcast<0>(x, wp[r / 2]));
+            }
         }
         if constexpr (GLDS) {
         } else if constexpr (TAIL) {
@@ -867,7 +883,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
-        if constexpr (!(EXP & 2)) fft_regs<N, true, true, RI, TWT, (EXP & 1) != 0>(v, t, my, tw);
+        if constexpr (!(EXP & 2))
+            fft_regs<N, true, true, RI, TWT, (EXP & 1) != 0, false, (EXP & 131072) ? 0 : 1>(v, t, my, tw);
         if constexpr (D2) {
             // the next pair's span: younger than it are the previous pair's NST
             // stores and, when in flight, the span just issued
