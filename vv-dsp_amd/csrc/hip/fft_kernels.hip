@@ -25,8 +25,10 @@ namespace vvh {
 // C2C
 // ------------------------------------------------------------------------
 // EXP: timing ablations for scripts/stftlab.hip only (the library instantiates
-// EXP = 0): bit 0 FFT without its LDS exchanges, bit 1 no FFT, bit 3 the exchange
-// reads as single ds_read_b32 (pass_exchange_ri RIV 1).  (Two transforms per loop
+// EXP = 0): bit 0 FFT without its LDS exchanges, bit 1 no FFT, bit 3 round 3's
+// exchange reads (the compiler's ds_read2 pairs and v_movs; the library reads
+// single ds_read_b32 into the complex register pairs, pass_exchange_ri RIV 1:
+// same buffers 0.1827 vs 0.1850 ms, profiles/r04_kbench_riv_ab.jsonl).  (Two transforms per loop
 // trip with alternating prefetch buffers, to drop the loop-carried copy, spilled
 // at the 128 VGPRs of four waves per SIMD.)
 // N = 1024 exchanges through the half-size real/imaginary buffer
@@ -65,7 +67,7 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
             for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(in + fn * in_dist + t + r * G::T);
         }
         if constexpr (!(EXP & 2))
-            fft_regs<N, FWD, false, RI, TwTab<N>, (EXP & 1) != 0, false, (EXP & 8) ? 1 : 0>(v, t, my, tw);
+            fft_regs<N, FWD, false, RI, TwTab<N>, (EXP & 1) != 0, false, (EXP & 8) ? 0 : 1>(v, t, my, tw);
         float2* dst = out + f * out_dist;
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {

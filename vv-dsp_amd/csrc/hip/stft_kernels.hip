@@ -269,7 +269,7 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
 // Log-mel (MODE 3) or MFCC (MODE 4) rows of one frame pair from the FFT
 // registers (N = 1024, one wave per transform).  The power of bins 0..N/2 of
 // both frames (pair_post<2>: the power rows' arithmetic) goes to the
-// transform's idle exchange buffer P in natural order; then k_mel_grp's steps
+// transform's idle exchange buffer P, the two rows interleaved bin by bin; then k_mel_grp's steps
 // with FR = 2 frames: chunk partials (FMA in bin order; lane c % 64 holds chunk
 // c in round c / 64), per-filter sums of the partials in chunk order (fetched
 // across lanes by ds_bpermute), logf(e + eps), and for MODE 4 the DCT-II and
@@ -291,7 +291,7 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
     using Mi = Mirror<N>;
     constexpr int R = G::RL, J = G::NPT / 2, NB = G::NB, T = G::T, RW = N / 2 + 1;
     static_assert(T == 64, "one wave per transform");
-    static_assert(2 * RW <= MEL_LM_OFF, "log-mel rows past the power rows");
+    static_assert(2 * RW <= MEL_LM_OFF, "log-mel rows past the (interleaved) power rows");
     float ea[J][R], eb[J][R], sa[R], sb[R];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -313,14 +313,18 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
         sb[r] = B2.x;
     }
     // block m of 64 bins: an even block (lane t: bin 64 m + t) or the mirror
-    // block of slot (jm, rm) (lane t: bin 64 m + (64 - t) % 64), as direct_rows
+    // block of slot (jm, rm) (lane t: bin 64 m + (64 - t) % 64), as direct_rows.
+    // The two rows go to P interleaved, P[2k] = |Xa[k]|^2, P[2k + 1] = |Xb[k]|^2:
+    // one ds_write_b64 per bin here and one ds_read_b64 per bin in the chunk sums
+    // below, the pair landing in one register pair for a packed FMA (two rows
+    // RW floats apart took two b32 accesses and v_movs to re-pair them)
+    auto put = [&](int bin, float va, float vb) { *reinterpret_cast<vf2_t*>(P + 2 * bin) = vf2_t{va, vb}; };
     static_for<0, N / T>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
         if constexpr (T * m < N / 2) {
             constexpr int je = m % (NB / T), re = m / (NB / T);
             if constexpr (je < J) {
-                P[T * m + t] = ea[je][re];
-                P[RW + T * m + t] = eb[je][re];
+                put(T * m + t, ea[je][re], eb[je][re]);
             } else {
                 constexpr int mm = (N / T - 1) - m, rm = mm / (NB / T), jm = mm % (NB / T);
                 float va, vb;
@@ -331,16 +335,11 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
                     va = t == 0 ? sa[rm] : ea[jm][rm];
                     vb = t == 0 ? sb[rm] : eb[jm][rm];
                 }
-                const int bin = T * m + (t == 0 ? 0 : T - t);
-                P[bin] = va;
-                P[RW + bin] = vb;
+                put(T * m + (t == 0 ? 0 : T - t), va, vb);
             }
         }
     });
-    if (t == 0) {
-        P[N / 2] = ea[0][R / 2];
-        P[RW + N / 2] = eb[0][R / 2];
-    }
+    if (t == 0) put(N / 2, ea[0][R / 2], eb[0][R / 2]);
     xsync<T>();
     const int nc = mel.nc, M = mel.M, C = mel.C;
     float pa[MEL_MAX_ROUNDS], pb[MEL_MAX_ROUNDS];
@@ -350,14 +349,15 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
         const int c = t + T * u;
         if (c < nc) {
             const int lo = sCh[3 * c], len = sCh[3 * c + 1], off = sCh[3 * c + 2];
-            float a0 = 0.0f, b0 = 0.0f;
+            vf2_t ab = {0.0f, 0.0f};   // (row a, row b) partials: fma per element, bin order
+            const vf2_t* pp = reinterpret_cast<const vf2_t*>(P) + lo;
+#pragma unroll 4
             for (int j = 0; j < len; ++j) {
                 const float w = sW[off + j];
-                a0 = __builtin_fmaf(P[lo + j], w, a0);
-                b0 = __builtin_fmaf(P[RW + lo + j], w, b0);
+                ab = __builtin_elementwise_fma(pp[j], vf2_t{w, w}, ab);
             }
-            pa[u] = a0;
-            pb[u] = b0;
+            pa[u] = ab.x;
+            pb[u] = ab.y;
         }
     }
     const int nr = (nc + T - 1) / T;   // rounds holding chunks (wave-uniform)
@@ -424,6 +424,7 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
                 float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
                 int m = 0;
                 if ((M & 3) == 0) {   // as k_mel_grp: four partial sums
+#pragma unroll 5
                     for (; m < M; m += 4) {
                         const vf4_t a = *reinterpret_cast<const vf4_t*>(l + m);
                         c0 = __builtin_fmaf(a[0], d[m], c0);
