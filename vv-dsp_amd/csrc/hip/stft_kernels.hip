@@ -1056,6 +1056,173 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
     }
 }
 
+// ------------------------------------------------------------------------
+// k_stft_r32<MODE>: power rows (MODE 2) of nfft = 1024, hop = 256 frames with
+// the transform split 32 x 32 on half-waves, as k_fir_r32: two frames per
+// complex FFT (z = w/2 (a + i b)), two frame pairs per wave (one per half),
+// ONE padded LDS transpose per FFT instead of k_stft_pair's two exchanges.
+//   lane m2 (residue 2 (m & 15) + (m >> 4), the PAIRED layout): the pair's
+//   1280-sample span as 20 dwordx2 loads re-laid by v_permlane16_swap -- frame
+//   a = span rows 0..31, frame b = span rows 8..39 (hop = 8 rows) -- times the
+//   window, DFT_32 over m1, twiddle W_1024^(m2 k1), transpose, DFT_32 over m2
+//   -> Z[m + 32 k2] in register k2 of lane m.
+// The mirror bins Z[N - k] (lane 32 - m, register 31 - k2; lane 0: register
+// 32 - k2) come back through the same LDS buffer (16 writes, 16 reads), then
+// pair_post<2> gives |Xa[k]|^2, |Xb[k]|^2 for bins 0..512 and each half stores
+// its pair's two rows, 128 B per instruction.  Spans that reach past the end
+// of the signal (the zero-padded tail) are staged through LDS with the zero
+// rule, in the same loop.  Persistent grid, static XCD walk over frame-pair
+// couples.  EXP (lab): bit 1 no FFT, bit 2 no stores.
+// ------------------------------------------------------------------------
+constexpr int R33_BUF = 33 * R32_ROW;   // 33 rows: the mirror read of lane 0 touches row 32
+template <int MODE, int EXP = 0>
+__global__ void __launch_bounds__(256, 2)
+k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, long long frames, const float* win,
+           float* out, long long out_ch_stride, const float2* tw1024) {
+    static_assert(MODE == 2, "power rows");
+    constexpr int N = 1024, HOP = 256, F = 4, RW = N / 2 + 1, SPAN = N + HOP;
+    __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R33_BUF];
+    __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r)
+    for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
+    const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
+    const int mr = 2 * (m & 15) + (m >> 4);   // this lane's input residue
+    float2* buf = xch + (2 * slot + half) * R33_BUF;
+    // 0.5 w[32 r + mr], two rows per register pair (the 1/2 of the two-frame split rides in the window)
+    vf2_t wp[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wp[i] = vf2_t{0.5f * win[64 * i + mr], 0.5f * win[64 * i + 32 + mr]};
+    __syncthreads();
+    const long long ppc = (frames + 1) / 2, pairs = nch * ppc, couples = (pairs + 1) / 2;
+    long long it, it_end, it_step;
+    xcd_walk(couples, F, slot, &it, &it_end, &it_step);
+    it = uni<64>(it);
+    it_end = uni<64>(it_end);
+    it_step = uni<64>(it_step);
+    if (it >= it_end) return;
+    // pair 2k = (channel c0, pair q0 of it), advanced incrementally (one division per wave)
+    long long c0 = (2 * it) / ppc, q0 = 2 * it - c0 * ppc;
+    const long long dc = (2 * it_step) / ppc, dq = 2 * it_step - dc * ppc;
+    auto locate = [&](long long k, long long* c, long long* q, bool* valid, bool* edge_any) {
+        const bool two = 2 * k + 1 < pairs;
+        const bool wrap = q0 + 1 == ppc;
+        const long long c1 = two ? c0 + (wrap ? 1 : 0) : c0, q1 = two ? (wrap ? 0 : q0 + 1) : q0;
+        *valid = !half || two;
+        *c = half ? c1 : c0;
+        *q = half ? q1 : q0;
+        *edge_any = 2 * q0 * HOP + SPAN > n || 2 * q1 * HOP + SPAN > n;
+    };
+    float xa[32], xt[8];   // span rows 0..31 (frame a) and 32..39 (frame b's rows 24..31)
+    auto load_bulk = [&](long long c, long long q) {
+        const float2* a = reinterpret_cast<const float2*>(sig + c * ch_stride + 2 * q * HOP) + m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float2 u = ld_nt(a + 32 * i);
+            xa[2 * i] = u.x;
+            xa[2 * i + 1] = u.y;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float2 u = a[32 * (16 + i)];   // the next pair's span starts here: cached
+            xt[2 * i] = u.x;
+            xt[2 * i + 1] = u.y;
+        }
+    };
+    // edge couples: the span through LDS with the zero rule (rolled loop), then the
+    // residue layout directly (no swap)
+    auto load_edge = [&](long long c, long long q) {
+        const float* xs = sig + c * ch_stride;
+        float* sf = reinterpret_cast<float*>(buf);
+        const long long s0 = 2 * q * HOP;
+#pragma unroll 1
+        for (int k = m; k < SPAN; k += 32) sf[k] = s0 + k < n ? xs[s0 + k] : 0.0f;
+        xsync<64>();
+#pragma unroll
+        for (int r = 0; r < 32; ++r) xa[r] = sf[32 * r + mr];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) xt[r] = sf[N + 32 * r + mr];
+        xsync<64>();
+    };
+    long long c, q;
+    bool valid, edge;
+    locate(it, &c, &q, &valid, &edge);
+    if (!edge) load_bulk(c, q);
+    for (; it < it_end; it += it_step) {
+        if (edge) {
+            load_edge(c, q);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) r32_pairswap(xa[2 * i], xa[2 * i + 1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r32_pairswap(xt[2 * i], xt[2 * i + 1]);
+        }
+        // v[r] = 0.5 w_r (a_r, b_r), b_r = span row r + 8
+        float2 v[32];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const vf2_t A = {xa[2 * i], xa[2 * i + 1]};
+            const vf2_t B = i < 12 ? vf2_t{xa[2 * i + 8], xa[2 * i + 9]} : vf2_t{xt[2 * i - 24], xt[2 * i - 23]};
+            v[2 * i] = upk(pk_mul_bcast<0>(pk_pair<0>(A, B), wp[i]));
+            v[2 * i + 1] = upk(pk_mul_bcast<1>(pk_pair<1>(A, B), wp[i]));
+        }
+        const long long itn = it + it_step;
+        long long cn = c, qn = q;
+        bool validn = valid, edgen = edge;
+        if (itn < it_end) {   // the next couple's span, in flight across this one's transform
+            q0 += dq;
+            c0 += dc;
+            if (q0 >= ppc) {
+                q0 -= ppc;
+                ++c0;
+            }
+            locate(itn, &cn, &qn, &validn, &edgen);
+            if (!edgen) load_bulk(cn, qn);
+        }
+        if constexpr (!(EXP & 2)) {
+            dft32<true>(v);
+            r32_twiddle<true>(v, ltw + mr);
+            r32_transpose(v, buf, mr, m);
+            dft32<true>(v);
+        }
+        // Z[N - k]: registers 16..31 of every lane through the buffer, read back mirrored
+#pragma unroll
+        for (int r = 16; r < 32; ++r) buf[R32_ROW * r + m] = v[r];
+        xsync<64>();
+        float2 zm[16];   // zm[15 - k2] = Z[N - (m + 32 k2)]
+        lds_rd64x16<0, 8 * R32_ROW>(buf + R32_ROW * (m == 0 ? 17 : 16) + ((32 - m) & 31), zm);
+        xsync<64>();   // the next couple's transpose writes stay behind these reads
+        if constexpr (!(EXP & 4)) {
+            const long long fa = 2 * q;
+            float* rowa = out + c * out_ch_stride + fa * RW + m;
+            float* rowb = rowa + RW;
+            const bool hb = fa + 1 < frames;
+            float A[16], B[16];
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) {
+                float2 pa, pb;
+                pair_post<2>(v[k2], (k2 == 0 && m == 0) ? v[0] : zm[15 - k2], &pa, &pb);
+                A[k2] = pa.x;
+                B[k2] = pb.x;
+            }
+            float2 na, nb;   // bin 512: Z[512] is its own mirror (lane 0, register 16)
+            pair_post<2>(v[16], v[16], &na, &nb);
+            if (valid) {
+#pragma unroll
+                for (int k2 = 0; k2 < 16; ++k2) rowa[32 * k2] = A[k2];
+                if (m == 0) rowa[512] = na.x;
+                if (hb) {
+#pragma unroll
+                    for (int k2 = 0; k2 < 16; ++k2) rowb[32 * k2] = B[k2];
+                    if (m == 0) rowb[512] = nb.x;
+                }
+            }
+        }
+        c = cn;
+        q = qn;
+        valid = validn;
+        edge = edgen;
+    }
+}
+
 template <int N, int MODE>
 static hipError_t run_stft(const float* sig, long long n, long long nch, long long ch_stride,
                            long long frames, long long hop, const float* win, void* out,
@@ -1144,6 +1311,21 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // power rows keep the ring walk below (2.689 ring vs 2.730 dynamic vs
         // 2.760 chunked, profiles/r03_kbench_dyn_modes.jsonl).  Knob STFT_DYN =
         // 1 forces it for every row kind (A/B).
+        // power rows, nfft 1024 / hop 256, 8 B aligned channels: the 32 x 32 split
+        // (k_stft_r32) when knob POW_R32 = 1 (A/B)
+        if constexpr (N == 1024 && MODE == 2) {
+            if (hop == 256 && knob(KNOB_POW_R32, 0) == 1 && ((uintptr_t)sig & 7) == 0 && (nch == 1 || (ch_stride & 1) == 0)) {
+                static std::atomic<int> capr;
+                const int cap = cached_grid(capr, (const void*)k_stft_r32<2>, 256, 0, 1LL << 40);
+                const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
+                const int grid = (int)(need < cap ? need : cap);
+                if (grid < 1) return hipSuccess;
+                stat_inc(STAT_POW_R32);
+                hipLaunchKernelGGL((k_stft_r32<2>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, win,
+                                   (float*)out, out_ch_stride, tN);
+                return hipGetLastError();
+            }
+        }
         const long long kdyn = knob(KNOB_STFT_DYN, -1);
         bool dyn = false;
         if constexpr (Geo<N>::T == 64) {
