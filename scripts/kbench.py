@@ -525,6 +525,7 @@ CASES = {
        for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026, 128, 256, 131072)},
     **{f"powlab{e}": (lambda e=e: case_lab(e, fn="stftpowlab_run", row=513)) for e in (0, 2, 4, 131072)},
     **{f"powr32lab{e}": (lambda e=e: case_lab(e, fn="stftpowr32lab_run", row=513)) for e in (0, 2, 4, 6)},
+    **{f"magr32lab{e}": (lambda e=e: case_lab(e, fn="stftmagr32lab_run")) for e in (0, 2, 4, 6)},
     **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
                                                                          128, 256, 512, 1024, 640, 1152,
                                                                          2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194,
@@ -558,6 +559,7 @@ CASES = {
     "stft60ring": with_env(lambda: case_stft(1, 60), "VVHIP_STFT_RING", "1"),
     "stftpow": lambda: case_stft_power(32, 600),
     "stftpowr32": with_env(lambda: case_stft_power(32, 600), "VVHIP_POW_R32", "1"),
+    "stftmagr32": with_env(lambda: case_stft(32, 600), "VVHIP_MAG_R32", "1"),
     "stftpowold": with_env(lambda: case_stft_power(32, 600), "VVHIP_POW_OLD", "1"),
     "stftc": lambda: case_stft(8, 600, complex_out=True),
     "stftcold": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_POW_OLD", "1"),
@@ -592,7 +594,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--mark", action="store_true",
                     help="launch a tiny torch fill kernel before each case's runs (splits a rocprofv3 trace per case)")
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "wp", "ex", "rw", "lab", "model", "firlab", "c2clab", "powlab", "powr32lab"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "wp", "ex", "rw", "lab", "model", "firlab", "c2clab", "powlab", "powr32lab", "magr32lab"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

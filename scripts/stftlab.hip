@@ -421,6 +421,26 @@ extern "C" int stftpowr32lab_run(int exp, const float* sig, long long n, long lo
     }
 }
 
+extern "C" int stftmagr32lab_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
+                                 void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const long long frames = n < 1024 ? 1 : 1 + (n - 1024 + 256) / 256, ppc = (frames + 1) / 2;
+    const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
+    switch (exp) {
+#define C(E)                                                                                                       \
+    case E: {                                                                                                      \
+        static std::atomic<int> cap;                                                                               \
+        const int cp = vvh::cached_grid(cap, (const void*)vvh::k_stft_r32<0, E>, 256, 0, 1LL << 40);              \
+        hipLaunchKernelGGL((vvh::k_stft_r32<0, E>), dim3((unsigned)(need < cp ? need : cp)), dim3(256), 0, s, sig, \
+                           n, nch, n, frames, win, out, frames * 1024, vvh::twiddle_table(1024));                  \
+        return (int)hipGetLastError();                                                                             \
+    }
+        C(0) C(2) C(4) C(6)
+#undef C
+        default: return -1;
+    }
+}
+
 extern "C" int stftpowlab_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
                               void* stream) {
     hipStream_t s = (hipStream_t)stream;

@@ -74,3 +74,31 @@ def test_pow_r32_large_sampled_and_repeatable(vdev, orc, knob):
             seg = np.concatenate([x[c].astype(np.float64), np.zeros(nfft)])[f * hop:f * hop + nfft]
             ref = np.abs(np.fft.rfft(seg * w)) ** 2
             assert np.all(np.abs(pw[c, f] - ref) <= 1e-4 * np.abs(ref) + 1e-4 * ref.max()), (c, f)
+
+
+@pytest.mark.parametrize("nch,n,stride_pad", [(3, 48000 + 333, 1), (1, 1280, 0), (5, 1024 + 3 * 256, 2),
+                                              (7, 48128, 0), (2, 1024, 0), (3, 1279, 5)])
+def test_mag_r32_vs_f64(vdev, orc, knob, nch, n, stride_pad):
+    """The magnitude rows of the same split (knob MAG_R32 = 1): all 1024 bins,
+    the upper half stored from the mirrored registers, against NumPy f64 at the
+    harness tolerance (rtol = atol = 5e-5, python/test_fft.py:37-38)."""
+    import torch
+    import vvdsp_amd as vv
+    nfft, hop = 1024, 256
+    g = torch.Generator(device="cuda").manual_seed(n + 29 * nch + stride_pad)
+    base = torch.rand(nch, n + stride_pad, device="cuda", generator=g) * 2 - 1
+    sig = base[:, :n]
+    st = vdev.Stft(nfft, hop)
+    fr = st.frames(n)
+    knob("MAG_R32", 1)
+    vv.debug_clear("STAT_MAG_R32")
+    mag = st.spectrogram(sig)
+    torch.cuda.synchronize()
+    assert vv.debug_get("STAT_MAG_R32") == 1, "k_stft_r32<0> did not run"
+    mag = mag.cpu().numpy()
+    w = orc.window(1, nfft).astype(np.float64)
+    x = sig.cpu().numpy()
+    for c in range(nch):
+        pad = np.concatenate([x[c].astype(np.float64), np.zeros(nfft + hop)])
+        X = np.fft.fft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1)
+        np.testing.assert_allclose(mag[c], np.abs(X), rtol=5e-5, atol=5e-5)

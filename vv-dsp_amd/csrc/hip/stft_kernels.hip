@@ -1079,8 +1079,8 @@ template <int MODE, int EXP = 0>
 __global__ void __launch_bounds__(256, 2)
 k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, long long frames, const float* win,
            float* out, long long out_ch_stride, const float2* tw1024) {
-    static_assert(MODE == 2, "power rows");
-    constexpr int N = 1024, HOP = 256, F = 4, RW = N / 2 + 1, SPAN = N + HOP;
+    static_assert(MODE == 0 || MODE == 2, "magnitude or power rows");
+    constexpr int N = 1024, HOP = 256, F = 4, RW = MODE == 2 ? N / 2 + 1 : N, SPAN = N + HOP;
     __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R33_BUF];
     __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r)
     for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
@@ -1190,7 +1190,47 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
         float2 zm[16];   // zm[15 - k2] = Z[N - (m + 32 k2)]
         lds_rd64x16<0, 8 * R32_ROW>(buf + R32_ROW * (m == 0 ? 17 : 16) + ((32 - m) & 31), zm);
         xsync<64>();   // the next couple's transpose writes stay behind these reads
-        if constexpr (!(EXP & 4)) {
+        if constexpr (!(EXP & 4) && MODE == 0) {
+            // magnitude rows (all N bins): block k2 < 16 straight (lane m: bin m + 32 k2),
+            // block 31 - k2 from the mirror -- lane m >= 1 writes |X[k]| at N - k =
+            // (32 - m) + 32 (31 - k2); lane 0 writes bin 32 (k2 + 1) there (position 0
+            // of that block, its own direct bin; k2 = 15: the Nyquist bin 512) -- so
+            // every store instruction covers one aligned 128 B line per half
+            const long long fa = 2 * q;
+            float* rowa = out + c * out_ch_stride + fa * RW;
+            float* rowb = rowa + RW;
+            const bool hb = fa + 1 < frames;
+            float A[17], B[17];
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) {
+                float2 pa, pb;
+                pair_post<0>(v[k2], (k2 == 0 && m == 0) ? v[0] : zm[15 - k2], &pa, &pb);
+                A[k2] = pa.x;
+                B[k2] = pb.x;
+            }
+            {
+                float2 pa, pb;   // lane 0: bin 512 (Z[512] is its own mirror)
+                pair_post<0>(v[16], v[16], &pa, &pb);
+                A[16] = pa.x;
+                B[16] = pb.x;
+            }
+            const int pm = m == 0 ? 0 : 32 - m;
+            if (valid) {
+#pragma unroll
+                for (int k2 = 0; k2 < 16; ++k2) __builtin_nontemporal_store(A[k2], rowa + m + 32 * k2);
+#pragma unroll
+                for (int k2 = 0; k2 < 16; ++k2)
+                    __builtin_nontemporal_store(m == 0 ? A[k2 + 1] : A[k2], rowa + pm + 32 * (31 - k2));
+                if (hb) {
+#pragma unroll
+                    for (int k2 = 0; k2 < 16; ++k2) __builtin_nontemporal_store(B[k2], rowb + m + 32 * k2);
+#pragma unroll
+                    for (int k2 = 0; k2 < 16; ++k2)
+                        __builtin_nontemporal_store(m == 0 ? B[k2 + 1] : B[k2], rowb + pm + 32 * (31 - k2));
+                }
+            }
+        }
+        if constexpr (!(EXP & 4) && MODE == 2) {
             const long long fa = 2 * q;
             float* rowa = out + c * out_ch_stride + fa * RW + m;
             float* rowb = rowa + RW;
@@ -1322,6 +1362,20 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 if (grid < 1) return hipSuccess;
                 stat_inc(STAT_POW_R32);
                 hipLaunchKernelGGL((k_stft_r32<2>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, win,
+                                   (float*)out, out_ch_stride, tN);
+                return hipGetLastError();
+            }
+        }
+        if constexpr (N == 1024 && MODE == 0) {   // magnitude rows: the same split on knob MAG_R32 = 1 (A/B)
+            if (hop == 256 && knob(KNOB_MAG_R32, 0) == 1 && ((uintptr_t)sig & 7) == 0 &&
+                (nch == 1 || (ch_stride & 1) == 0) && ((uintptr_t)out & 127) == 0 && (out_ch_stride & 31) == 0) {
+                static std::atomic<int> capm;
+                const int cap = cached_grid(capm, (const void*)k_stft_r32<0>, 256, 0, 1LL << 40);
+                const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
+                const int grid = (int)(need < cap ? need : cap);
+                if (grid < 1) return hipSuccess;
+                stat_inc(STAT_MAG_R32);
+                hipLaunchKernelGGL((k_stft_r32<0>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, win,
                                    (float*)out, out_ch_stride, tN);
                 return hipGetLastError();
             }
