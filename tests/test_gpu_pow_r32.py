@@ -4,8 +4,9 @@ bin at the power-row tolerance of test_gpu_parity.test_stft_power_rows, against
 the default kernel, and with the path counter proving the kernel ran.  Shapes:
 odd channel counts (a frame-pair couple spanning two channels, a missing last
 pair), odd frame counts (a pair without its second frame), zero-padded tail
-frames (spans staged through LDS), signals shorter than one span, padded
-(even) channel strides, and rows that are not 16 B aligned."""
+frames (spans staged through LDS), signals shorter than one span, and rows
+that are not 16 B aligned (the path takes 8 B aligned channels: even channel
+strides, or one channel)."""
 import numpy as np
 import pytest
 
@@ -17,16 +18,15 @@ def _ref_power(x, nfft, hop, fr, w):
     return np.abs(np.fft.rfft(np.stack([pad[f * hop:f * hop + nfft] for f in range(fr)]) * w, axis=1)) ** 2
 
 
-@pytest.mark.parametrize("nch,n,stride_pad,off", [(3, 48000 + 333, 1, 0), (1, 1280, 0, 0), (1, 701, 0, 1),
-                                                  (5, 1024 + 3 * 256, 2, 0), (4, 20000, 6, 3),
-                                                  (7, 48128, 0, 2), (2, 1024, 0, 0), (3, 1279, 5, 0)])
-def test_pow_r32_vs_f64(vdev, orc, knob, nch, n, stride_pad, off):
+@pytest.mark.parametrize("nch,n,off", [(3, 48000 + 334, 0), (1, 1280, 0), (1, 701, 1), (1, 48000 + 333, 0),
+                                        (5, 1024 + 3 * 256, 0), (4, 20000, 3), (7, 48128, 2), (2, 1024, 0),
+                                        (3, 1280 + 2, 0)])
+def test_pow_r32_vs_f64(vdev, orc, knob, nch, n, off):
     import torch
     import vvdsp_amd as vv
     nfft, hop = 1024, 256
-    g = torch.Generator(device="cuda").manual_seed(n + 17 * nch + stride_pad)
-    base = torch.rand(nch, n + stride_pad, device="cuda", generator=g) * 2 - 1
-    sig = base[:, :n]
+    g = torch.Generator(device="cuda").manual_seed(n + 17 * nch)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1   # channel stride n: even, or one channel
     st = vdev.Stft(nfft, hop)
     fr, nh = st.frames(n), nfft // 2 + 1
     buf = torch.full((off + nch * fr * nh + 64,), -7.0, device="cuda")
@@ -76,18 +76,17 @@ def test_pow_r32_large_sampled_and_repeatable(vdev, orc, knob):
             assert np.all(np.abs(pw[c, f] - ref) <= 1e-4 * np.abs(ref) + 1e-4 * ref.max()), (c, f)
 
 
-@pytest.mark.parametrize("nch,n,stride_pad", [(3, 48000 + 333, 1), (1, 1280, 0), (5, 1024 + 3 * 256, 2),
-                                              (7, 48128, 0), (2, 1024, 0), (3, 1279, 5)])
-def test_mag_r32_vs_f64(vdev, orc, knob, nch, n, stride_pad):
+@pytest.mark.parametrize("nch,n", [(3, 48000 + 334), (1, 1280), (1, 48000 + 333), (5, 1024 + 3 * 256),
+                                   (7, 48128), (2, 1024), (3, 1280 + 2)])
+def test_mag_r32_vs_f64(vdev, orc, knob, nch, n):
     """The magnitude rows of the same split (knob MAG_R32 = 1): all 1024 bins,
     the upper half stored from the mirrored registers, against NumPy f64 at the
     harness tolerance (rtol = atol = 5e-5, python/test_fft.py:37-38)."""
     import torch
     import vvdsp_amd as vv
     nfft, hop = 1024, 256
-    g = torch.Generator(device="cuda").manual_seed(n + 29 * nch + stride_pad)
-    base = torch.rand(nch, n + stride_pad, device="cuda", generator=g) * 2 - 1
-    sig = base[:, :n]
+    g = torch.Generator(device="cuda").manual_seed(n + 29 * nch)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
     st = vdev.Stft(nfft, hop)
     fr = st.frames(n)
     knob("MAG_R32", 1)

@@ -1183,50 +1183,39 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
             r32_transpose(v, buf, mr, m);
             dft32<true>(v);
         }
-        // Z[N - k]: registers 16..31 of every lane through the buffer, read back mirrored
+        // Z[N - k] (lane 32 - m, register 31 - r; lane 0: register 32 - r) through the
+        // buffer: registers 16..31 for the power rows' bins 0..512, all 32 for the
+        // magnitude rows, whose upper half each lane computes from its own
+        // registers 16..31 (the same roundings as the mirror's: |X[N - k]| = |X[k]|
+        // bit for bit), so every store has the lanes in address order
 #pragma unroll
-        for (int r = 16; r < 32; ++r) buf[R32_ROW * r + m] = v[r];
+        for (int r = MODE == 0 ? 0 : 16; r < 32; ++r) buf[R32_ROW * r + m] = v[r];
         xsync<64>();
-        float2 zm[16];   // zm[15 - k2] = Z[N - (m + 32 k2)]
+        float2 zm[16];   // zm[15 - k2] = Z[N - (m + 32 k2)], k2 < 16
         lds_rd64x16<0, 8 * R32_ROW>(buf + R32_ROW * (m == 0 ? 17 : 16) + ((32 - m) & 31), zm);
+        float2 zu[16];   // MODE 0: zu[31 - r] = Z[N - (m + 32 r)], r >= 16 (lane 0, r = 16: Z[512] itself)
+        if constexpr (MODE == 0) lds_rd64x16<0, 8 * R32_ROW>(buf + R32_ROW * (m == 0 ? 1 : 0) + ((32 - m) & 31), zu);
         xsync<64>();   // the next couple's transpose writes stay behind these reads
         if constexpr (!(EXP & 4) && MODE == 0) {
-            // magnitude rows (all N bins): block k2 < 16 straight (lane m: bin m + 32 k2),
-            // block 31 - k2 from the mirror -- lane m >= 1 writes |X[k]| at N - k =
-            // (32 - m) + 32 (31 - k2); lane 0 writes bin 32 (k2 + 1) there (position 0
-            // of that block, its own direct bin; k2 = 15: the Nyquist bin 512) -- so
-            // every store instruction covers one aligned 128 B line per half
+            // magnitude rows, all N bins: lane m stores bin m + 32 r of both rows, r < 32
             const long long fa = 2 * q;
-            float* rowa = out + c * out_ch_stride + fa * RW;
+            float* rowa = out + c * out_ch_stride + fa * RW + m;
             float* rowb = rowa + RW;
             const bool hb = fa + 1 < frames;
-            float A[17], B[17];
+            float A[32], B[32];
 #pragma unroll
-            for (int k2 = 0; k2 < 16; ++k2) {
+            for (int r = 0; r < 32; ++r) {
                 float2 pa, pb;
-                pair_post<0>(v[k2], (k2 == 0 && m == 0) ? v[0] : zm[15 - k2], &pa, &pb);
-                A[k2] = pa.x;
-                B[k2] = pb.x;
+                pair_post<0>(v[r], r < 16 ? ((r == 0 && m == 0) ? v[0] : zm[15 - r]) : zu[31 - r], &pa, &pb);
+                A[r] = pa.x;
+                B[r] = pb.x;
             }
-            {
-                float2 pa, pb;   // lane 0: bin 512 (Z[512] is its own mirror)
-                pair_post<0>(v[16], v[16], &pa, &pb);
-                A[16] = pa.x;
-                B[16] = pb.x;
-            }
-            const int pm = m == 0 ? 0 : 32 - m;
             if (valid) {
 #pragma unroll
-                for (int k2 = 0; k2 < 16; ++k2) __builtin_nontemporal_store(A[k2], rowa + m + 32 * k2);
-#pragma unroll
-                for (int k2 = 0; k2 < 16; ++k2)
-                    __builtin_nontemporal_store(m == 0 ? A[k2 + 1] : A[k2], rowa + pm + 32 * (31 - k2));
+                for (int r = 0; r < 32; ++r) __builtin_nontemporal_store(A[r], rowa + 32 * r);
                 if (hb) {
 #pragma unroll
-                    for (int k2 = 0; k2 < 16; ++k2) __builtin_nontemporal_store(B[k2], rowb + m + 32 * k2);
-#pragma unroll
-                    for (int k2 = 0; k2 < 16; ++k2)
-                        __builtin_nontemporal_store(m == 0 ? B[k2 + 1] : B[k2], rowb + pm + 32 * (31 - k2));
+                    for (int r = 0; r < 32; ++r) __builtin_nontemporal_store(B[r], rowb + 32 * r);
                 }
             }
         }
