@@ -902,6 +902,15 @@ __device__ __forceinline__ void r32_transpose(float2* v, float2* buf, int lane32
 // l < 16 and 2l + 1, 2l + 33 in lane l + 16: the r32 layout (one residue mod 32
 // per lane) with residue 2 (l & 15) + (l >> 4).  The same swap turns two r32
 // registers (rows b, b + 1 of that residue layout) back into 8 B pairs.
+// Half-waves trade a <-> b (v_permlane32_swap: lanes 32..63 of `a` with lanes
+// 0..31 of `b`): afterwards a = (half 0's a | half 0's b), b = (half 1's a |
+// half 1's b) -- each register then holds one half's pair of values across the
+// whole wave.
+__device__ __forceinline__ void r32_halfswap(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
 // (a.lo, b.lo) (SEL 0) or (a.hi, b.hi) (SEL 1) as one v_pk_mov_b32: two
 // registers from two different pairs without a v_mov per half
 template <int SEL>

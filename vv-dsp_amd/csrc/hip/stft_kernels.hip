@@ -1102,7 +1102,14 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
     // pair 2k = (channel c0, pair q0 of it), advanced incrementally (one division per wave)
     long long c0 = (2 * it) / ppc, q0 = 2 * it - c0 * ppc;
     const long long dc = (2 * it_step) / ppc, dq = 2 * it_step - dc * ppc;
-    auto locate = [&](long long k, long long* c, long long* q, bool* valid, bool* edge_any) {
+    // a couple's rows as the stores see them: both pairs' row offsets (every lane
+    // stores 256 B runs of ONE pair per instruction, see below), whether the second
+    // pair exists, and whether each pair has its second frame
+    struct Rows {
+        long long oa, ob;
+        bool two, ha, hb;
+    };
+    auto locate = [&](long long k, long long* c, long long* q, bool* valid, bool* edge_any, Rows* rw) {
         const bool two = 2 * k + 1 < pairs;
         const bool wrap = q0 + 1 == ppc;
         const long long c1 = two ? c0 + (wrap ? 1 : 0) : c0, q1 = two ? (wrap ? 0 : q0 + 1) : q0;
@@ -1110,6 +1117,11 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
         *c = half ? c1 : c0;
         *q = half ? q1 : q0;
         *edge_any = 2 * q0 * HOP + SPAN > n || 2 * q1 * HOP + SPAN > n;
+        rw->oa = c0 * out_ch_stride + 2 * q0 * RW;
+        rw->ob = c1 * out_ch_stride + 2 * q1 * RW;
+        rw->two = two;
+        rw->ha = 2 * q0 + 1 < frames;
+        rw->hb = 2 * q1 + 1 < frames;
     };
     float xa[32], xt[8];   // span rows 0..31 (frame a) and 32..39 (frame b's rows 24..31)
     auto load_bulk = [&](long long c, long long q) {
@@ -1144,7 +1156,8 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
     };
     long long c, q;
     bool valid, edge;
-    locate(it, &c, &q, &valid, &edge);
+    Rows rw;
+    locate(it, &c, &q, &valid, &edge, &rw);
     if (!edge) load_bulk(c, q);
     for (; it < it_end; it += it_step) {
         if (edge) {
@@ -1167,6 +1180,7 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
         const long long itn = it + it_step;
         long long cn = c, qn = q;
         bool validn = valid, edgen = edge;
+        Rows rwn = rw;
         if (itn < it_end) {   // the next couple's span, in flight across this one's transform
             q0 += dq;
             c0 += dc;
@@ -1174,7 +1188,7 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
                 q0 -= ppc;
                 ++c0;
             }
-            locate(itn, &cn, &qn, &validn, &edgen);
+            locate(itn, &cn, &qn, &validn, &edgen, &rwn);
             if (!edgen) load_bulk(cn, qn);
         }
         if constexpr (!(EXP & 2)) {
@@ -1197,11 +1211,11 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
         if constexpr (MODE == 0) lds_rd64x16<0, 8 * R32_ROW>(buf + R32_ROW * (m == 0 ? 1 : 0) + ((32 - m) & 31), zu);
         xsync<64>();   // the next couple's transpose writes stay behind these reads
         if constexpr (!(EXP & 4) && MODE == 0) {
-            // magnitude rows, all N bins: lane m stores bin m + 32 r of both rows, r < 32
-            const long long fa = 2 * q;
-            float* rowa = out + c * out_ch_stride + fa * RW + m;
-            float* rowb = rowa + RW;
-            const bool hb = fa + 1 < frames;
+            // magnitude rows, all N bins: lane m holds bin m + 32 r of its pair's two
+            // rows, r < 32.  Blocks 2j, 2j + 1 of one row are an aligned 256 B run: one
+            // v_permlane32_swap per register pair moves half 0's block 2j + 1 up and half
+            // 1's block 2j down, so each store writes 256 B of ONE pair's row (the first
+            // pair's, then the second's) -- the 64-lane width of k_stft_pair's stores.
             float A[32], B[32];
 #pragma unroll
             for (int r = 0; r < 32; ++r) {
@@ -1210,13 +1224,27 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
                 A[r] = pa.x;
                 B[r] = pb.x;
             }
-            if (valid) {
+            const int lo = half * 32 + m;   // this lane's float in a 256 B run
+            float* ra = out + rw.oa + lo;
+            float* rb = out + rw.ob + lo;
 #pragma unroll
-                for (int r = 0; r < 32; ++r) __builtin_nontemporal_store(A[r], rowa + 32 * r);
-                if (hb) {
+            for (int j = 0; j < 16; ++j) {
+                r32_halfswap(A[2 * j], A[2 * j + 1]);
+                r32_halfswap(B[2 * j], B[2 * j + 1]);
+            }
 #pragma unroll
-                    for (int r = 0; r < 32; ++r) __builtin_nontemporal_store(B[r], rowb + 32 * r);
-                }
+            for (int j = 0; j < 16; ++j) __builtin_nontemporal_store(A[2 * j], ra + 64 * j);
+            if (rw.two) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) __builtin_nontemporal_store(A[2 * j + 1], rb + 64 * j);
+            }
+            if (rw.ha) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) __builtin_nontemporal_store(B[2 * j], ra + RW + 64 * j);
+            }
+            if (rw.two && rw.hb) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) __builtin_nontemporal_store(B[2 * j + 1], rb + RW + 64 * j);
             }
         }
         if constexpr (!(EXP & 4) && MODE == 2) {
@@ -1234,21 +1262,40 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
             }
             float2 na, nb;   // bin 512: Z[512] is its own mirror (lane 0, register 16)
             pair_post<2>(v[16], v[16], &na, &nb);
-            if (valid) {
+            if (valid && m == 0) {   // each half's lane 0: its own pair's bin 512
+                rowa[512] = na.x;
+                if (hb) rowb[512] = nb.x;
+            }
+            // bins 0..511 as 256 B runs of one pair's row per store (v_permlane32_swap,
+            // as the magnitude rows)
 #pragma unroll
-                for (int k2 = 0; k2 < 16; ++k2) rowa[32 * k2] = A[k2];
-                if (m == 0) rowa[512] = na.x;
-                if (hb) {
+            for (int j = 0; j < 8; ++j) {
+                r32_halfswap(A[2 * j], A[2 * j + 1]);
+                r32_halfswap(B[2 * j], B[2 * j + 1]);
+            }
+            const int lo = half * 32 + m;
+            float* pa = out + rw.oa + lo;
+            float* pb = out + rw.ob + lo;
 #pragma unroll
-                    for (int k2 = 0; k2 < 16; ++k2) rowb[32 * k2] = B[k2];
-                    if (m == 0) rowb[512] = nb.x;
-                }
+            for (int j = 0; j < 8; ++j) pa[64 * j] = A[2 * j];
+            if (rw.two) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pb[64 * j] = A[2 * j + 1];
+            }
+            if (rw.ha) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pa[RW + 64 * j] = B[2 * j];
+            }
+            if (rw.two && rw.hb) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pb[RW + 64 * j] = B[2 * j + 1];
             }
         }
         c = cn;
         q = qn;
         valid = validn;
         edge = edgen;
+        rw = rwn;
     }
 }
 
