@@ -421,6 +421,14 @@ extern "C" int stftpowr32lab_run(int exp, const float* sig, long long n, long lo
     }
 }
 
+// workgroups per CU of the fused log-mel (mode 3) / MFCC (mode 4) kernel with `dyn` bytes of dynamic LDS
+extern "C" int lab_mel_occupancy(int mode, long long dyn) {
+    int per_cu = -1;
+    const void* k = mode == 3 ? (const void*)vvh::k_stft_pair<1024, 3, 4> : (const void*)vvh::k_stft_pair<1024, 4, 4>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, (size_t)dyn) != hipSuccess) return -2;
+    return per_cu;
+}
+
 extern "C" int stftmagr32lab_run(int exp, const float* sig, long long n, long long nch, const float* win, float* out,
                                  void* stream) {
     hipStream_t s = (hipStream_t)stream;
