@@ -361,9 +361,10 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
         }
     }
     const int nr = (nc + T - 1) / T;   // rounds holding chunks (wave-uniform)
-    float la[2], lb[2];
+    float la[2] = {0.0f, 0.0f}, lb[2] = {0.0f, 0.0f};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+        if (T * u >= M) break;   // no filter in this round (M <= 64): skip its reduction and logf
         const int m = t + T * u;
         const bool on = m < M;
         const int cb = on ? sCb[m] : 0, ce = on ? sCb[m + 1] : 0;
