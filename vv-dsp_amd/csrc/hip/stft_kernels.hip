@@ -368,12 +368,7 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
         const int m = t + T * u;
         const bool on = m < M;
         const int cb = on ? sCb[m] : 0, ce = on ? sCb[m + 1] : 0;
-        int kmax = ce - cb;   // the wave's longest filter (in chunks) sets the trip count
-#pragma unroll
-        for (int sh = 32; sh >= 1; sh >>= 1) {
-            const int o = __shfl_xor(kmax, sh, 64);
-            kmax = o > kmax ? o : kmax;
-        }
+        const int kmax = mel.kmax[u];   // the round's longest filter (in chunks, from the plan) sets the trip count
         float e0 = 0.0f, e1 = 0.0f;
         for (int k = 0; k < kmax; ++k) {   // chunk cb + k of this lane's filter, in order
             const int c = cb + k < ce ? cb + k : 0;
@@ -419,7 +414,7 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
             float res = 0.0f;
             float* dst = snk;
             if (idx < 2 * C) {
-                const int f = idx / C, i = idx - f * C;
+                const int f = idx >= C ? 1 : 0, i = idx - f * C;
                 const float* l = lm + f * M;
                 const float* d = sD + i * M;
                 float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
@@ -428,10 +423,11 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
 #pragma unroll 5
                     for (; m < M; m += 4) {
                         const vf4_t a = *reinterpret_cast<const vf4_t*>(l + m);
-                        c0 = __builtin_fmaf(a[0], d[m], c0);
-                        c1 = __builtin_fmaf(a[1], d[m + 1], c1);
-                        c2 = __builtin_fmaf(a[2], d[m + 2], c2);
-                        c3 = __builtin_fmaf(a[3], d[m + 3], c3);
+                        const vf4_t b = *reinterpret_cast<const vf4_t*>(d + m);   // 16 B aligned: M % 4 == 0
+                        c0 = __builtin_fmaf(a[0], b[0], c0);
+                        c1 = __builtin_fmaf(a[1], b[1], c1);
+                        c2 = __builtin_fmaf(a[2], b[2], c2);
+                        c3 = __builtin_fmaf(a[3], b[3], c3);
                     }
                 } else {
                     for (; m + 1 < M; m += 2) {
