@@ -522,7 +522,7 @@ CASES = {
     **{f"lab60_{e}": (lambda e=e: case_lab(e, nch=1, seconds=60)) for e in (0, 2, 4, 6, 8, 10, 14, 32782, 65550, 98318)},
     **{f"empty{g}": (lambda g=g: case_empty(g)) for g in (703, 2048)},
     **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
-       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026, 128, 256, 131072)},
+       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026, 128, 256, 131072, 262144)},
     **{f"powlab{e}": (lambda e=e: case_lab(e, fn="stftpowlab_run", row=513)) for e in (0, 2, 4, 131072)},
     **{f"powr32lab{e}": (lambda e=e: case_lab(e, fn="stftpowr32lab_run", row=513)) for e in (0, 2, 4, 6)},
     **{f"magr32lab{e}": (lambda e=e: case_lab(e, fn="stftmagr32lab_run")) for e in (0, 2, 4, 6)},

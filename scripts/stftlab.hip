@@ -466,7 +466,7 @@ extern "C" int stftlab5_run(int exp, const float* sig, long long n, long long nc
     switch (exp) {
 #define C(E) case E: return (int)vvh::lab_launch5<E>(sig, n, nch, win, out, s);
         C(0) C(2) C(4) C(6) C(8) C(10) C(16) C(18) C(32) C(34) C(512) C(514) C(1024) C(1026) C(128) C(256)
-        C(131072)
+        C(131072) C(262144)
 #undef C
         default: return -1;
     }
