@@ -613,14 +613,17 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     unsigned* const ctr = DYN ? ctrs + 32 * stream : nullptr;
     // DB = 2^dbs consecutive items per stream and band (VAR 5: log2 in chunk's low bits)
     const int dbs = DRING ? (int)(chunk & 15) : 6;
-    // EXP bit 18 (probe): each XCD group walks its own contiguous eighth of the
-    // runs (its F slot streams banded inside it) instead of one chip-wide band in
-    // which every XCD owns 4 MB of each 32 MB -- the write probe's best layout
-    // (scripts/membench.hip k_wprobe BAND 1); a stream past its eighth is done
+    // Each XCD group walks its own contiguous eighth of the runs (its F slot
+    // streams banded inside it) -- the write probe's best layout (scripts/
+    // membench.hip k_wprobe BAND 1: 0.896 of peak for pure writes against 0.840
+    // for 2 MB chunks dealt round robin); a stream past its eighth is done.
+    // 3.2967 -> 3.2556 ms for the config-5 shard, same buffers, bit-identical
+    // (profiles/r04_kbench_xcd_eighths.jsonl).  EXP bit 18 (lab): round 3's one
+    // chip-wide band in which every XCD owns 4 MB of each 32 MB.
     const long long nrun = DYN ? (pairs + rl - 1) / rl : 0, r8 = (nrun + 7) / 8;
     auto band_pair = [&](unsigned k) -> long long {
         const long long DB = 1LL << dbs;
-        if constexpr ((EXP & 262144) != 0) {
+        if constexpr ((EXP & 262144) == 0) {
             const long long g = stream / F, sl = stream % F;   // wave-uniform (stream is readfirstlane'd)
             const long long it = g * r8 + (long long)(k >> dbs) * (F * DB) + sl * DB + (long long)(k & (DB - 1));
             const long long ge = (g + 1) * r8 < nrun ? (g + 1) * r8 : nrun;
