@@ -515,7 +515,7 @@ CASES = {
     "stft256ch": lambda: case_stft(256, 600),
     **{f"place_i{i}_o{o}": (lambda i=i, o=o: case_stft_place(i, o))
        for i in (0, 4, 64, 1024, 2052) for o in (0, 4, 8, 64, 1024, 2052, 4100)},
-    **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2, 4, 6, 8)},
+    **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2, 4, 6, 8, 16)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
     **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
                                                                           256, 258, 266, 512, 768, 1536, 1792)},

@@ -346,6 +346,7 @@ extern "C" int c2clab_run(int exp, const void* in, void* out, long long batch, v
         case 4: return (int)vvh::lab_c2c<4>((const float2*)in, (float2*)out, batch, s);
         case 6: return (int)vvh::lab_c2c<6>((const float2*)in, (float2*)out, batch, s);
         case 8: return (int)vvh::lab_c2c<8>((const float2*)in, (float2*)out, batch, s);
+        case 16: return (int)vvh::lab_c2c<16>((const float2*)in, (float2*)out, batch, s);
         default: return -1;
     }
 }

@@ -50,19 +50,26 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
-    const long long stride = (long long)gridDim.x * F;
+    long long stride = (long long)gridDim.x * F;
     long long f = uni<G::T>((long long)blockIdx.x * F + slot);
+    long long fend = batch;
+    if constexpr ((EXP & 16) != 0) {   // probe: each XCD group walks a contiguous eighth of the batch
+        xcd_walk(batch, F, slot, &f, &fend, &stride);
+        f = uni<G::T>(f);
+        fend = uni<G::T>(fend);
+        stride = uni<G::T>(stride);
+    }
     float2 nx[G::P];
-    if (f < batch) {
+    if (f < fend) {
 #pragma unroll
         for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(in + f * in_dist + t + r * G::T);
     }
-    for (; f < batch; f += stride) {
+    for (; f < fend; f += stride) {
         float2 v[G::P];
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = nx[r];
         const long long fn = f + stride;
-        if (fn < batch) {
+        if (fn < fend) {
 #pragma unroll
             for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(in + fn * in_dist + t + r * G::T);
         }
@@ -137,20 +144,21 @@ k_r2c(const float* in, float2* out, long long batch, long long in_dist, long lon
     const PostTab<M> pw{lpost};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
-    const long long stride = (long long)gridDim.x * F;
+    long long stride = (long long)gridDim.x * F;
     long long f = uni<G::T>((long long)blockIdx.x * F + slot);
+    long long fend = batch;
     float2 nx[G::P];
-    if (f < batch) {
+    if (f < fend) {
         const float2* src = reinterpret_cast<const float2*>(in + f * in_dist);
 #pragma unroll
         for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(src + t + r * G::T);
     }
-    for (; f < batch; f += stride) {
+    for (; f < fend; f += stride) {
         float2 v[G::P];
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = nx[r];
         const long long fn = f + stride;
-        if (fn < batch) {
+        if (fn < fend) {
             const float2* src = reinterpret_cast<const float2*>(in + fn * in_dist);
 #pragma unroll
             for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(src + t + r * G::T);
