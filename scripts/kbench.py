@@ -571,7 +571,7 @@ CASES = {
     "firstatic": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_DYN", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "firr16": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_R32", "0"),
-    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 16, 32, 64, 128, 96, 192, 18, 34, 256, 258, 288, 290)},
+    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 16, 32, 64, 128, 96, 192, 18, 34, 256, 258, 288, 290, 768)},
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),
     "ola": lambda: case_ola(),

@@ -382,7 +382,7 @@ extern "C" int firr32lab_run(int exp, const void* H, const float* x, float* y, l
     switch (exp) {
 #define C(E) case E: return (int)vvh::lab_firr32<E>(h, x, y, n, nch, s);
         C(0) C(2) C(4) C(6) C(8) C(10) C(12) C(16) C(32) C(64) C(128) C(96) C(192) C(18) C(34)
-        C(256) C(258) C(288) C(290)
+        C(256) C(258) C(288) C(290) C(768)
 #undef C
         default: return -1;
     }

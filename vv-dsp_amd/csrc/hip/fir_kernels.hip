@@ -431,7 +431,8 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // FFT, bit 2 no stores, bit 3 no loads; walks: bit 4 non-persistent chunks of 8
 // couples per wave (the launcher sizes the grid), bit 5 the dynamic band walk
 // of k_fir_bulk_reg (counters in `ctrs`); bit 6 plain output stores, bit 7
-// plain block-a loads.
+// plain block-a loads; bit 9 one grid-wide interleaved front instead of the
+// per-XCD eighths.
 // PAIRED (the launcher's choice for 8 B aligned channels): bulk samples move as 8 B per lane -- a block's 1024 inputs as 16
 // dwordx2 loads (rows 0..7 of block b are rows 24..31 of block a: 12 more), its
 // 768 outputs as 12 dwordx2 stores -- each pair of dwords re-laid by one
@@ -479,8 +480,15 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         it_step = 0;
         if (it < it_end && lane == 0) rk = atomicAdd(ctr, 1u);
     } else {
-        if constexpr (EXP & 16) work_walk(couples, F, slot, 8 * F, &it, &it_end, &it_step);
-        else xcd_walk(couples, F, slot, &it, &it_end, &it_step);
+        if constexpr (EXP & 16) {
+            work_walk(couples, F, slot, 8 * F, &it, &it_end, &it_step);
+        } else if constexpr (EXP & 512) {   // probe: one grid-wide interleaved front (k_c2c's walk)
+            it = (long long)blockIdx.x * F + slot;
+            it_end = couples;
+            it_step = (long long)gridDim.x * F;
+        } else {
+            xcd_walk(couples, F, slot, &it, &it_end, &it_step);
+        }
         it = uni<64>(it);
         it_end = uni<64>(it_end);
         it_step = uni<64>(it_step);
