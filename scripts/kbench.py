@@ -549,6 +549,7 @@ CASES = {
     **{f"stftcdr{r}": with_env(with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_DYN", "2"),
                                "VVHIP_STFT_RUN", str(r)) for r in (2, 4)},
     "stftchunk256ch": with_env(lambda: case_stft(256, 600), "VVHIP_STFT_DYN", "0"),
+    **{f"stftdbs{d}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DBS", str(d)) for d in (3, 4, 5, 7, 8)},
     "stftpowspan": with_env(lambda: case_stft_power(32, 600), "VVHIP_STFT_RING", "0"),
     "stftcspan": with_env(lambda: case_stft(8, 600, complex_out=True), "VVHIP_STFT_RING", "0"),
     "stft60span": with_env(lambda: case_stft(1, 60), "VVHIP_STFT_RING", "0"),
