@@ -247,3 +247,33 @@ def test_filtfilt_argument_checks(cpu_lib, ref):
                                        C.c_size_t(8)) == ERR_NULL
         assert lib.vv_dsp_filtfilt_fir(h.ctypes.data_as(C.c_void_p), C.c_size_t(0), x.ctypes.data_as(C.c_void_p),
                                        y.ctypes.data_as(C.c_void_p), C.c_size_t(8)) == ERR_SIZE
+
+
+def test_knob_registry_without_gpu():
+    """The A/B knobs and path counters (csrc/hip/debug.hip) through the C-ABI,
+    no GPU needed: every documented knob can be set, read back and cleared
+    (-1 = unset, the launcher's default path); counters read as integers and
+    clear to 0; unknown names and negative values are refused; the VVHIP_
+    prefix is accepted."""
+    import vvdsp_amd as vv
+    knobs = ["STFT_CPS", "STFT_RUN", "STFT_DBS", "POW_OLD", "STFT_RING", "STFT_DYN", "FS_VAR", "FS_CHUNK_MB",
+             "FS_OLD", "BLUE_UNFUSED", "C2C_MAX", "STFT_SQ", "MIX_VAR", "MIX_CHUNK_MB", "MIX_R2C_FULL", "FIR_OLD",
+             "FIR_DYN", "FIR_DIRECT_LDS", "FIR_BLOCK", "HOST_CHUNK_MB", "NO_MIXED", "REAL_PROMOTE", "ISTFT_OLD",
+             "MEL_FUSED", "CZT_UNFUSED", "CEPS_UNFUSED", "FIR_R32", "DIST_SLAB_KB", "POW_R32", "MAG_R32"]
+    try:
+        for i, k in enumerate(knobs):
+            vv.debug_set(k, i + 1)
+            assert vv.debug_get(k) == i + 1
+            assert vv.debug_get("VVHIP_" + k) == i + 1
+            vv.debug_clear(k)
+            assert vv.debug_get(k) == -1
+        for st in ("STAT_STFT_DYN", "STAT_FIR_DYN", "STAT_FIR_STATIC", "STAT_MEL_FUSED", "STAT_MEL_SPLIT",
+                   "STAT_FIR_R32", "STAT_POW_R32", "STAT_MAG_R32"):
+            vv.debug_clear(st)
+            assert vv.debug_get(st) == 0
+        for bad in ("NOT_A_KNOB", "STFT_HALF", "FIR_REG", "MEL_OLD", "C2C_R32"):   # removed in round 4
+            with pytest.raises(vv.VvError):
+                vv.debug_get(bad)
+        assert vv.lib().vvhip_debug_set(b"STFT_DYN", -3) != 0
+    finally:
+        vv.debug_clear(None)
