@@ -18,8 +18,12 @@ overlap-save 257 taps, 8 ch x 2^24) GB/s, and the reference's own CPU STFT
 (oracle/_ref, i.e. the reference sources compiled in the build container) timed
 on this host's cores on a bounded sample.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: one process drives N GPUs)
+    torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU)
+Both N > 1 forms run through the library's plain-C RCCL layer
+(include/vv_dsp/vv_dsp_dist.h): ncclCommInitAll in one process, or
+ncclCommInitRank per torchrun rank; `--gpus N` on a box with fewer than N
+visible GPUs exits non-zero.
 """
 import argparse
 import concurrent.futures as cf
@@ -38,7 +42,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "vv-dsp_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import vvdsp_amd as vv  # noqa: E402
-import vvdsp_dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 NFFT, HOP = 1024, 256
@@ -351,44 +354,6 @@ def hbm_traffic(channels):
     return kernel_traffic(["vvh::k_stft_pair<1024, 0, 5"], channels=channels)
 
 
-def gather_leg(out, total_ch, compute_s, frames_per_step, rank, half=True):
-    """One timed RCCL gather (torch.distributed nccl backend = RCCL, point to
-    point over xGMI) of every rank's [ch][frame][1024] rows to rank 0.  With
-    `half` (default) each rank sends bins 0..512 only (vv_dsp_spectrogram_pack_
-    half_device) and rank 0 expands them by mirror symmetry
-    (vv_dsp_spectrogram_unpack_half_device) -- bit-identical rows for half the
-    xGMI bytes (SURVEY 8e row note 1); the timed region covers pack, gather
-    and expand."""
-    try:
-        full = None
-        if rank == 0:
-            full = torch.empty((total_ch,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        if half:
-            vvdsp_dist.gather_rows_half(out, total_ch, NFFT, dst=0, out=full)
-        else:
-            vvdsp_dist.gather_rows(out, total_ch, dst=0, out=full)
-        torch.cuda.synchronize()
-        dist.barrier()
-        g = time.perf_counter() - t0
-        t = torch.tensor([g], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        g = float(t.item())
-        row_bins = NFFT // 2 + 1 if half else NFFT
-        gathered = (total_ch - out.shape[0]) * out.shape[1] * row_bins * out.element_size()
-        del full
-        return {"gather_s": round(g, 4), "bins_sent": row_bins, "bytes_into_rank0": gathered,
-                "xgmi_GBs_into_rank0": round(gathered / g / 1e9, 1),
-                "frames_per_s_with_gather": round(frames_per_step / (compute_s + g), 1),
-                "note": "one step of compute + one gather of every rank's magnitude rows to rank 0 "
-                        + ("(bins 0..512 packed on each rank, expanded to 1024 on rank 0, bit-identical)"
-                           if half else "(all 1024 bins)")}
-    except Exception as e:  # report, do not lose the bench line
-        return {"error": repr(e)[:300]}
-
-
 def shard_leg(ch=CH_SHARD, steps=20, warm=10):
     """Config 5's per-GPU shard at 8 GPUs -- 32 ch x 10 min @ 48 kHz, 18.4 GB in
     + out -- on one GPU: what each rank of the driver's N = 8 run computes.  Same
@@ -424,9 +389,12 @@ def hann64():
                      for i in range(NFFT)], np.float64)
 
 
-def main():
+def parse_args():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (default 1).  Without torchrun (no WORLD_SIZE) N > 1 runs every GPU "
+                         "from this one process over the library's plain-C RCCL layer (vv_dsp_dist_init_all); "
+                         "under torchrun it must equal WORLD_SIZE (one rank per GPU, vv_dsp_dist_init_rank)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=25)
     ap.add_argument("--channels", type=int, default=CH_TOTAL,
@@ -442,78 +410,42 @@ def main():
     ap.add_argument("--gather", choices=["auto", "on", "off"], default="auto",
                     help="after the timed steps, time one RCCL gather of all spectrogram rows to rank 0 "
                          "(config 5 'with gather'; auto = on when N > 1)")
-    args = ap.parse_args()
+    ap.add_argument("--dist-c", action="store_true",
+                    help="run N = 1 through the multi-GPU layer too (vv_dsp_dist_init_all over one device): "
+                         "the N > 1 code path on a one-GPU box")
+    return ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    if vv.device_count() <= 0:
-        raise SystemExit("libvvdsp_amd.so sees no HIP device")
 
-    # ---- this rank's shard of the job: channels [lo, hi) (contiguous, sizes differ by <= 1) ----
-    total_ch = args.channels
-    lo, hi = vvdsp_dist.channel_shard(total_ch, world, rank)
-    C_ = hi - lo
-    nfr = frames_of(SAMPLES)
-    sig = torch.empty(C_, SAMPLES, device="cuda")
-    for c in range(C_):
-        g = torch.Generator(device="cuda").manual_seed(lo + c)
-        sig[c].uniform_(-1.0, 1.0, generator=g)
-    out = torch.empty(C_, nfr, NFFT, device="cuda")
-    st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
+def launch_mode(args):
+    """("plain", 1): today's single-GPU line; ("node", N): one process drives N
+    GPUs (ncclCommInitAll); ("ranks", N): torchrun, one process per GPU.
+    Never re-launches anything: a process that has touched the GPU must not exec."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and (int(env_world) > 1 or args.dist_c):
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return "ranks", world
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}")
+    visible = torch.cuda.device_count()   # counts devices without initialising them
+    if visible < n:
+        raise SystemExit(f"bench.py: --gpus {n} asks for {n} GPUs but this process sees {visible}; "
+                         f"refusing to report an {n}-GPU number from fewer devices")
+    return ("node", n) if (n > 1 or args.dist_c) else ("plain", 1)
 
-    def step():
-        st.spectrogram(sig, out=out)
 
-    for _ in range(args.warmup):
-        step()
-    # kernel duration for the roofline: events around each launch on the launch stream
-    s = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(s)
-        step()
-        b.record(s)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+def main():
+    args = parse_args()
+    mode, world = launch_mode(args)
+    if mode == "plain":
+        return main_plain(args)
+    return main_dist(args, mode, world)
 
-    frames_total = total_ch * nfr * args.steps      # every rank's frames
-    value = frames_total / elapsed
-    bytes_per_launch = C_ * SAMPLES * 4 + C_ * nfr * NFFT * 4 + NFFT * 4
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
 
-    traffic, traffic_src = hbm_traffic(C_)
-
-    # spot-check one frame row of the first and last channel against NumPy f64
-    # so a fast-but-wrong kernel cannot report
-    fr = 12345
-    ok = True
-    for c in (0, C_ - 1):
-        x0 = sig[c, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
-        ok = ok and np.allclose(out[c, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * hann64())), rtol=5e-5, atol=5e-5)
-    gather = None
-    if world > 1 and (args.gather == "on" or args.gather == "auto"):
-        gather = gather_leg(out, total_ch, elapsed / args.steps, frames_total / args.steps, rank,
-                            half=args.gather_bins == "half")
-    del sig, out, st
-    torch.cuda.empty_cache()
-
-    res = {
+def result_line(args, value, world, elapsed, total_ch, per_gpu, nfr, parallelism, roofline, ok):
+    return {
         "metric": METRIC,
         "value": round(value, 1),
         "unit": "frames/s",
@@ -532,26 +464,85 @@ def main():
         "config": {
             "workload": f"config5: multi-channel STFT magnitude, {total_ch} ch x 10 min @ 48 kHz "
                         f"({total_ch * nfr:,} frames per step), nfft 1024 Hann, hop 256; strong scaling: "
-                        f"{C_} ch on this rank" + (" (the whole job on one GPU)" if world == 1 else ""),
-            "channels_total": total_ch, "channels_per_gpu": C_, "samples_per_channel": SAMPLES,
+                        + (f"{per_gpu} ch per GPU" if world > 1 else f"{per_gpu} ch on this rank")
+                        + (" (the whole job on one GPU)" if world == 1 else ""),
+            "channels_total": total_ch, "channels_per_gpu": per_gpu, "samples_per_channel": SAMPLES,
             "frames_per_channel": nfr, "frames_per_step": total_ch * nfr,
             "nfft": NFFT, "hop": HOP, "window": "hann (symmetric, window.c:25-36)",
             "output": "[ch][frame][1024] f32 magnitudes (stft.c:133-139)",
-            "parallelism": f"dp{world} (channel shards, no data-path collective)"},
-        "roofline": {"kernel": "vvh::k_stft_pair<1024,0,5> (persistent dynamic band walk in runs of 2 pairs; LDS-DMA frame spans kept as a ring of 256-float chunks + "
-                               "Hann + two frames per 1024-pt complex FFT + |X| rows as full-line streaming stores; "
-                               "the zero-padded tail pairs run in the same launch); kernel_ms = HIP events around "
-                               f"each of the {args.steps} timed launches on the launch stream ({C_} channels per launch)",
-                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "bytes_per_launch": bytes_per_launch, "kernel_ms": round(kern_ms, 4)},
+            "parallelism": parallelism},
+        "roofline": roofline,
         "check_row_vs_numpy_f64": bool(ok),
     }
-    if gather is not None:
-        res["with_gather"] = gather
+
+
+ROOFLINE_KERNEL = ("vvh::k_stft_pair<1024,0,5> (persistent dynamic band walk in runs of 2 pairs; LDS-DMA frame "
+                   "spans kept as a ring of 256-float chunks + Hann + two frames per 1024-pt complex FFT + |X| rows "
+                   "as full-line streaming stores; the zero-padded tail pairs run in the same launch)")
+
+
+def check_rows(sig, out, channels):
+    """one frame row of the given channels against NumPy f64, so a fast-but-wrong
+    kernel cannot report"""
+    fr, ok = 12345, True
+    for c in channels:
+        x0 = sig[c, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
+        ok = ok and np.allclose(out[c, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * hann64())), rtol=5e-5, atol=5e-5)
+    return ok
+
+
+def main_plain(args):
+    """N = 1 (no torchrun): the whole job on cuda:0 through the single-GPU API."""
+    torch.cuda.set_device(0)
+    if vv.device_count() <= 0:
+        raise SystemExit("libvvdsp_amd.so sees no HIP device")
+    total_ch = args.channels
+    C_ = total_ch
+    nfr = frames_of(SAMPLES)
+    sig = torch.empty(C_, SAMPLES, device="cuda")
+    for c in range(C_):
+        g = torch.Generator(device="cuda").manual_seed(c)
+        sig[c].uniform_(-1.0, 1.0, generator=g)
+    out = torch.empty(C_, nfr, NFFT, device="cuda")
+    st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
+
+    def step():
+        st.spectrogram(sig, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    # kernel duration for the roofline: events around each launch on the launch stream
+    s = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(s)
+        step()
+        b.record(s)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    frames_total = total_ch * nfr * args.steps
+    value = frames_total / elapsed
+    bytes_per_launch = C_ * SAMPLES * 4 + C_ * nfr * NFFT * 4 + NFFT * 4
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = hbm_traffic(C_)
+    ok = check_rows(sig, out, (0, C_ - 1))
+    del sig, out, st
+    torch.cuda.empty_cache()
+
+    roof = {"kernel": ROOFLINE_KERNEL + "; kernel_ms = HIP events around "
+                      f"each of the {args.steps} timed launches on the launch stream ({C_} channels per launch)",
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "bytes_per_launch": bytes_per_launch, "kernel_ms": round(kern_ms, 4)}
+    res = result_line(args, value, 1, elapsed, total_ch, C_, nfr,
+                      "dp1 (channel shards, no data-path collective)", roof, ok)
     legs = set(args.legs.split(","))
-    if rank == 0 and not args.no_extras and world == 1:
+    if not args.no_extras:
         if "shard" in legs:
             res["config5_shard_32ch"] = shard_leg()
             torch.cuda.empty_cache()
@@ -564,13 +555,204 @@ def main():
         if "config3" in legs:
             res["stft_config3"] = stft_config3()
             torch.cuda.empty_cache()
-    if rank == 0 and not args.no_extras and not args.no_cpu and world == 1:
+    if not args.no_extras and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline()
-    if rank == 0:
+    print(json.dumps(res), flush=True)
+
+
+def main_dist(args, mode, world):
+    """N GPUs through the library's plain-C multi-GPU layer (vv_dsp_dist.h):
+    mode "node": this one process drives all N GPUs (vv_dsp_dist_init_all =
+    ncclCommInitAll), launching each rank's channel shard on its own device's
+    stream (vv_dsp_dist_stft); mode "ranks": torchrun's one process per GPU,
+    each a one-slot context of a communicator made by vv_dsp_dist_init_rank
+    (ncclCommInitRank; the 128-byte id and the barriers / max-over-ranks go over
+    torch.distributed's gloo group -- rendezvous only, no data).  The timed
+    region is K steps of the sharded STFT (no data-path collective: channels are
+    independent, stft.c:112-144 per channel); the gather of every rank's rows to
+    rank 0 (ncclSend/ncclRecv slabs, half-spectrum rows) is timed after it as
+    `with_gather`."""
+    total_ch = args.channels
+    nfr = frames_of(SAMPLES)
+    if mode == "node":
+        rank0, local = 0, 0
+        devs = list(range(world))
+        d = vv.Dist.all(devs)
+        torch.cuda.set_device(0)
+    else:
+        rank0 = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank0 == 0:
+            uid.copy_(torch.frombuffer(bytearray(vv.Dist.unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        d = vv.Dist.rank(world, rank0, bytes(uid.tolist()), local)
+    if vv.device_count() <= 0:
+        raise SystemExit("libvvdsp_amd.so sees no HIP device")
+    rccl_ranks = d.comm_count(0)
+    if rccl_ranks != world:
+        raise SystemExit(f"bench.py: RCCL reports {rccl_ranks} ranks, expected {world}")
+
+    # ---- every local slot's shard: channels [lo, lo + cnt) on its device ----
+    slots = []
+    root_slot = None
+    full = None
+    want_gather = world > 1 and args.gather in ("auto", "on") or args.gather == "on"
+    for s in range(d.slots):
+        r, w, dev = d.rank_info(s)
+        lo, cnt = vv.shard_range(total_ch, w, r)
+        with torch.cuda.device(dev):
+            sig = torch.empty(cnt, SAMPLES, device=dev)
+            for c in range(cnt):
+                g = torch.Generator(device=torch.device("cuda", dev)).manual_seed(lo + c)
+                sig[c].uniform_(-1.0, 1.0, generator=g)
+            if r == 0 and want_gather:
+                # the root's rows are written in place inside the gathered output
+                full = torch.empty(total_ch, nfr, NFFT, device=dev)
+                out = full[lo:lo + cnt]
+                root_slot = s
+            else:
+                out = torch.empty(cnt, nfr, NFFT, device=dev)
+        slots.append({"rank": r, "dev": dev, "lo": lo, "cnt": cnt, "sig": sig, "out": out,
+                      "stream": torch.cuda.current_stream(dev)})
+    st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
+
+    def step():
+        d.stft(st, [x["sig"] for x in slots], SAMPLES, total_ch, SAMPLES, [x["out"] for x in slots],
+               streams=[x["stream"] for x in slots])
+
+    def sync_all():
+        for x in slots:
+            torch.cuda.synchronize(x["dev"])
+
+    def barrier():
+        if mode == "ranks":
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if mode != "ranks":
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    for _ in range(args.warmup):
+        step()
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in slots]
+          for _ in range(args.steps)]
+    sync_all()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        for x, (a, _) in zip(slots, ev[k]):
+            a.record(x["stream"])
+        step()
+        for x, (_, b) in zip(slots, ev[k]):
+            b.record(x["stream"])
+    sync_all()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    # per-device kernel time (HIP events on each device's launch stream); the
+    # roofline is quoted on the slowest device of the job
+    per_dev = []
+    for i, x in enumerate(slots):
+        ms = float(np.mean([ev[k][i][0].elapsed_time(ev[k][i][1]) for k in range(args.steps)]))
+        byts = x["cnt"] * SAMPLES * 4 + x["cnt"] * nfr * NFFT * 4 + NFFT * 4
+        per_dev.append((ms, byts, x["rank"], x["dev"], x["cnt"]))
+    slow = max(per_dev)
+    if mode == "ranks":
+        t = torch.tensor([slow[0], slow[1], slow[2], slow[3], slow[4]], dtype=torch.float64)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per_dev = [tuple(float(v) for v in a.tolist()) for a in allt]
+        slow = max(per_dev)
+    kern_ms, bytes_per_launch = slow[0], int(slow[1])
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+
+    frames_per_step = total_ch * nfr
+    value = frames_per_step * args.steps / elapsed
+    ok = all(check_rows(x["sig"], x["out"], (0, x["cnt"] - 1)) for x in slots if x["cnt"])
+    if mode == "ranks":
+        t = torch.tensor([1.0 if ok else 0.0])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item() > 0.5)
+
+    gather = None
+    if want_gather:
+        gather = dist_gather_leg(d, slots, root_slot, full, total_ch, nfr, elapsed / args.steps,
+                                 frames_per_step, half=args.gather_bins == "half", sync_all=sync_all,
+                                 barrier=barrier, max_over_ranks=max_over_ranks)
+    per_gpu = max(x[4] for x in per_dev)
+    roof = {"kernel": ROOFLINE_KERNEL + f"; kernel_ms = HIP events around each of the {args.steps} timed launches "
+                                        "on every device's launch stream, the slowest device's average",
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "traffic_source": f"PMC summaries are taken on the one-GPU box ({TRAFFIC_JSON and os.path.basename(TRAFFIC_JSON)}, "
+                              "256 channels per launch); not collected for this shard size",
+            "bytes_per_launch": bytes_per_launch, "kernel_ms": round(kern_ms, 4),
+            "per_device": [{"rank": int(r), "device": int(dv), "channels": int(c), "kernel_ms": round(m, 4),
+                            "frac": round(b / (m * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                           for (m, b, r, dv, c) in sorted(per_dev, key=lambda x: x[2])]}
+    launch = (f"one process driving {world} GPUs (vv_dsp_dist_init_all = ncclCommInitAll; one launch per device "
+              "per step, vv_dsp_dist_stft)" if mode == "node" else
+              f"torchrun: {world} processes, one GPU each (vv_dsp_dist_init_rank = ncclCommInitRank; "
+              "gloo for the id broadcast, barriers and max-over-ranks)")
+    res = result_line(args, value, world, elapsed, total_ch, per_gpu, nfr,
+                      f"dp{world} (channel shards, no data-path collective)", roof, ok)
+    res["rccl_ranks"] = rccl_ranks
+    res["launch"] = launch
+    if gather is not None:
+        res["with_gather"] = gather
+    if rank0 == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    del slots, full
+    del d
+    if mode == "ranks":
         dist.barrier()
         dist.destroy_process_group()
+
+
+def dist_gather_leg(d, slots, root_slot, full, total_ch, nfr, compute_s, frames_per_step, half, sync_all, barrier,
+                    max_over_ranks):
+    """One timed vv_dsp_dist_gather_rows of every rank's [ch][frame][1024] rows
+    into rank 0's [256][frame][1024] output (grouped ncclSend / ncclRecv slabs over
+    xGMI, each peer on its own link into the root).  `half`: each rank packs bins
+    0..512 and the root expands them by mirror symmetry -- bit-identical rows for
+    half the xGMI bytes (SURVEY 8e row note 1).  Checked afterwards: sampled rows
+    of every rank equal the rank's own rows bit for bit."""
+    try:
+        sync_all()
+        barrier()
+        t0 = time.perf_counter()
+        d.gather_rows([x["out"] for x in slots], total_ch, nfr, NFFT, full, root=0, half=half,
+                      streams=[x["stream"] for x in slots])
+        sync_all()
+        barrier()
+        g = max_over_ranks(time.perf_counter() - t0)
+        row_bins = NFFT // 2 + 1 if half else NFFT
+        root_ch = vv.shard_range(total_ch, d.rank_info(0)[1], 0)[1]
+        gathered = (total_ch - root_ch) * nfr * row_bins * 4
+        res = {"gather_s": round(g, 4), "bins_sent": row_bins, "bytes_into_rank0": gathered,
+               "xgmi_GBs_into_rank0": round(gathered / g / 1e9, 1),
+               "frames_per_s_with_gather": round(frames_per_step / (compute_s + g), 1),
+               "note": "one step of compute + one vv_dsp_dist_gather_rows of every rank's magnitude rows to rank 0 "
+                       + ("(bins 0..512 packed on each rank, expanded to 1024 on rank 0, bit-identical)"
+                          if half else "(all 1024 bins)")}
+        if full is not None and len(slots) > 1:   # one process holds every rank's rows: check them
+            same = True
+            for x in slots:
+                for c in sorted({0, x["cnt"] // 2, x["cnt"] - 1}):
+                    for f in (0, 12345, nfr - 1):
+                        a = full[x["lo"] + c, f].cpu()
+                        b = x["out"][c, f].cpu()
+                        same = same and torch.equal(a, b)
+            res["rows_bit_identical_after_gather"] = bool(same)
+        return res
+    except Exception as e:  # report, do not lose the bench line
+        return {"error": repr(e)[:300]}
+
 
 
 if __name__ == "__main__":

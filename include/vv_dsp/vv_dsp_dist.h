@@ -27,8 +27,19 @@ extern "C" {
 
 typedef struct vv_dsp_dist vv_dsp_dist;
 
+#define VV_DSP_DIST_ID_BYTES 128 /* = NCCL_UNIQUE_ID_BYTES */
+
 /* ndev ranks in this process, rank i on devices[i] (ncclCommInitAll). */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_init_all(int ndev, const int* devices, vv_dsp_dist** out);
+/* One process per GPU: rank 0 makes an id (ncclGetUniqueId) and hands its
+ * VV_DSP_DIST_ID_BYTES bytes to every rank by any means (e.g. a broadcast of the
+ * job's launcher); each rank then joins with vv_dsp_dist_init_rank
+ * (ncclCommInitRank, collective over the `world` ranks) with its rank and the
+ * device it runs on.  The communicator is the context's own: vv_dsp_dist_destroy
+ * destroys it. */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_unique_id(unsigned char id[VV_DSP_DIST_ID_BYTES]);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_init_rank(int world, int rank, const unsigned char id[VV_DSP_DIST_ID_BYTES],
+                                                     int device, vv_dsp_dist** out);
 /* One rank of a communicator the caller made (an ncclComm_t passed as void*,
  * e.g. ncclCommInitRank in a one-process-per-GPU job); rank, world size and
  * device are read from it, and vv_dsp_dist_destroy leaves it alone. */
@@ -42,6 +53,13 @@ int vv_dsp_dist_local_ranks(const vv_dsp_dist* d);
 /* local slot s: its rank, the world size and its device */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_rank_info(const vv_dsp_dist* d, int slot, int* rank, int* world,
                                                      int* device);
+/* the rank count RCCL reports for slot s's communicator (ncclCommCount; the
+ * world size for a loopback context) */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_comm_count(const vv_dsp_dist* d, int slot, int* count);
+
+/* Streams: every per-rank `streams` array has one hipStream_t per local slot,
+ * each on that slot's device (OUT_OF_RANGE otherwise; NULL = the device's null
+ * stream).  Work for slot s is enqueued on streams[s] with its device current. */
 
 /* Config 5: each local rank's share of a [total_ch][n] multi-channel STFT --
  * the channels vv_dsp_shard_range(total_ch, world, rank) gives it, d_signal[s]
@@ -58,12 +76,17 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_stft(vv_dsp_dist* d, vv_dsp_stft* h, 
  * spectrogram, rows_per_item = its frames) into d_root_out =
  * [total_items][rows_per_item][row_floats] on rank `root` (ignored on other
  * ranks), in rank = item order, in slabs of at most 256 MiB per rank (a slab
- * may end inside an item).  half != 0: the rows are
- * magnitude (or mirror-symmetric) rows of fft_size = row_floats bins; each rank
- * sends bins 0..fft_size/2 only and the root expands them
+ * may end inside an item; every rank derives the same slab bounds).  The
+ * root's own rows may already sit at their place in d_root_out (no copy then).
+ * half != 0: the rows MUST be mirror-symmetric rows of fft_size = row_floats
+ * bins (row[k] == row[fft_size - k]: magnitude rows of real frames -- never
+ * the fft_size/2+1-wide power rows, which are gathered with half = 0); each
+ * rank sends bins 0..fft_size/2 only and the root expands them
  * (vv_dsp_spectrogram_pack/unpack_half_device): the same rows for half the
- * xGMI bytes.  Stream-ordered on streams[s]: returns once everything is
- * enqueued; the sources must be complete in stream order on streams[s]. */
+ * xGMI bytes.  Stream-ordered: returns once everything is enqueued; the
+ * sources must be complete in stream order on streams[s].  Loopback contexts
+ * run every copy on streams[root], after a device-side wait for each
+ * streams[s]. */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* d_local,
                                                        size_t total_items, size_t rows_per_item, size_t row_floats,
                                                        int half, vv_dsp_real* d_root_out, int root,

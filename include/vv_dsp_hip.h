@@ -77,6 +77,11 @@ int vvhip_memset(void* dst, int value, size_t bytes);
 int vvhip_malloc_async(void** p, size_t bytes, void* stream);
 int vvhip_free_async(void* p, void* stream);
 int vvhip_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream);
+/* the device of a stream (NULL: the current device's null stream), and a
+ * device-side wait of `waiter` for everything enqueued on `producer` so far
+ * (an event on the producer's device; no host synchronisation) */
+int vvhip_stream_device(void* stream, int* device);
+int vvhip_stream_wait(void* waiter, void* producer);
 /* sets the text vvhip_last_error() returns on this thread (host front-end errors) */
 void vvhip_set_error(const char* what);
 int vvhip_stream_sync(void* stream);

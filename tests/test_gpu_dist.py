@@ -1,10 +1,18 @@
 """The plain-C multi-GPU layer (include/vv_dsp/vv_dsp_dist.h, csrc/host/dist.c)
-on the one GPU of the test box, and the Python gathers (vvdsp_dist.py) on a
-world-1 nccl (= RCCL) process group:
+and the Python gathers (vvdsp_dist.py) on a world-1 nccl (= RCCL) process group.
 
-* an RCCL context of one rank (ncclCommInitAll over device 0): the sharded STFT
-  and the gather (full and half-spectrum rows) give the unsharded rows, bit for
-  bit -- RCCL's ncclGroupStart/End path with no peer;
+What runs where:
+* two or more visible GPUs (skipped on the one-GPU test box):
+  `test_rccl_two_devices` -- ncclCommInitAll over devices 0 and 1, 7 uneven
+  channels, roots 0 and 1, full and half rows, 256 MiB and 1500 KiB slabs:
+  the grouped ncclSend / ncclRecv slabs (dist.c, "the transfers of this slab")
+  against the single-call rows, bit for bit; and a stream on the wrong device
+  refused;
+* one GPU: RCCL communicators of ONE rank (ncclCommInitAll over device 0, and
+  ncclGetUniqueId + ncclCommInitRank): the sharded STFT and the gather return
+  before any ncclSend / ncclRecv (a world of one has no peer), so these cover the
+  communicator set-up and the root's own rows only -- RCCL refuses two ranks
+  on one device ("Duplicate GPU detected"), so no send / receive runs here;
 * loopback contexts of 2 and 3 ranks on device 0 (the same slab / offset /
   pack-unpack logic with device copies in place of ncclSend/ncclRecv): uneven
   channel shards (vv_dsp_shard_range), roots 0 and world-1, small slabs;
@@ -50,11 +58,13 @@ def _sharded_rows(d, sig, st, world, kind=0):
     return rows
 
 
-def test_rccl_one_rank_stft_and_gather(job):
+@pytest.mark.parametrize("how", ["init_all", "init_rank"])
+def test_rccl_one_rank_stft_and_gather(job, how):
     import torch
     sig, st, ref = job
-    d = vv.Dist.all([0])
+    d = vv.Dist.all([0]) if how == "init_all" else vv.Dist.rank(1, 0, vv.Dist.unique_id(), 0)
     assert d.slots == 1 and d.rank_info(0) == (0, 1, 0)
+    assert d.comm_count(0) == 1
     rows = _sharded_rows(d, sig, st, 1)
     torch.cuda.synchronize()
     assert torch.equal(rows[0], ref)
@@ -63,6 +73,90 @@ def test_rccl_one_rank_stft_and_gather(job):
         d.gather_rows([rows[0]], NCH, ref.shape[1], 1024, out, root=0, half=half)
         torch.cuda.synchronize()
         assert torch.equal(out, ref)
+    # the root's rows already in place inside the output: nothing moves
+    out = ref.clone()
+    d.gather_rows([out], NCH, ref.shape[1], 1024, out, root=0, half=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+def test_unique_ids_differ():
+    a, b = vv.Dist.unique_id(), vv.Dist.unique_id()
+    assert len(a) == len(b) == 128 and a != b
+
+
+def _two_gpus():
+    import torch
+    return torch.cuda.device_count() >= 2
+
+
+@pytest.mark.skipif(not _two_gpus(), reason="needs two visible GPUs (RCCL refuses two ranks on one device)")
+@pytest.mark.parametrize("root", [0, 1])
+@pytest.mark.parametrize("half", [False, True])
+@pytest.mark.parametrize("slab_kb", [0, 1500])
+def test_rccl_two_devices(job, knob, root, half, slab_kb):
+    """ncclCommInitAll over devices 0 and 1: rank 1's shard lives on device 1,
+    the sends / receives cross xGMI, and the gathered rows on the root equal the
+    unsharded single-call rows bit for bit (1500 KiB slabs end inside a channel)."""
+    import torch
+    sig, st, ref = job
+    if slab_kb:
+        knob("DIST_SLAB_KB", slab_kb)
+    d = vv.Dist.all([0, 1])
+    assert d.slots == 2 and d.comm_count(0) == 2 and d.comm_count(1) == 2
+    assert [d.rank_info(s) for s in range(2)] == [(0, 2, 0), (1, 2, 1)]
+    sl = _shards(NCH, 2)
+    fr = st.frames(N)
+    sigs = [sig[sl[0][0]:sl[0][0] + sl[0][1]], sig[sl[1][0]:sl[1][0] + sl[1][1]].to("cuda:1")]
+    rows = [torch.full((c, fr, 1024), -3.0, device=f"cuda:{i}") for i, (_, c) in enumerate(sl)]
+    assert d.stft(st, sigs, N, NCH, N, rows) == fr
+    for i in range(2):
+        torch.cuda.synchronize(i)
+    for (f, c), r in zip(sl, rows):
+        assert torch.equal(r.to("cuda:0"), ref[f:f + c])
+    out = torch.full(ref.shape, -1.0, device=f"cuda:{root}")
+    d.gather_rows(rows, NCH, fr, 1024, out, root=root, half=half)
+    for i in range(2):
+        torch.cuda.synchronize(i)
+    assert torch.equal(out.to("cuda:0"), ref)
+
+
+@pytest.mark.skipif(not _two_gpus(), reason="needs two visible GPUs")
+def test_rccl_stream_on_wrong_device_refused(job):
+    import torch
+    sig, st, _ = job
+    d = vv.Dist.all([0, 1])
+    s0 = torch.cuda.Stream(device=0)
+    with pytest.raises(vv.VvError, match="device"):
+        d.stft(st, [sig, sig], N, NCH, N, [sig, sig], streams=[s0, s0])
+
+
+def test_loopback_distinct_streams(job):
+    """Each slot writes its rows on its own stream and the gather is enqueued
+    right after, with no host synchronisation: the loopback copies run on the
+    root's stream after a device-side wait for every slot's stream."""
+    import torch
+    sig, st, ref = job
+    world = 3
+    d = vv.Dist.loopback(world)
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    sl = _shards(NCH, world)
+    fr = st.frames(N)
+    for half in (False, True):
+        rows = [torch.full((c, fr, 1024), -3.0, device="cuda") for (_, c) in sl]
+        torch.cuda.synchronize()
+        d.stft(st, [sig[f] for f, _ in sl], N, NCH, N, rows, streams=streams)
+        out = torch.full_like(ref, -1.0)
+        d.gather_rows(rows, NCH, fr, 1024, out, root=1, half=half, streams=streams)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+
+
+def test_half_rows_need_two_bins(job):
+    d = vv.Dist.loopback(2)
+    sig, _, ref = job
+    with pytest.raises(vv.VvError):
+        d.gather_rows([ref, ref], 2, 1, 1, ref, root=0, half=True)
 
 
 @pytest.mark.parametrize("world,root,slab_kb", [(2, 0, 0), (3, 0, 0), (3, 2, 0), (3, 1, 1500), (2, 1, 4097)])

@@ -342,6 +342,31 @@ int vvhip_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* strea
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream), ST_INTERNAL);
     return ST_OK;
 }
+// the device a stream belongs to (the null stream: the current device's)
+int vvhip_stream_device(void* stream, int* device) {
+    if (!device) return ST_NULL;
+    if (device_count() <= 0) return fail(ST_UNSUP, "no HIP device");
+    HIPCHK(hipStreamGetDevice((hipStream_t)stream, device), ST_INTERNAL);
+    return ST_OK;
+}
+// `waiter` waits (on the device) for the work enqueued on `producer` so far:
+// an event recorded on the producer's device, waited on by the waiter; the
+// event is released once it has completed (hipEventDestroy defers)
+int vvhip_stream_wait(void* waiter, void* producer) {
+    if (waiter == producer) return ST_OK;
+    int prev = 0, pdev = 0;
+    HIPCHK(hipGetDevice(&prev), ST_INTERNAL);
+    HIPCHK(hipStreamGetDevice((hipStream_t)producer, &pdev), ST_INTERNAL);
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipSetDevice(pdev);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, (hipStream_t)producer);
+    (void)hipSetDevice(prev);
+    if (e == hipSuccess) e = hipStreamWaitEvent((hipStream_t)waiter, ev, 0);
+    if (ev) (void)hipEventDestroy(ev);
+    HIPCHK(e, ST_INTERNAL);
+    return ST_OK;
+}
 void vvhip_set_error(const char* what) { g_err = what ? what : ""; }
 
 int vvhip_memset(void* dst, int value, size_t bytes) {

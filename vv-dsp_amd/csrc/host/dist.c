@@ -33,6 +33,8 @@
 /* ---- RCCL entry points, resolved at run time ---- */
 static struct {
     ncclResult_t (*init_all)(ncclComm_t*, int, const int*);
+    ncclResult_t (*unique_id)(ncclUniqueId*);
+    ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int);
     ncclResult_t (*destroy)(ncclComm_t);
     ncclResult_t (*group_start)(void);
     ncclResult_t (*group_end)(void);
@@ -56,6 +58,8 @@ static void rccl_load(void) {
         if (!R.field) return;                              \
     } while (0)
     SYM(init_all, "ncclCommInitAll");
+    SYM(unique_id, "ncclGetUniqueId");
+    SYM(init_rank, "ncclCommInitRank");
     SYM(destroy, "ncclCommDestroy");
     SYM(group_start, "ncclGroupStart");
     SYM(group_end, "ncclGroupEnd");
@@ -88,6 +92,8 @@ struct vv_dsp_dist {
     ncclComm_t comm[DIST_MAX_SLOTS];
     int own_comms;   /* created here: destroyed by vv_dsp_dist_destroy */
     int loopback;    /* all ranks in this process on one device, transfers are copies */
+    int one_process; /* every rank of the world is a slot of this context (init_all,
+                        loopback): only then may the slab size follow a per-process knob */
 };
 
 static vv_dsp_dist* dist_new(void) { return (vv_dsp_dist*)calloc(1, sizeof(vv_dsp_dist)); }
@@ -110,6 +116,7 @@ vv_dsp_status vv_dsp_dist_init_all(int ndev, const int* devices, vv_dsp_dist** o
     }
     d->nslots = d->world = ndev;
     d->own_comms = 1;
+    d->one_process = 1;
     for (int i = 0; i < ndev; ++i) {
         d->rank[i] = i;
         d->dev[i] = devices[i];
@@ -139,6 +146,51 @@ vv_dsp_status vv_dsp_dist_from_comm(void* nccl_comm, vv_dsp_dist** out) {
     return VV_DSP_OK;
 }
 
+vv_dsp_status vv_dsp_dist_unique_id(unsigned char id[VV_DSP_DIST_ID_BYTES]) {
+    if (!id) return VV_DSP_ERROR_NULL_POINTER;
+    if (!rccl_ready()) return VV_DSP_ERROR_UNSUPPORTED;
+    ncclUniqueId u;
+    const ncclResult_t e = R.unique_id(&u);
+    if (e != ncclSuccess) return nccl_fail("ncclGetUniqueId", e);
+    memcpy(id, u.internal, VV_DSP_DIST_ID_BYTES);
+    return VV_DSP_OK;
+}
+
+vv_dsp_status vv_dsp_dist_init_rank(int world, int rank, const unsigned char id[VV_DSP_DIST_ID_BYTES], int device,
+                                    vv_dsp_dist** out) {
+    if (!out || !id) return VV_DSP_ERROR_NULL_POINTER;
+    *out = NULL;
+    if (world < 1) return VV_DSP_ERROR_INVALID_SIZE;
+    if (rank < 0 || rank >= world) return VV_DSP_ERROR_OUT_OF_RANGE;
+    const int nd = vvhip_available();
+    if (nd <= 0) return VV_DSP_ERROR_UNSUPPORTED;
+    if (device < 0 || device >= nd) return VV_DSP_ERROR_OUT_OF_RANGE;
+    if (!rccl_ready()) return VV_DSP_ERROR_UNSUPPORTED;
+    vv_dsp_dist* d = dist_new();
+    if (!d) return VV_DSP_ERROR_INTERNAL;
+    ncclUniqueId u;
+    memcpy(u.internal, id, VV_DSP_DIST_ID_BYTES);
+    /* the communicator binds to the current device */
+    int prev = 0;
+    if (vvhip_get_device(&prev) != 0 || vvhip_set_device(device) != 0) {
+        free(d);
+        return VV_DSP_ERROR_INTERNAL;
+    }
+    const ncclResult_t e = R.init_rank(&d->comm[0], world, u, rank);
+    (void)vvhip_set_device(prev);
+    if (e != ncclSuccess) {
+        free(d);
+        return nccl_fail("ncclCommInitRank", e);
+    }
+    d->nslots = 1;
+    d->world = world;
+    d->rank[0] = rank;
+    d->dev[0] = device;
+    d->own_comms = 1;
+    *out = d;
+    return VV_DSP_OK;
+}
+
 vv_dsp_status vv_dsp_dist_init_loopback(int world, int device, vv_dsp_dist** out) {
     if (!out) return VV_DSP_ERROR_NULL_POINTER;
     *out = NULL;
@@ -150,6 +202,7 @@ vv_dsp_status vv_dsp_dist_init_loopback(int world, int device, vv_dsp_dist** out
     if (!d) return VV_DSP_ERROR_INTERNAL;
     d->nslots = d->world = world;
     d->loopback = 1;
+    d->one_process = 1;
     for (int i = 0; i < world; ++i) {
         d->rank[i] = i;
         d->dev[i] = device;
@@ -177,6 +230,17 @@ vv_dsp_status vv_dsp_dist_rank_info(const vv_dsp_dist* d, int slot, int* rank, i
     if (world) *world = d->world;
     if (device) *device = d->dev[slot];
     return VV_DSP_OK;
+}
+
+vv_dsp_status vv_dsp_dist_comm_count(const vv_dsp_dist* d, int slot, int* count) {
+    if (!d || !count) return VV_DSP_ERROR_NULL_POINTER;
+    if (slot < 0 || slot >= d->nslots) return VV_DSP_ERROR_OUT_OF_RANGE;
+    if (d->loopback) {
+        *count = d->world;
+        return VV_DSP_OK;
+    }
+    const ncclResult_t e = R.count(d->comm[slot], count);
+    return e == ncclSuccess ? VV_DSP_OK : nccl_fail("ncclCommCount", e);
 }
 
 /* ---- helpers ---- */
@@ -209,9 +273,27 @@ static int slot_of_rank(const vv_dsp_dist* d, int r) {
     return -1;
 }
 
+/* every non-null stream must belong to its slot's device (work for slot s is
+ * enqueued with d->dev[s] current; a null stream is that device's null stream) */
+static vv_dsp_status check_streams(const vv_dsp_dist* d, void* const* streams) {
+    for (int s = 0; s < d->nslots; ++s) {
+        if (!streams[s]) continue;
+        int dev = -1;
+        if (vvhip_stream_device(streams[s], &dev) != 0) return VV_DSP_ERROR_INTERNAL;
+        if (dev != d->dev[s]) {
+            char buf[160];
+            snprintf(buf, sizeof buf, "dist: the stream of slot %d is on device %d, the slot's rank runs on device %d", s,
+                     dev, d->dev[s]);
+            vvhip_set_error(buf);
+            return VV_DSP_ERROR_OUT_OF_RANGE;
+        }
+    }
+    return VV_DSP_OK;
+}
+
 static vv_dsp_status check_arrays(const vv_dsp_dist* d, const void* a, const void* b, void* const* streams) {
     if (!d || !a || !b || !streams) return VV_DSP_ERROR_NULL_POINTER;
-    return VV_DSP_OK;
+    return check_streams(d, streams);
 }
 
 /* ---- shards ---- */
@@ -289,8 +371,11 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
                                       int root, void* const* streams) {
     if (!d || !d_local || !streams) return VV_DSP_ERROR_NULL_POINTER;
     if (row_floats == 0 || rows_per_item == 0) return VV_DSP_ERROR_INVALID_SIZE;
+    if (half && row_floats < 2) return VV_DSP_ERROR_INVALID_SIZE;
     if (root < 0 || root >= d->world) return VV_DSP_ERROR_OUT_OF_RANGE;
     if (!d->loopback && !rccl_ready()) return VV_DSP_ERROR_UNSUPPORTED;
+    vv_dsp_status st = check_streams(d, streams);
+    if (st != VV_DSP_OK) return st;
     const int world = d->world, rs = slot_of_rank(d, root);
     if (rs >= 0 && !d_root_out) return VV_DSP_ERROR_NULL_POINTER;
     for (int s = 0; s < d->nslots; ++s)
@@ -302,12 +387,13 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
         if (c > cmax) cmax = c;
     }
     if (cmax == 0) return VV_DSP_OK;
-    const long long kb = vvhip_debug_get("DIST_SLAB_KB");   /* knob (tests): a smaller slab */
+    /* knob (tests): a smaller slab -- only where one process drives every rank,
+     * since the sender and the root each derive the slab bounds */
+    const long long kb = d->one_process ? vvhip_debug_get("DIST_SLAB_KB") : -1;
     size_t slab = (kb > 0 ? (size_t)kb << 10 : DIST_SLAB_BYTES) / (sizeof(float) * w);
     if (slab < 1) slab = 1;
     if (slab > cmax) slab = cmax;
 
-    vv_dsp_status st = VV_DSP_OK;
     /* the root's own rows: one device copy to their place (no-op in place) */
     if (rs >= 0) {
         const size_t c = rows_count(total_items, rows_per_item, world, root);
@@ -322,12 +408,18 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
         if (st != VV_DSP_OK) return st;
     }
     if (world == 1) return VV_DSP_OK;
+    void* const rstream = rs >= 0 ? streams[rs] : NULL;
+    /* loopback: every pack, copy and unpack runs on the root's stream, so it
+     * first waits for each slot's stream, where that slot's rows were written */
+    if (d->loopback)
+        for (int s = 0; s < d->nslots && st == VV_DSP_OK; ++s)
+            if (s != rs && vvhip_stream_wait(rstream, streams[s]) != 0) st = VV_DSP_ERROR_INTERNAL;
+    if (st != VV_DSP_OK) return st;
 
     /* scratch: a packed slab per sending slot (half rows); on the root one
      * staging slab per peer (half rows; full rows land in place) */
     float* pack[DIST_MAX_SLOTS] = {0};
     float* stage = NULL;
-    void* const rstream = rs >= 0 ? streams[rs] : NULL;
     if (half) {
         for (int s = 0; s < d->nslots && st == VV_DSP_OK; ++s) {
             if (d->rank[s] == root || rows_count(total_items, rows_per_item, world, d->rank[s]) == 0) continue;

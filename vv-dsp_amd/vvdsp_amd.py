@@ -84,6 +84,9 @@ def lib():
     L.vv_dsp_dist_init_all.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(_vp)]
     L.vv_dsp_dist_init_loopback.argtypes = [C.c_int, C.c_int, C.POINTER(_vp)]
     L.vv_dsp_dist_from_comm.argtypes = [_vp, C.POINTER(_vp)]
+    L.vv_dsp_dist_unique_id.argtypes = [C.c_char_p]
+    L.vv_dsp_dist_init_rank.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_int, C.POINTER(_vp)]
+    L.vv_dsp_dist_comm_count.argtypes = [_vp, C.c_int, C.POINTER(C.c_int)]
     L.vv_dsp_dist_destroy.argtypes = [_vp]
     L.vv_dsp_dist_local_ranks.argtypes = [_vp]
     L.vv_dsp_dist_rank_info.argtypes = [_vp, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -526,9 +529,13 @@ def _ptrs(xs):
     return (_vp * len(xs))(*[None if x is None else (x if isinstance(x, int) else x.data_ptr()) for x in xs])
 
 
-def _streams(streams, n):
+def _streams(streams, n, devices=None):
+    """per-slot hipStream_t array; default: each slot's device's current stream"""
     if streams is None:
-        streams = [torch.cuda.current_stream()] * n
+        streams = [torch.cuda.current_stream(d) for d in devices] if devices is not None else \
+            [torch.cuda.current_stream()] * n
+    if len(streams) != n:
+        raise VvError(f"{len(streams)} streams for {n} local ranks")
     return (_vp * n)(*[s if (s is None or isinstance(s, int)) else s.cuda_stream for s in streams])
 
 
@@ -536,12 +543,37 @@ class Dist:
     """Multi-GPU layout of the spectral path over RCCL (include/vv_dsp/vv_dsp_dist.h):
     Dist.all([0, 1, ...]) -- every rank in this process (ncclCommInitAll);
     Dist.from_comm(ptr)   -- one rank of a caller's ncclComm_t;
+    Dist.rank(world, r, id, device) -- one rank per process (ncclCommInitRank;
+                             id = Dist.unique_id() on rank 0, shared by the caller);
     Dist.loopback(world)  -- `world` ranks on one device, transfers as device copies.
-    Per-rank list arguments have one element per local rank (slot)."""
+    Per-rank list arguments have one element per local rank (slot); streams
+    default to each slot's device's current stream."""
 
     def __init__(self, handle):
         self.h = handle
         self.slots = lib().vv_dsp_dist_local_ranks(self.h)
+        self.devices = [self.rank_info(s)[2] for s in range(self.slots)]
+
+    @staticmethod
+    def unique_id():
+        """VV_DSP_DIST_ID_BYTES (128) bytes naming a new communicator (ncclGetUniqueId)"""
+        buf = C.create_string_buffer(128)
+        _check(lib().vv_dsp_dist_unique_id(buf), "dist_unique_id")
+        return buf.raw
+
+    @classmethod
+    def rank(cls, world, rank, uid, device):
+        if len(uid) != 128:
+            raise VvError("a communicator id is 128 bytes")
+        h = _vp()
+        _check(lib().vv_dsp_dist_init_rank(world, rank, bytes(uid), device, C.byref(h)), "dist_init_rank")
+        return cls(h)
+
+    def comm_count(self, slot=0):
+        """ranks RCCL reports for slot's communicator (ncclCommCount)"""
+        n = C.c_int()
+        _check(lib().vv_dsp_dist_comm_count(self.h, slot, C.byref(n)), "dist_comm_count")
+        return n.value
 
     @classmethod
     def all(cls, devices):
@@ -570,7 +602,7 @@ class Dist:
     def stft(self, st, sigs, n, total_ch, ch_stride, rows, out_kind=0, streams=None):
         nf = _sz(0)
         _check(lib().vv_dsp_dist_stft(self.h, st.h, _ptrs(sigs), n, total_ch, ch_stride, out_kind, _ptrs(rows),
-                                      _streams(streams, self.slots), C.byref(nf)), "dist_stft")
+                                      _streams(streams, self.slots, self.devices), C.byref(nf)), "dist_stft")
         return nf.value
 
     def gather_rows(self, local, total_items, rows_per_item, row_floats, out, root=0, half=False, streams=None):
@@ -579,16 +611,16 @@ class Dist:
         _check(lib().vv_dsp_dist_gather_rows(self.h, _ptrs(local), total_items, rows_per_item, row_floats,
                                              1 if half else 0,
                                              None if out is None else _ptr(out), root,
-                                             _streams(streams, self.slots)), "dist_gather_rows")
+                                             _streams(streams, self.slots, self.devices)), "dist_gather_rows")
 
     def fft(self, n, kind, direction, total_batch, ins, outs, streams=None):
         _check(lib().vv_dsp_dist_fft(self.h, n, kind, direction, total_batch, _ptrs(ins), _ptrs(outs),
-                                     _streams(streams, self.slots)), "dist_fft")
+                                     _streams(streams, self.slots, self.devices)), "dist_fft")
 
     def fir(self, plans, n, total_ch, xs, x_stride, ys, y_stride, streams=None):
         arr = (_vp * len(plans))(*[p.h for p in plans])
         _check(lib().vv_dsp_dist_fir_apply_fft(self.h, arr, n, total_ch, _ptrs(xs), x_stride, _ptrs(ys), y_stride,
-                                               _streams(streams, self.slots)), "dist_fir_apply_fft")
+                                               _streams(streams, self.slots, self.devices)), "dist_fir_apply_fft")
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
