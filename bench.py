@@ -666,7 +666,7 @@ def main_dist(args, mode, world):
         t = torch.tensor([slow[0], slow[1], slow[2], slow[3], slow[4]], dtype=torch.float64)
         allt = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(allt, t)
-        per_dev = [tuple(float(v) for v in a.tolist()) for a in allt]
+        per_dev = [(float(a[0]), int(a[1]), int(a[2]), int(a[3]), int(a[4])) for a in allt]
         slow = max(per_dev)
     kern_ms, bytes_per_launch = slow[0], int(slow[1])
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9

@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Same-buffer A/B of library builds in ONE process (timing tool, not a test).
+
+Each build (`--libs a.so,b.so,...`) is dlopen'ed on its own (RTLD_LOCAL: its own
+kernels, caches and knobs) and every case runs through the C device API of
+each build on the SAME device buffers, interleaved A, B, A, B ... per round, so
+neither the placement of a fresh allocation (up to 5 % on the headline,
+profiles/r03_kbench_placement.jsonl) nor the box separates the builds.  Time =
+HIP events around each launch on the launch stream; prints one JSON line per
+(case, build) with the median and its ratio to the first build.
+
+    python scripts/ab2.py --libs scripts/ab/prev.so,vv-dsp_amd/lib/libvvdsp_amd.so --cases fir,stft
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PEAK = 8000.0
+vp, sz = C.c_void_p, C.c_size_t
+
+
+class StftParams(C.Structure):
+    _fields_ = [("fft_size", C.c_size_t), ("hop_size", C.c_size_t), ("window", C.c_int)]
+
+
+def load(path):
+    L = C.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_NOW)
+    L.vvhip_last_error.restype = C.c_char_p
+    L.vv_dsp_fir_design_lowpass.argtypes = [vp, sz, C.c_float, C.c_int]
+    L.vv_dsp_fir_plan_create.argtypes = [vp, sz, C.POINTER(vp)]
+    L.vv_dsp_fir_apply_fft_device.argtypes = [vp, vp, vp, sz, sz, sz, sz, vp]
+    L.vv_dsp_stft_create.argtypes = [C.POINTER(StftParams), C.POINTER(vp)]
+    for f in ("spectrogram", "power"):
+        getattr(L, f"vv_dsp_stft_{f}_device").argtypes = [vp, vp, sz, sz, sz, vp, sz, vp, C.POINTER(sz)]
+    for f in ("log_mel", "mfcc"):
+        getattr(L, f"vv_dsp_stft_{f}_device").argtypes = [vp, vp, vp, sz, sz, sz, vp, sz, vp, C.POINTER(sz)]
+    L.vv_dsp_mfcc_init.argtypes = [sz, sz, sz, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, C.c_float,
+                                   C.c_float, C.POINTER(vp)]
+    L.vv_dsp_fft_make_plan_many.argtypes = [sz, C.c_int, C.c_int, sz, C.POINTER(vp)]
+    L.vv_dsp_fft_execute_device.argtypes = [vp, vp, vp, vp]
+    return L
+
+
+def ok(L, st, what):
+    if st != 0:
+        raise RuntimeError(f"{what}: status {st}: {L.vvhip_last_error().decode()}")
+
+
+_BUF = {}
+
+
+def buf(key, make):
+    if key not in _BUF:
+        _BUF[key] = make()
+    return _BUF[key]
+
+
+def frames_of(n, nfft=1024, hop=256):
+    return 1 if n < nfft else 1 + (n - nfft + hop) // hop
+
+
+def case_fir(L, s, nch=8, n=1 << 24):
+    x, y = buf(("fir", nch, n), lambda: (torch.rand(nch, n, device="cuda") * 2 - 1, torch.empty(nch, n, device="cuda")))
+    h = np.zeros(257, np.float32)
+    ok(L, L.vv_dsp_fir_design_lowpass(h.ctypes.data, 257, 0.25, 2), "design")
+    p = vp()
+    ok(L, L.vv_dsp_fir_plan_create(h.ctypes.data, 257, C.byref(p)), "fir plan")
+    return (lambda: ok(L, L.vv_dsp_fir_apply_fft_device(p, x.data_ptr(), y.data_ptr(), n, nch, n, n, s), "fir")), \
+        2 * nch * n * 4, (lambda: y.clone())
+
+
+def _stft(L):
+    h = vp()
+    ok(L, L.vv_dsp_stft_create(C.byref(StftParams(1024, 256, 1)), C.byref(h)), "stft create")
+    return h
+
+
+def case_stft_rows(L, s, kind, nch, seconds):
+    n = seconds * 48000
+    fr = frames_of(n)
+    w = {"mag": 1024, "pow": 513}[kind]
+    sig, out = buf(("stft", kind, nch, n), lambda: (torch.rand(nch, n, device="cuda") * 2 - 1,
+                                                    torch.empty(nch, fr, w, device="cuda")))
+    h = _stft(L)
+    f = L.vv_dsp_stft_spectrogram_device if kind == "mag" else L.vv_dsp_stft_power_device
+    nf = sz()
+    return (lambda: ok(L, f(h, sig.data_ptr(), n, nch, n, out.data_ptr(), fr * w, s, C.byref(nf)), "stft")), \
+        nch * n * 4 + nch * fr * w * 4, (lambda: out.clone())
+
+
+def case_mel(L, s, mfcc, nch=32, seconds=600):
+    n = seconds * 48000
+    fr = frames_of(n)
+    w = 13 if mfcc else 40
+    sig, out = buf(("mel", mfcc, nch, n), lambda: (torch.rand(nch, n, device="cuda") * 2 - 1,
+                                                   torch.empty(nch, fr, w, device="cuda")))
+    h = _stft(L)
+    m = vp()
+    ok(L, L.vv_dsp_mfcc_init(1024, 40, 13, 48000.0, 20.0, 20000.0, 0, 2, 22.0, 1e-10, C.byref(m)), "mfcc init")
+    f = L.vv_dsp_stft_mfcc_device if mfcc else L.vv_dsp_stft_log_mel_device
+    nf = sz()
+    return (lambda: ok(L, f(h, m, sig.data_ptr(), n, nch, n, out.data_ptr(), fr * w, s, C.byref(nf)), "mel")), \
+        nch * n * 4 + nch * fr * w * 4, (lambda: out.clone())
+
+
+def case_c2c(L, s, n=1024, batch=65536):
+    x, y = buf(("c2c", n, batch), lambda: (torch.complex(torch.rand(batch, n, device="cuda") - 0.5,
+                                                         torch.rand(batch, n, device="cuda") - 0.5),
+                                           torch.empty(batch, n, dtype=torch.complex64, device="cuda")))
+    p = vp()
+    ok(L, L.vv_dsp_fft_make_plan_many(n, 0, 1, batch, C.byref(p)), "fft plan")
+    return (lambda: ok(L, L.vv_dsp_fft_execute_device(p, x.data_ptr(), y.data_ptr(), s), "fft")), \
+        2 * batch * n * 8, (lambda: y.clone())
+
+
+CASES = {
+    "fir": case_fir,
+    "stft": lambda L, s: case_stft_rows(L, s, "mag", 32, 600),
+    "stft60": lambda L, s: case_stft_rows(L, s, "mag", 1, 60),
+    "stftpow": lambda L, s: case_stft_rows(L, s, "pow", 32, 600),
+    "logmel": lambda L, s: case_mel(L, s, False),
+    "mfcc": lambda L, s: case_mel(L, s, True),
+    "c2c1024": case_c2c,
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--cases", required=True)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--check", action="store_true", help="also compare each build's output with the first's")
+    a = ap.parse_args()
+    libs = [load(p) for p in a.libs.split(",")]
+    tags = [os.path.basename(p) for p in a.libs.split(",")]
+    torch.cuda.init()
+    s = torch.cuda.current_stream()
+    sp = s.cuda_stream
+    for case in a.cases.split(","):
+        built = [CASES[case](L, sp) for L in libs]
+        res = [[] for _ in libs]
+        same = []
+        if a.check:
+            outs = []
+            for fn, _, get in built:
+                fn()
+                torch.cuda.synchronize()
+                outs.append(get())
+            same = [bool(torch.equal(outs[0], o)) for o in outs]
+            del outs
+        for _ in range(a.rounds):
+            for i, (fn, _, _) in enumerate(built):
+                t0 = time.perf_counter()
+                while time.perf_counter() - t0 < 0.05:
+                    for _ in range(3):
+                        fn()
+                    torch.cuda.synchronize()
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+                for e0, e1 in ev:
+                    e0.record(s)
+                    fn()
+                    e1.record(s)
+                torch.cuda.synchronize()
+                res[i] += [e0.elapsed_time(e1) for e0, e1 in ev]
+        base = float(np.median(res[0]))
+        for i, tag in enumerate(tags):
+            med = float(np.median(res[i]))
+            byts = built[i][1]
+            line = {"case": case, "lib": tag, "ms_median": round(med, 4), "ms_min": round(float(np.min(res[i])), 4),
+                    "frac": round(byts / (med * 1e-3) / 1e9 / PEAK, 4), "vs_first": round(med / base, 4)}
+            if same:
+                line["bit_identical_to_first"] = same[i]
+            print(json.dumps(line), flush=True)
+        del built
+        _BUF.clear()
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
