@@ -65,12 +65,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--chunk-mb", default="", help="comma list: time the host rows at each VVHIP_HOST_CHUNK_MB")
+    ap.add_argument("--chunk-mb", default="", help="comma list: time the host rows at each HOST_CHUNK_MB knob value")
     a = ap.parse_args()
     if a.chunk_mb:
         for c in a.chunk_mb.split(","):
-            os.environ["VVHIP_HOST_CHUNK_MB"] = c
-            sub = run_rows(a, quick=True)
+            with vv.knobs(HOST_CHUNK_MB=int(c)):   # the registry knob, read by each host call
+                sub = run_rows(a, quick=True)
             for r in sub:
                 r["chunk_mb"] = int(c)
                 print(json.dumps(r), flush=True)

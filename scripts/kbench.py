@@ -38,9 +38,8 @@ def case_r2c(n, batch, env=None):
         fn = inner[0]
 
         def run():
-            os.environ[env[0]] = env[1]
-            fn()
-            os.environ[env[0]] = ""
+            with vv.knobs(**{env[0].replace("VVHIP_", ""): int(env[1])}):
+                fn()
         return (run,) + tuple(inner[1:])
     x = torch.rand(batch, n, device="cuda")
     y = torch.empty(batch, n // 2 + 1, dtype=torch.complex64, device="cuda")
@@ -65,9 +64,8 @@ def case_stft(nch, seconds, complex_out=False, env=None, shared=True):
         fn = inner[0]
 
         def run():
-            os.environ[k] = v
-            fn()
-            os.environ[k] = ""
+            with vv.knobs(**{k.replace("VVHIP_", ""): int(v)}):
+                fn()
         return (run,) + tuple(inner[1:])
     n = seconds * 48000
     st = vv.Stft(1024, 256)
@@ -283,26 +281,6 @@ def case_stft_exp(e, nch=32, seconds=600):
         byts, (sig, win, out, lib)
 
 
-def case_lab(e, nch=32, seconds=600, fn="stftlab_run", row=1024):
-    """the product STFT kernel with parts switched off (scripts/stftlab.hip, EXP bits:
-    1 no FFT exchanges, 2 no FFT, 4 no row stores, 8 no span loads); bytes = the real job's"""
-    import ctypes
-    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
-    run = getattr(lib, fn)
-    run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
-                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-    n = seconds * 48000
-    fr = (n - 1024 + 256) // 256 + 1
-    if ("lab", nch, n) not in _SHARED:   # one buffer pair for every lab case: A/B on the same placement
-        _SHARED[("lab", nch, n)] = (torch.rand(nch, n, device="cuda") * 2 - 1, torch.empty(nch, fr, 1024, device="cuda"))
-    sig, out = _SHARED[("lab", nch, n)]
-    win = torch.hann_window(1024, periodic=False, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
-    byts = nch * n * 4 + nch * fr * row * 4
-    return (lambda: run(e, sig.data_ptr(), n, nch, win.data_ptr(), out.data_ptr(), s)), \
-        byts, (sig, win, out, lib)
-
-
 def case_empty(grid):
     """an empty kernel of grid x 256 threads (scripts/stftlab.hip emptylab_run): launch +
     kernel-boundary floor; bytes = config 3's, for a comparable frac column"""
@@ -311,18 +289,6 @@ def case_empty(grid):
     lib.emptylab_run.argtypes = [ctypes.c_int, ctypes.c_void_p]
     s = torch.cuda.current_stream().cuda_stream
     return (lambda: lib.emptylab_run(grid, s)), 57591808, (lib,)
-
-
-def case_firreglab(e, nch=8, n=1 << 24):
-    """the product's k_fir_bulk_reg with parts switched off (scripts/stftlab.hip firreglab_run:
-    2 no FFTs, 4 no stores, 8 no loads)"""
-    return case_firlab(e, nch, n, fn="firreglab_run")
-
-
-def case_firr32lab(e, nch=8, n=1 << 24):
-    """k_fir_r32 (the product's config-4 kernel) with parts switched off (scripts/stftlab.hip
-    firr32lab_run: 2 no FFTs, 4 no stores, 8 no loads)"""
-    return case_firlab(e, nch, n, fn="firr32lab_run")
 
 
 def case_firlab(e, nch=8, n=1 << 24, fn="firlab_run"):
@@ -344,9 +310,8 @@ def case_firlab(e, nch=8, n=1 << 24, fn="firlab_run"):
         (x, y, H, lib)
 
 
-def case_c2clab(e, batch=65536, fn="c2clab_run"):
-    """k_c2c<1024> forward with parts switched off (scripts/stftlab.hip c2clab_run: 1 no exchanges, 2 no FFT;
-    c2cr32lab_run: k_c2c_r32, 2 no FFT)"""
+def case_c2clab(e, batch=65536, fn="c2cr32lab_run"):
+    """the lab's k_c2c_r32 (scripts/stftlab.hip c2cr32lab_run; EXP 2 no FFT)"""
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "libstftlab.so"))
     run = getattr(lib, fn)
@@ -515,21 +480,8 @@ CASES = {
     "stft256ch": lambda: case_stft(256, 600),
     **{f"place_i{i}_o{o}": (lambda i=i, o=o: case_stft_place(i, o))
        for i in (0, 4, 64, 1024, 2052) for o in (0, 4, 8, 64, 1024, 2052, 4100)},
-    **{f"c2clab{e}": (lambda e=e: case_c2clab(e)) for e in (0, 1, 2, 4, 6, 8, 16)},
     **{f"firlab{e}": (lambda e=e: case_firlab(e)) for e in (0, 1, 2, 3, 4, 5, 6, 8, 10, 12, 14)},
-    **{f"firreglab{e}": (lambda e=e: case_firreglab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 14, 16, 32, 64, 80, 18, 34, 66, 82, 128, 144, 130,
-                                                                          256, 258, 266, 512, 768, 1536, 1792)},
-    **{f"lab60_{e}": (lambda e=e: case_lab(e, nch=1, seconds=60)) for e in (0, 2, 4, 6, 8, 10, 14, 32782, 65550, 98318)},
     **{f"empty{g}": (lambda g=g: case_empty(g)) for g in (703, 2048)},
-    **{f"lab5_{e}": (lambda e=e: case_lab(e, fn="stftlab5_run"))
-       for e in (0, 2, 4, 6, 8, 10, 16, 18, 32, 34, 512, 514, 1024, 1026, 128, 256, 131072, 262144)},
-    **{f"powlab{e}": (lambda e=e: case_lab(e, fn="stftpowlab_run", row=513)) for e in (0, 2, 4, 131072)},
-    **{f"powr32lab{e}": (lambda e=e: case_lab(e, fn="stftpowr32lab_run", row=513)) for e in (0, 2, 4, 6)},
-    **{f"magr32lab{e}": (lambda e=e: case_lab(e, fn="stftmagr32lab_run")) for e in (0, 2, 4, 6)},
-    **{f"lab{e}": (lambda e=e: case_lab(e)) for e in list(range(16)) + [16, 18, 24, 26, 32, 34, 40, 42, 64, 66, 68, 80, 82,
-                                                                         128, 256, 512, 1024, 640, 1152,
-                                                                         2048, 2050, 2052, 2056, 4096, 4098, 8192, 8194,
-                                                                         16384, 16448]},
     **{f"stftcps{c}": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_CPS", str(c)) for c in (1, 2, 4, 8)},
     "stftspan": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_RING", "0"),
     "stftchunk": with_env(lambda: case_stft(32, 600), "VVHIP_STFT_DYN", "0"),
@@ -572,7 +524,6 @@ CASES = {
     "firstatic": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_DYN", "0"),
     "firold": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_OLD", "1"),
     "firr16": with_env(lambda: case_fir(8, 1 << 24), "VVHIP_FIR_R32", "0"),
-    **{f"firr32lab{e}": (lambda e=e: case_firr32lab(e)) for e in (0, 2, 4, 6, 8, 10, 12, 16, 32, 64, 128, 96, 192, 18, 34, 256, 258, 288, 290, 768)},
     "hilbert1024": lambda: case_hilbert(1024, 65536),
     "logmel": lambda: case_mel(0), "mfcc": lambda: case_mel(1),
     "ola": lambda: case_ola(),
@@ -595,7 +546,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--mark", action="store_true",
                     help="launch a tiny torch fill kernel before each case's runs (splits a rocprofv3 trace per case)")
-    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "wp", "ex", "rw", "lab", "model", "firlab", "c2clab", "powlab", "powr32lab", "magr32lab"))))
+    ap.add_argument("--cases", default=",".join(k for k in CASES if not k.startswith(("wr", "wp", "ex", "rw", "model", "firlab", "c2cr32lab"))))
     a = ap.parse_args()
     names = a.cases.split(",")
     built = {k: CASES[k]() for k in names}

@@ -6,6 +6,7 @@ register length, an odd frame count (a missing second frame) included.
 import os
 import sys
 
+
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -19,11 +20,9 @@ for nf in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960):
     for n in (3 * 48000 + 77, 48000):
         sig = torch.rand(3, n, device="cuda", generator=g) * 2 - 1
         for cpx in (False, True):
-            os.environ["VVHIP_MIX_VAR"] = ""
             a = st.spectrogram(sig, complex_out=cpx).clone()
-            os.environ["VVHIP_MIX_VAR"] = var
-            b = st.spectrogram(sig, complex_out=cpx)
-            os.environ["VVHIP_MIX_VAR"] = ""
+            with vv.knobs(MIX_VAR=int(var)):   # the registry knob (csrc/hip/debug.hip), set per call
+                b = st.spectrogram(sig, complex_out=cpx)
             torch.cuda.synchronize()
             bad = (a != b).sum().item()
             print(f"nfft {nf} n {n} {'complex' if cpx else 'magnitude'} frames {a.shape[1]}: {bad} differ")

@@ -24,18 +24,18 @@ namespace vvh {
 // ------------------------------------------------------------------------
 // C2C
 // ------------------------------------------------------------------------
-// EXP: timing ablations for scripts/stftlab.hip only (the library instantiates
-// EXP = 0): bit 0 FFT without its LDS exchanges, bit 1 no FFT, bit 3 round 3's
-// exchange reads (the compiler's ds_read2 pairs and v_movs; the library reads
-// single ds_read_b32 into the complex register pairs, pass_exchange_ri RIV 1:
-// same buffers 0.1827 vs 0.1850 ms, profiles/r04_kbench_riv_ab.jsonl).  (Two transforms per loop
-// trip with alternating prefetch buffers, to drop the loop-carried copy, spilled
-// at the 128 VGPRs of four waves per SIMD.)
+// The exchange reads are single ds_read_b32 into the complex register pairs
+// (pass_exchange_ri RIV 1; the compiler's ds_read2 pairs and v_movs measured
+// 0.1850 vs 0.1827 ms on the same buffers, profiles/r04_kbench_riv_ab.jsonl).
+// (Two transforms per loop trip with alternating prefetch buffers, to drop the
+// loop-carried copy, spilled at the 128 VGPRs of four waves per SIMD.)  A grid-
+// wide interleaved front: per-XCD eighths measured 0.1992 vs 0.1836 ms
+// (profiles/r04_kbench_c2c_walk.jsonl).
 // N = 1024 exchanges through the half-size real/imaginary buffer
 // (pass_exchange_ri): 26 KB of LDS per workgroup instead of 43 KB, so four
 // workgroups (16 waves) fit per CU and keep more transforms' loads in flight.
-template <int N, bool FWD, int EXP = 0>
-__global__ void __launch_bounds__(Wg<N>::value, N == 1024 ? ((EXP & 4) ? 5 : 4) : 1)
+template <int N, bool FWD>
+__global__ void __launch_bounds__(Wg<N>::value, N == 1024 ? 4 : 1)
 k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
       const float2* gpass, const float2* gtab, float scale) {
     using G = Geo<N>;
@@ -50,15 +50,9 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
-    long long stride = (long long)gridDim.x * F;
+    const long long stride = (long long)gridDim.x * F;
     long long f = uni<G::T>((long long)blockIdx.x * F + slot);
-    long long fend = batch;
-    if constexpr ((EXP & 16) != 0) {   // probe: each XCD group walks a contiguous eighth of the batch
-        xcd_walk(batch, F, slot, &f, &fend, &stride);
-        f = uni<G::T>(f);
-        fend = uni<G::T>(fend);
-        stride = uni<G::T>(stride);
-    }
+    const long long fend = batch;
     float2 nx[G::P];
     if (f < fend) {
 #pragma unroll
@@ -73,8 +67,7 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
 #pragma unroll
             for (int r = 0; r < G::P; ++r) nx[r] = ld_nt(in + fn * in_dist + t + r * G::T);
         }
-        if constexpr (!(EXP & 2))
-            fft_regs<N, FWD, false, RI, TwTab<N>, (EXP & 1) != 0, false, (EXP & 8) ? 0 : 1>(v, t, my, tw);
+        fft_regs<N, FWD, false, RI, TwTab<N>, false, false, 1>(v, t, my, tw);
         float2* dst = out + f * out_dist;
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {

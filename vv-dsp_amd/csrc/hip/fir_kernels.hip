@@ -201,29 +201,20 @@ k_fir_pair(long long lm1, long long le, const float2* Hg, const float* x, float*
 // pair's stores (issued during the FFT they would need 32 more VGPRs than the
 // four waves per SIMD allow).  All global accesses are compiler-visible.
 // ------------------------------------------------------------------------
-// EXP: timing ablations for scripts/stftlab.hip only (library: EXP = 0): bit 1 no
-// FFTs, bit 2 no output stores, bit 3 no input loads (results are wrong); bit 4
-// stores as sc0 sc1 nt, bit 5 plain stores, bit 6 non-persistent walk (8 pairs per
-// wave, the launcher sizes the grid), bit 8 the dynamic band walk of k_stft_pair
-// VAR 4 (persistent grid, each wave's next pair from a per-(XCD group, slot)
-// counter in `ctrs`, the last wave of each counter stream resets it).
-template <int N, int EXP = 0>
+// DYN: the dynamic band walk of k_stft_pair VAR 4 (persistent grid, each
+// wave's next pair from a per-(XCD group, slot) counter in `ctrs`, the last wave
+// of each counter stream resets it); otherwise the static XCD walk.
+template <int N, bool DYN = false>
 __global__ void __launch_bounds__(256, 4)
 k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
                long long cnt, long long q0, const float2* gpass, long long n, const float* prefix, long long lm1,
                long long qf, long long ql, unsigned* ctrs) {
     using G = Geo<N>;
-    constexpr bool DYN = (EXP & 256) != 0;
-    // EXP bit 9: the FFT exchanges as whole complex values (b64 LDS accesses,
-    // 2x the buffer) instead of real/imaginary halves (b32); bit 10 with it:
-    // through pass_exchange_c1024's explicit offsets instead of pass_exchange
-    constexpr bool B64X = (EXP & 512) != 0;
-    constexpr bool C64 = B64X && (EXP & 1024) != 0;
     static_assert(G::T == 64 && N == 1024 && !TwLayout<N>::SPLIT, "one wave per transform (T = N/16), pass-major twiddles");
     constexpr int F = 4, RL = G::RL;
     constexpr int LE = N / 4, LOUT = N - LE;   // taps <= N/4 + 1
     constexpr int TWL = G::tw_off(G::NPASS - 1) > 0 ? G::tw_off(G::NPASS - 1) : 1;
-    constexpr int XW = B64X ? 2 * G::LDS : ri_floats<N>();
+    constexpr int XW = ri_floats<N>();   // the FFT exchanges as real / imaginary halves (b32)
     __shared__ __attribute__((aligned(16))) float xch[F * XW];
     __shared__ float2 ltab[TWL];
     __shared__ float2 lH[N / 2 + 1];
@@ -252,9 +243,7 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
         p_step = 0;
         if (p < p_end && t == 0) rk = atomicAdd(ctr, 1u);
     } else {
-        if constexpr (EXP & 64) work_walk(nch * cnt, F, slot, 8 * F, &p, &p_end, &p_step);
-        else if constexpr (EXP & 128) band_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
-        else xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
+        xcd_walk(nch * cnt, F, slot, &p, &p_end, &p_step);
         p = uni<64>(p);
         p_end = uni<64>(p_end);
         p_step = uni<64>(p_step);
@@ -268,13 +257,11 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
     if (p < p_end) locate(p, &c, &j);
     float xa[G::P], xb[G::P];
     auto load_a = [&](long long cc, long long jj) {
-        if constexpr (EXP & 8) return;
         const float* a = x + cc * x_stride + jj * LOUT - LE;   // wave-uniform block base
 #pragma unroll
         for (int r = 0; r < G::P; ++r) xa[r] = __builtin_nontemporal_load(a + t + 64 * r);
     };
     auto load_b = [&](long long cc, long long jj) {
-        if constexpr (EXP & 8) return;
         const float* b = x + cc * x_stride + jj * LOUT - LE + LOUT;
 #pragma unroll
         for (int r = 0; r < G::P; ++r) xb[r] = b[t + 64 * r];   // overlaps the next pair's block a: cached
@@ -286,10 +273,6 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
     // An edge pair is loaded at the top of its own iteration (nothing else live
     // then); a bulk pair is prefetched during the previous pair's stores.
     auto is_edge = [&](long long jj) { return (jj >> 1) < qf || (jj >> 1) >= ql; };
-    if constexpr (EXP & 8) {
-#pragma unroll
-        for (int r = 0; r < G::P; ++r) xa[r] = xb[r] = (float)(t + r);
-    }
     if (p < p_end && !is_edge(j)) {
         load_a(c, j);
         load_b(c, j);
@@ -329,7 +312,7 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 #pragma unroll
         for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r], xb[r]);
         tw.opaque();
-        if constexpr (!(EXP & 2)) fft_regs<N, true, false, !B64X, TwLastReg<N>, false, C64>(v, t, my, tw);
+        fft_regs<N, true, false, true, TwLastReg<N>, false, false>(v, t, my, tw);
         float2 u[G::P];
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
@@ -338,7 +321,7 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
             else u[m] = cmul(v[q], cconj(lH[N - t - 64 * m]));
         }
         tw.opaque();
-        if constexpr (!(EXP & 2)) fft_regs<N, false, false, !B64X, TwLastReg<N>, false, C64>(u, t, my, tw);
+        fft_regs<N, false, false, true, TwLastReg<N>, false, false>(u, t, my, tw);
         if (more && !is_edge(jn)) {   // ahead of this pair's stores: in flight across them
             load_a(cn, jn);
             load_b(cn, jn);
@@ -364,30 +347,11 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
         }
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
-            if constexpr (EXP & 4) {
-                asm volatile("" ::"v"(u[q].x), "v"(u[q].y));
-            } else if constexpr (EXP & 48) {
-            } else if (q % RL != 0) {   // e = t + 64 m >= LE exactly for these registers
+            if (q % RL != 0) {   // e = t + 64 m >= LE exactly for these registers
                 const int m = q / RL + G::NPT * (q % RL);
                 __builtin_nontemporal_store(u[q].x, ya + t + 64 * m);
                 __builtin_nontemporal_store(u[q].y, ya + LOUT + t + 64 * m);
             }
-        }
-        if constexpr ((EXP & 48) != 0 && (EXP & 4) == 0) {
-            const unsigned lo = 4u * (unsigned)t;
-            static_for<0, G::P>([&](auto qc) {
-                constexpr int q = decltype(qc)::value;
-                constexpr int m = q / RL + G::NPT * (q % RL);
-                if constexpr (q % RL != 0) {
-                    if constexpr (EXP & 16) {
-                        st4_pol_sbase<256 * m, 2>(lo, u[q].x, ya);
-                        st4_pol_sbase<256 * m, 2>(lo, u[q].y, ya + LOUT);
-                    } else {
-                        st4_sbase<256 * m>(lo, u[q].x, ya);
-                        st4_sbase<256 * m>(lo, u[q].y, ya + LOUT);
-                    }
-                }
-            });
         }
         c = cn;
         j = jn;
@@ -427,12 +391,9 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // 66 KB + H 4 KB + twiddles 8 KB per workgroup, two workgroups per CU.
 // Edge pairs (span before sample 0 or past n) load through the prefix / zero
 // rule and store predicated, in the same loop (a wave-uniform branch).
-// EXP (timing ablations, scripts/stftlab.hip; the library uses 0): bit 1 no
-// FFT, bit 2 no stores, bit 3 no loads; walks: bit 4 non-persistent chunks of 8
-// couples per wave (the launcher sizes the grid), bit 5 the dynamic band walk
-// of k_fir_bulk_reg (counters in `ctrs`); bit 6 plain output stores, bit 7
-// plain block-a loads; bit 9 one grid-wide interleaved front instead of the
-// per-XCD eighths.
+// Walk: each XCD group takes one contiguous eighth of the couples (xcd_walk), so
+// neighbouring blocks' overlap comes from that XCD's L2 (a grid-wide front
+// measured 0.2517 vs 0.2019 ms, profiles/r04_kbench_fir_walk.jsonl).
 // PAIRED (the launcher's choice for 8 B aligned channels): bulk samples move as 8 B per lane -- a block's 1024 inputs as 16
 // dwordx2 loads (rows 0..7 of block b are rows 24..31 of block a: 12 more), its
 // 768 outputs as 12 dwordx2 stores -- each pair of dwords re-laid by one
@@ -441,13 +402,12 @@ k_fir_bulk_reg(const float2* Hg, const float* x, float* y, long long nch, long l
 // and the rows the transposes use.  Needs 8 B aligned channels (x, y and
 // their strides even).
 // ------------------------------------------------------------------------
-template <bool PAIRED, int EXP = 0>
+template <bool PAIRED>
 __global__ void __launch_bounds__(256, 2)
 k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
           long long ppc, const float2* tw1024, long long n, const float* prefix, long long lm1, long long qf,
-          long long ql, unsigned* ctrs) {
+          long long ql) {
     constexpr int N = 1024, LE = 256, LOUT = N - LE, F = 4;
-    constexpr bool DYN = (EXP & 32) != 0;
     __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R32_BUF];
     __shared__ float2 lH[N / 2 + 1];
     __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r) (row 0 unused)
@@ -464,35 +424,10 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     __syncthreads();
     const long long pairs = nch * ppc, couples = (pairs + 1) / 2;
     long long it, it_end, it_step;
-    // DYN: counter value k of stream s (= XCD group, slot) is couple
-    // (k / 64) * 8 F 64 + s * 64 + k % 64: the chip sweeps one moving band
-    const int stream = __builtin_amdgcn_readfirstlane((int)(blockIdx.x & 7) * F + slot);
-    unsigned* const ctr = DYN ? ctrs + 32 * stream : nullptr;
-    auto band_item = [&](unsigned k) -> long long {
-        return (long long)(k >> 6) * (8 * F * 64) + (long long)stream * 64 + (long long)(k & 63);
-    };
-    unsigned rk = 0;   // lane 0: the counter value of the couple after `it`
-    if constexpr (DYN) {
-        unsigned r0 = 0;
-        if (lane == 0) r0 = atomicAdd(ctr, 1u);
-        it = band_item(__builtin_amdgcn_readfirstlane(r0));
-        it_end = couples;
-        it_step = 0;
-        if (it < it_end && lane == 0) rk = atomicAdd(ctr, 1u);
-    } else {
-        if constexpr (EXP & 16) {
-            work_walk(couples, F, slot, 8 * F, &it, &it_end, &it_step);
-        } else if constexpr (EXP & 512) {   // probe: one grid-wide interleaved front (k_c2c's walk)
-            it = (long long)blockIdx.x * F + slot;
-            it_end = couples;
-            it_step = (long long)gridDim.x * F;
-        } else {
-            xcd_walk(couples, F, slot, &it, &it_end, &it_step);
-        }
-        it = uni<64>(it);
-        it_end = uni<64>(it_end);
-        it_step = uni<64>(it_step);
-    }
+    xcd_walk(couples, F, slot, &it, &it_end, &it_step);
+    it = uni<64>(it);
+    it_end = uni<64>(it_end);
+    it_step = uni<64>(it_step);
     if (it < it_end) {
     // couple k: pairs 2k (lanes 0..31) and 2k+1 (lanes 32..63); a missing
     // second pair (odd total) computes pair 2k again and stores nothing.
@@ -512,26 +447,19 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         *j = 2 * (half ? q1 : q0);
         *edge_any = q0 < qf || q0 >= ql || q1 < qf || q1 >= ql;
     };
-    auto advance = [&](long long k) {   // (c0, q0) of couple k from those of k - it_step
-        if constexpr (DYN) {
-            seek(k);
-        } else {
-            q0 += dq;
-            c0 += dc;
-            if (q0 >= ppc) {
-                q0 -= ppc;
-                ++c0;
-            }
+    auto advance = [&]() {   // (c0, q0) of couple k + it_step from those of k
+        q0 += dq;
+        c0 += dc;
+        if (q0 >= ppc) {
+            q0 -= ppc;
+            ++c0;
         }
     };
-    if constexpr (!DYN) {
-        dc = (2 * it_step) / ppc;
-        dq = 2 * it_step - dc * ppc;
-    }
+    dc = (2 * it_step) / ppc;
+    dq = 2 * it_step - dc * ppc;
     seek(it);
     float xa[32], xb[32];
     auto load_bulk = [&](long long c, long long j) {
-        if constexpr (EXP & 8) return;
         if constexpr (PAIRED) {
             // 8 B pairs (samples 64 i + 2m, +1), swapped into the residue layout at use
             const float2* a = reinterpret_cast<const float2*>(x + c * x_stride + j * LOUT - LE) + m;
@@ -552,7 +480,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             const float* a = x + c * x_stride + j * LOUT - LE + m;
             const float* b = a + LOUT;
 #pragma unroll
-            for (int r = 0; r < 32; ++r) xa[r] = (EXP & 128) ? a[32 * r] : __builtin_nontemporal_load(a + 32 * r);
+            for (int r = 0; r < 32; ++r) xa[r] = __builtin_nontemporal_load(a + 32 * r);
 #pragma unroll
             for (int r = 0; r < 32; ++r) xb[r] = b[32 * r];   // overlaps the next pair's block a: cached
         }
@@ -588,7 +516,6 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     locate(it, &c, &j, &valid, &edge);
     if (!edge) load_bulk(c, j);
     for (; it < it_end; it += it_step) {
-        if constexpr (DYN) it_step = band_item(__builtin_amdgcn_readfirstlane(rk)) - it;
         if (edge) {
             load_edge(c, j);   // at the top of its own iteration (a bulk couple was prefetched)
         } else if constexpr (PAIRED) {
@@ -613,17 +540,14 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             for (int r = 0; r < 32; ++r) v[r] = make_float2(xa[r], xb[r]);
         }
         const long long itn = it + it_step;
-        if constexpr (DYN) {
-            if (itn < it_end && lane == 0) rk = atomicAdd(ctr, 1u);   // -> the couple after itn
-        }
         long long cn = c, jn = j;
         bool validn = valid, edgen = edge;
         if (itn < it_end) {   // the next couple's loads, in flight across this one's transforms
-            advance(itn);
+            advance();
             locate(itn, &cn, &jn, &validn, &edgen);
             if (!edgen) load_bulk(cn, jn);
         }
-        if constexpr (!(EXP & 2)) {
+        {
             // forward: DFT over m1, twiddle, transpose, DFT over m2 -> X[m + 32 k2] in v[k2]
             dft32<true>(v);
             r32_twiddle<true>(v, atwf);
@@ -645,7 +569,7 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
             r32_transpose(v, buf, m, mr);
             dft32<false>(v);
         }
-        if constexpr (!(EXP & 4)) {
+        {
             float* ya = y + c * y_stride + j * LOUT - LE + mr;   // + 32 b: block j's output (b >= 8)
             if (!edge) {
                 if constexpr (PAIRED) {
@@ -667,17 +591,10 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
                         for (int i = 0; i < 12; ++i) st_nt(ob[i], yp + LOUT / 2 + 16 * (8 + 2 * i));
                     }
                 } else if (valid) {
-                    if constexpr (EXP & 64) {
 #pragma unroll
-                        for (int b = 8; b < 32; ++b) ya[32 * b] = v[b].x;
+                    for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].x, ya + 32 * b);
 #pragma unroll
-                        for (int b = 8; b < 32; ++b) ya[LOUT + 32 * b] = v[b].y;
-                    } else {
-#pragma unroll
-                        for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].x, ya + 32 * b);
-#pragma unroll
-                        for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].y, ya + LOUT + 32 * b);
-                    }
+                    for (int b = 8; b < 32; ++b) __builtin_nontemporal_store(v[b].y, ya + LOUT + 32 * b);
                 }
             } else if (valid) {   // outputs past n are not stored
                 const long long rem = n - (j * LOUT - LE + mr);
@@ -694,15 +611,6 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
         valid = validn;
         edge = edgen;
     }
-    }
-    if constexpr (DYN) {   // the XCD group's last wave out resets its counters for the next launch
-        if (lane == 0) {
-            const unsigned nw = (unsigned)((gridDim.x - (blockIdx.x & 7) + 7) / 8);
-            if (atomicAdd(ctr + 16, 1u) == nw - 1) {
-                atomicExch(ctr, 0u);
-                atomicExch(ctr + 16, 0u);
-            }
-        }
     }
 }
 
@@ -773,10 +681,10 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
             stat_inc(STAT_FIR_R32);
             if (paired)
                 hipLaunchKernelGGL((k_fir_r32<true>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride,
-                                   ppc, t1024, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
+                                   ppc, t1024, n, prefix, lm1, qf, ql);
             else
                 hipLaunchKernelGGL((k_fir_r32<false>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride,
-                                   ppc, t1024, n, prefix, lm1, qf, ql, (unsigned*)nullptr);
+                                   ppc, t1024, n, prefix, lm1, qf, ql);
             return hipGetLastError();
         }
     }
@@ -786,18 +694,18 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
         // second, latency-bound launch: 11 us of config 4's 237)
         if constexpr (FIR_BULK<N>) {
             static std::atomic<int> capc_r, capc_rd;
-            // the dynamic band walk (k_fir_bulk_reg EXP bit 8): 0.2385 -> 0.2323 ms
+            // the dynamic band walk (k_fir_bulk_reg<N, true>): 0.2385 -> 0.2323 ms
             // for config 4, same buffers, bit-identical (profiles/r03_kbench_fir_dyn.jsonl);
             // knob FIR_DYN = 0 keeps the static XCD walk (A/B)
             // Small jobs (< 8 pairs per wave slot of the persistent grid), a grid
             // too small for 8 XCD groups, or no counter block (pool exhausted, a
             // first use inside a graph capture) take the static walk below.
             if (knob(KNOB_FIR_DYN, -1) != 0) {
-                const int cap_d = cached_grid(capc_rd, (const void*)k_fir_bulk_reg<N, 256>, 256, 0, 1LL << 40);
+                const int cap_d = cached_grid(capc_rd, (const void*)k_fir_bulk_reg<N, true>, 256, 0, 1LL << 40);
                 unsigned* ctrs = (cap_d >= 8 && nch * ppc >= 8LL * 4 * cap_d) ? stream_counters(s) : nullptr;
                 if (ctrs) {
                     stat_inc(STAT_FIR_DYN);
-                    hipLaunchKernelGGL((k_fir_bulk_reg<N, 256>), dim3(cap_d / 8 * 8), dim3(256), 0, s, H, x, y, nch,
+                    hipLaunchKernelGGL((k_fir_bulk_reg<N, true>), dim3(cap_d / 8 * 8), dim3(256), 0, s, H, x, y, nch,
                                        x_stride, y_stride, ppc, 0LL, pN, n, prefix, lm1, qf, ql, ctrs);
                     return hipGetLastError();
                 }

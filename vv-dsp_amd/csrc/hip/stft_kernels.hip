@@ -108,7 +108,7 @@ __device__ __forceinline__ void put_bin(char* row, int k, float2 X) {
 // per transform, mirror-paired last pass; see k_stft_pair).  Issues exactly
 // the kernel's NST stores per pair (rows of a missing second frame go to the
 // sink), so the caller's hand-counted vmcnt stays exact.
-template <int N, int MODE, int EXP>
+template <int N, int MODE>
 __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, char* rowb, bool has_b,
                                             float* sink) {
     using G = Geo<N>;
@@ -196,17 +196,13 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
         // in L2; streaming stores of partial lines measured 1.65x slower)
         auto st = [&](auto imm, unsigned off, float val, const void* base) {
             constexpr int I = decltype(imm)::value;
-            if constexpr (EXP & 4) {
-                asm volatile("" ::"v"(val));
-            } else if constexpr (MODE == 2) {
+            if constexpr (MODE == 2) {
                 if constexpr (I < 4 * (N / 2)) st4_sbase<I>(off, val, base);
             } else {
                 // streaming stores with sc0 sc1 (write-through, not kept in L2):
                 // 0.6 % faster than nt alone on the config-5 shard (same-box A/B,
-                // six alternating runs each); bit 9 = sc1 only, bit 10 = nt only
-                if constexpr (EXP & 512) st4_pol_sbase<I, 1>(off, val, base);
-                else if constexpr (EXP & 1024) st4_nt_sbase<I>(off, val, base);
-                else st4_pol_sbase<I, 2>(off, val, base);
+                // six alternating runs each)
+                st4_pol_sbase<I, 2>(off, val, base);
             }
         };
         // The N/T blocks of a row in ascending address order, row a then
@@ -231,31 +227,8 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
                 else st(std::integral_constant<int, 4 * T * m>{}, vo - 4u * (NB - T), val(mc, e, sp), base);
             });
         };
-        if constexpr (EXP & 16) {
-            // ablation: the same 8 KB as 8 x 16 B/lane streaming stores (values garbage)
-            static_assert(MODE == 0, "store-count bookkeeping (NST = 8)");
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const vf4_t va = {ea[0][u], ea[1][u], sa[u], eb[0][u]};
-                const vf4_t vb = {eb[1][u], sb[u], ea[0][u], eb[0][u]};
-                st16_nt_counted(reinterpret_cast<vf4_t*>(const_cast<void*>(ra)) + u * 64 + t, va);
-                st16_nt_counted(reinterpret_cast<vf4_t*>(const_cast<void*>(rb)) + u * 64 + t, vb);
-            }
-        } else if constexpr (EXP & 32) {
-            // ablation: plain (write-back) dword stores instead of streaming ones
-            auto rowp = [&](const float (&e)[J][R], const float (&sp)[R], const void* base) {
-                static_for<0, N / T>([&](auto mc) {
-                    constexpr int m = decltype(mc)::value;
-                    if constexpr (m % (NB / T) < J) st4_sbase<4 * T * m>(ve, val(mc, e, sp), base);
-                    else st4_sbase<4 * T * m>(vo - 4u * (NB - T), val(mc, e, sp), base);
-                });
-            };
-            rowp(ea, sa, ra);
-            rowp(eb, sb, rb);
-        } else {
-            row(ea, sa, ra);
-            row(eb, sb, rb);
-        }
+        row(ea, sa, ra);
+        row(eb, sb, rb);
         if constexpr (MODE == 2) {
             // bin N/2 = NB * (R/2): even slot j = 0, r = R/2, lane 0 (one
             // lane-0 store per row, counted; rb is the sink for a missing frame)
@@ -453,15 +426,8 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
 //   VAR 1: bulk, stores straight from registers
 //   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
 // N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
-// EXP: timing ablations for scripts/membench.hip only (the library instantiates
-// EXP = 0): bit 0 FFT without its LDS exchanges, bit 1 no FFT, bit 2 no row
-// stores, bit 3 no span loads, bit 4 the rows as 16 B/lane stores, bit 5 plain
-// instead of streaming row stores, bit 6 only the 2 hop new samples of a span
-// (the HBM traffic of a ring, the LDS-DMA count of one), bits 7/8 span DMA
-// with nt / sc1, bits 9/10 row stores with sc1 / nt (default sc0 sc1 nt).  Results are
-// wrong under bits 0-4 and 6.
-template <int N, int MODE, int VAR, int EXP = 0>
-__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ? ((EXP & 2048) ? 4 : 3) : 1)
+template <int N, int MODE, int VAR>
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ? 3 : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink,
@@ -480,18 +446,12 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // per counter value, each run walked with VAR 3's ring
     constexpr bool DRING = VAR == 5;
     constexpr bool RING = VAR == 3 || DRING;
-    // EXP bit 13 (probe): dynamic band walk -- each wave takes its next pair from
-    // its XCD's counter (ctr, passed as `sink`): counter value k is pair
-    // (k / DB) * 8 DB + xcd * DB + k % DB, so the chip works on one moving band and
-    // neighbouring pairs share an L2, while waves balance dynamically.  The
-    // counter atomics are hand-counted VMEM ops like the spans and stores.
-    // VAR 4 (the library's bulk launch for magnitude rows of large jobs) is
-    // this walk: a persistent grid, counters from stream_counters()
-    constexpr bool DYN = (EXP & 8192) != 0 || VAR == 4 || DRING;
-    // EXP bit 14 (probe): two span buffers per transform slot, the span of pair
-    // i+2 DMA'd while pair i is transformed, pair i+1's waited for before pair
-    // i's stores (LDS: 2 workgroups per CU instead of 3)
-    constexpr bool D2V = (EXP & 16384) != 0;
+    // VAR 4 / 5: the dynamic band walk -- each wave takes its next pair (run) from
+    // a counter of its (XCD group, slot) stream, so the chip works on one moving
+    // band and neighbouring pairs share an L2 while waves balance dynamically;
+    // a persistent grid, counters from stream_counters().  The counter atomics
+    // are hand-counted VMEM ops like the spans and stores.
+    constexpr bool DYN = VAR == 4 || DRING;
     constexpr bool STAGE = BULK && MODE == 0 && G::NPASS > 1 && G::T > 1;
     // power rows (N = 1024): the DIRECT stores below, keeping only the
     // 64-bin blocks under N/2 plus one lane for bin N/2
@@ -500,17 +460,15 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // complex rows (N = 1024): DIRECT with 8 B/lane stores, conj() for the mirror blocks
     constexpr bool CPXD = BULK && MODE == 1 && G::T == 64 && G::NPASS > 1;
     constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
-    constexpr bool D2 = D2V && GLDS && !RING && !DYN;
-    // floats per transform: hop <= N/2 (MEL and the EXP bit 11 probe: hop <= 256)
-    constexpr int SPAN = GLDS ? (((EXP & 2048) || MEL) ? N + 256 : N + N / 2) : 1;
+    // floats per transform: hop <= N/2 (MEL: hop <= 256)
+    constexpr int SPAN = GLDS ? (MEL ? N + 256 : N + N / 2) : 1;
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
     // written as 16 B/lane stores
     constexpr bool DIRECT = GLDS && G::T == 64;
     static_assert(!RING || DIRECT, "ring spans: one wave per transform on the LDS-DMA path");
     // stores per pair (both rows): power rows keep half the blocks + bin N/2
-    constexpr int NST = (EXP & 4) ? 0 : (EXP & 16) ? 8 : MEL ? (MODE == 3 ? 4 : 2)
-                                                       : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
+    constexpr int NST = MEL ? (MODE == 3 ? 4 : 2) : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
@@ -518,20 +476,16 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr int XF = RI ? (ri_floats<N>() + 3) / 4 * 2 : G::LDS;   // float2 per transform (16 B multiple)
     constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
     __shared__ __attribute__((aligned(16))) float2 lds[LDSN];   // 16 B: pass_exchange_ri's b128 writes
-    // EXP bit 11 (occupancy probe, wrong results): a 128-entry twiddle table and
-    // N + 256 float spans, so 4 workgroups fit per CU
-    constexpr int TWE = (EXP & 2048) ? 128 : TwLayout<N>::ENTRIES;
-    __shared__ float2 ltab[TWE];
-    __shared__ float span_all[GLDS ? F * SPAN * (D2 ? 2 : 1) : 1];
-    using TWT = std::conditional_t<(EXP & 2048) != 0, TwMask<N>, TwTab<N>>;
-    const TWT tw{ltab};
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    __shared__ float span_all[GLDS ? F * SPAN : 1];
+    const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
     // window values 0.5 w[t + r T], packed two per VGPR pair (pk_mul_bcast)
     vf2_t wp[(G::P + 1) / 2];
 #pragma unroll
     for (int r = 0; r < G::P; ++r) {
-        const float wr = (EXP & 65536) ? 0.5f : 0.5f * win[t + r * G::T];   // bit 16 (probe): no window loads
+        const float wr = 0.5f * win[t + r * G::T];
         if (r & 1) wp[r / 2].y = wr;
         else wp[r / 2] = vf2_t{wr, 0.0f};
     }
@@ -595,8 +549,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         p = (long long)blockIdx.x * ch + slot * rl;
         p_end = (long long)(blockIdx.x + 1) * ch < pairs ? (long long)(blockIdx.x + 1) * ch : pairs;
         p_step = 1;
-    } else if constexpr ((EXP & 4096) != 0) {   // probe: persistent band walk (lab launches cap0 blocks)
-        band_walk(pairs, F, slot, &p, &p_end, &p_step);
     } else if constexpr (DYN) {
         p = 0;   // set below from the XCD's counter
         p_end = pairs;
@@ -618,19 +570,14 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // membench.hip k_wprobe BAND 1: 0.896 of peak for pure writes against 0.840
     // for 2 MB chunks dealt round robin); a stream past its eighth is done.
     // 3.2967 -> 3.2556 ms for the config-5 shard, same buffers, bit-identical
-    // (profiles/r04_kbench_xcd_eighths.jsonl).  EXP bit 18 (lab): round 3's one
-    // chip-wide band in which every XCD owns 4 MB of each 32 MB.
+    // (profiles/r04_kbench_xcd_eighths.jsonl).
     const long long nrun = DYN ? (pairs + rl - 1) / rl : 0, r8 = (nrun + 7) / 8;
     auto band_pair = [&](unsigned k) -> long long {
         const long long DB = 1LL << dbs;
-        if constexpr ((EXP & 262144) == 0) {
-            const long long g = stream / F, sl = stream % F;   // wave-uniform (stream is readfirstlane'd)
-            const long long it = g * r8 + (long long)(k >> dbs) * (F * DB) + sl * DB + (long long)(k & (DB - 1));
-            const long long ge = (g + 1) * r8 < nrun ? (g + 1) * r8 : nrun;
-            return it < ge ? it : pairs;
-        } else {
-            return (long long)(k >> dbs) * (8 * F * DB) + (long long)stream * DB + (long long)(k & (DB - 1));
-        }
+        const long long g = stream / F, sl = stream % F;   // wave-uniform (stream is readfirstlane'd)
+        const long long it = g * r8 + (long long)(k >> dbs) * (F * DB) + sl * DB + (long long)(k & (DB - 1));
+        const long long ge = (g + 1) * r8 < nrun ? (g + 1) * r8 : nrun;
+        return it < ge ? it : pairs;
     };
     unsigned rr = 0;   // lane 0: an issued counter atomic's result (valid after a vmcnt wait)
     auto grab = [&]() {
@@ -664,8 +611,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // GLDS: the pair's span [fa*hop, fa*hop + hop + N) goes HBM/L2 -> LDS by
     // 16 B/lane LDS-DMA, issued right after the previous span was read, so it
     // lands while that pair is transformed -- no VGPRs held across iterations.
-    float* span = span_all + (GLDS ? slot * SPAN * (D2 ? 2 : 1) : 0);
-    float* span_dst = span;   // where issue_span puts the next span (D2: alternates)
+    float* span = span_all + (GLDS ? slot * SPAN : 0);
     // Pairs that reach past the end of the signal (the zero-padded tail, at
     // most a few per channel) fill the span with ordinary bounds-checked loads
     // and LDS stores instead: the compiler waits on those itself, and being
@@ -674,11 +620,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         const float* s0 = sig + cc * ch_stride + ff * hop;
         const int len = (int)(N + hop), lane = t & 63;
         if (ff * hop + len <= n) {
-            for (int u = t >> 6; u * 256 < ((EXP & 64) ? 2 * (int)hop : len); u += G::T / 64) {
+            for (int u = t >> 6; u * 256 < len; u += G::T / 64) {
                 const int e = u * 256 + lane * 4;
-                if constexpr (EXP & 128) glds16_pol<1>(s0 + (e < len ? e : 0), span_dst + u * 256);
-                else if constexpr (EXP & 256) glds16_pol<2>(s0 + (e < len ? e : 0), span_dst + u * 256);
-                else glds16(s0 + (e < len ? e : 0), span_dst + u * 256);
+                glds16(s0 + (e < len ? e : 0), span + u * 256);
             }
         } else {
             const long long left = n - ff * hop;   // samples of this span inside the signal
@@ -687,7 +631,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 vf4_t q;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) q[k] = e + k < left ? s0[e + k] : 0.0f;
-                *reinterpret_cast<vf4_t*>(span_dst + u * 256 + lane * 4) = q;
+                *reinterpret_cast<vf4_t*>(span + u * 256 + lane * 4) = q;
             }
         }
     };
@@ -703,15 +647,12 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         rsn = rs + h2 >= rc ? rs + h2 - rc : rs + h2;
         for (int k = rc - h2; k < rc; ++k) {
             const int sl = rsn + k >= rc ? rsn + k - rc : rsn + k;
-            if constexpr (EXP & 128) glds16_pol<1>(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
-            else if constexpr (EXP & 256) glds16_pol<2>(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
-            else glds16(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
+            glds16(s0 + k * 256 + (t & 63) * 4, span + sl * 256);
         }
     };
     auto load_pair = [&](long long cc, long long ff) {
         if constexpr (RING) rsn = 0;   // whole span, chunk k in slot k
-        if constexpr (EXP & 8) {
-        } else if constexpr (GLDS) {
+        if constexpr (GLDS) {
             issue_span(cc, ff);
         } else if constexpr (TAIL) {
             const float* s = sig + cc * ch_stride;
@@ -729,18 +670,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     };
     // the first span's DMA is in flight while the block stages its twiddles
     if (any) load_pair(c, fa);
-    if constexpr (D2) {   // and the second pair's, into the other buffer
-        if (any && p + p_step < p_end) {
-            long long c1, f1;
-            locate(p + p_step, &c1, &f1);
-            span_dst = span + SPAN;
-            issue_span(c1, f1);
-        }
-    }
-    // D2: LDS-DMA ops of one full span (hop <= N/2), and whether the span issued
-    // this iteration is in flight (a tail span is filled synchronously)
-    const int nd = D2 ? (int)((N + hop + 255) >> 8) : 0;
-    bool d2_async = false;
     if constexpr (DYN) {
         if constexpr (DRING) {
             if (any) grab();   // -> the next run
@@ -748,12 +677,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (any && pn < pairs) grab();   // -> the pair after pn
         }
     }
-    if constexpr ((EXP & 32768) != 0) {   // bit 15 (probe): no twiddle staging
-    } else if constexpr ((EXP & 2048) != 0) {
-        for (int i = threadIdx.x; i < TWE; i += WG) ltab[i] = gpass[i];
-    } else {
-        stage_twiddles<N, WG>(ltab, gpass, gtab);
-    }
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
     if constexpr (MEL) {
         int* const mi = reinterpret_cast<int*>(mel_lds);
         for (int i = threadIdx.x; i < mel.nnz; i += WG) mel_lds[i] = mel.W[i];
@@ -835,26 +759,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                 if (pnn < pairs) grab();
             }
             pn = pnn;
-        } else if constexpr (D2) {
-            // this pair's span is complete (waited for before the previous
-            // pair's stores, or by the prologue); after reading it, its buffer
-            // takes the span of the pair two ahead
-            float* cur = span + (kk & 1) * SPAN;
-#pragma unroll
-            for (int r = 0; r < G::P; ++r) {
-                xa[r] = cur[t + r * G::T];
-                xb[r] = cur[hop + t + r * G::T];
-            }
-            lgkm_wait0();   // span read before it is refilled
-            d2_async = false;
-            const long long p2 = p + 2 * p_step;
-            if (p2 < p_end) {
-                long long c2, f2;
-                locate(p2, &c2, &f2);
-                span_dst = cur;
-                issue_span(c2, f2);
-                d2_async = f2 * hop + N + hop <= n;
-            }
         } else if constexpr (GLDS) {
             // younger than this span's DMA: only the previous pair's NST stores
             vm_wait<NST>();
@@ -869,14 +773,13 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (more) load_pair(cn, fn);
         }
         float2 v[G::P];
-        if constexpr (!(EXP & 131072) && BULK && G::T == 64) {
+        if constexpr (BULK && G::T == 64) {
             // the span reads come in pairs (r, r + 1) of one frame (ds_read2st64: adjacent
             // registers); one v_pk_mov_b32 per (frame a, frame b) register pair instead of
             // two v_mov_b32.  With the exchange reads as single ds_read_b32 (RIV 1) the
             // loop's v_movs drop from 87 to 27 (power rows; VALU 419 -> 370 per pair),
             // bit-identical, 2.766 -> 2.741 ms power / 3.410 -> 3.399 ms magnitude
-            // (profiles/r04_kbench_stft_movefree.jsonl).  EXP bit 17 (lab): round 3's
-            // read2 pairing and v_movs.
+            // (profiles/r04_kbench_stft_movefree.jsonl).
 #pragma unroll
             for (int i = 0; i < G::P / 2; ++i) {
                 const vf2_t A = {xa[2 * i], xa[2 * i + 1]}, B = {xb[2 * i], xb[2 * i + 1]};
@@ -896,18 +799,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
-        if constexpr (!(EXP & 2))
-            fft_regs<N, true, true, RI, TWT, (EXP & 1) != 0, false, (EXP & 131072) ? 0 : 1>(v, t, my, tw);
-        if constexpr (D2) {
-            // the next pair's span: younger than it are the previous pair's NST
-            // stores and, when in flight, the span just issued
-            if (more) {
-                if (!d2_async) vm_wait<NST>();
-                else if (nd == 5) vm_wait<NST + 5>();
-                else if (nd == 6) vm_wait<NST + 6>();
-                else vm_wait<NST>();
-            }
-        }
+        fft_regs<N, true, true, RI, TwTab<N>, false, false, 1>(v, t, my, tw);
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROWR) * ES;
         char* rowb = rowa + ROWR * ES;
         const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
@@ -917,7 +809,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                               reinterpret_cast<float*>(my), mel_lds, mi + mel.nnz, mi + mel.nnz + 3 * mel.nc,
                               mel_lds + mel_dpos, mel_lds + mel_dpos + mel.C * mel.M, mel);
         } else if constexpr (DIRECT) {
-            direct_rows<N, MODE, EXP>(v, t, rowa, rowb, has_b, sink);
+            direct_rows<N, MODE>(v, t, rowa, rowb, has_b, sink);
         } else if constexpr (STAGE) {
             // both magnitude rows through the (now idle) exchange buffer, then
             // full-line 16 B/lane streaming stores: 2N/(4T) instead of 2P per lane
@@ -969,7 +861,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if constexpr (DRING) kk = kk + 1 == rl ? 0 : kk + 1;
             else ++kk;
         }
-        if constexpr (D2) ++kk;
     }
     if constexpr (DYN) {   // the XCD's last wave out resets its counters for the next launch
         vm_wait<0>();
@@ -1084,10 +975,10 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
 // its pair's two rows, 128 B per instruction.  Spans that reach past the end
 // of the signal (the zero-padded tail) are staged through LDS with the zero
 // rule, in the same loop.  Persistent grid, static XCD walk over frame-pair
-// couples.  EXP (lab): bit 1 no FFT, bit 2 no stores.
+// couples.
 // ------------------------------------------------------------------------
 constexpr int R33_BUF = 33 * R32_ROW;   // 33 rows: the mirror read of lane 0 touches row 32
-template <int MODE, int EXP = 0>
+template <int MODE>
 __global__ void __launch_bounds__(256, 2)
 k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, long long frames, const float* win,
            float* out, long long out_ch_stride, const float2* tw1024) {
@@ -1203,12 +1094,10 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
             locate(itn, &cn, &qn, &validn, &edgen, &rwn);
             if (!edgen) load_bulk(cn, qn);
         }
-        if constexpr (!(EXP & 2)) {
-            dft32<true>(v);
-            r32_twiddle<true>(v, ltw + mr);
-            r32_transpose(v, buf, mr, m);
-            dft32<true>(v);
-        }
+        dft32<true>(v);
+        r32_twiddle<true>(v, ltw + mr);
+        r32_transpose(v, buf, mr, m);
+        dft32<true>(v);
         // Z[N - k] (lane 32 - m, register 31 - r; lane 0: register 32 - r) through the
         // buffer: registers 16..31 for the power rows' bins 0..512, all 32 for the
         // magnitude rows, whose upper half each lane computes from its own
@@ -1222,7 +1111,7 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
         float2 zu[16];   // MODE 0: zu[31 - r] = Z[N - (m + 32 r)], r >= 16 (lane 0, r = 16: Z[512] itself)
         if constexpr (MODE == 0) lds_rd64x16<0, 8 * R32_ROW>(buf + R32_ROW * (m == 0 ? 1 : 0) + ((32 - m) & 31), zu);
         xsync<64>();   // the next couple's transpose writes stay behind these reads
-        if constexpr (!(EXP & 4) && MODE == 0) {
+        if constexpr (MODE == 0) {
             // magnitude rows, all N bins: lane m holds bin m + 32 r of its pair's two
             // rows, r < 32.  Blocks 2j, 2j + 1 of one row are an aligned 256 B run: one
             // v_permlane32_swap per register pair moves half 0's block 2j + 1 up and half
@@ -1259,7 +1148,7 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
                 for (int j = 0; j < 16; ++j) __builtin_nontemporal_store(B[2 * j + 1], rb + RW + 64 * j);
             }
         }
-        if constexpr (!(EXP & 4) && MODE == 2) {
+        if constexpr (MODE == 2) {
             const long long fa = 2 * q;
             float* rowa = out + c * out_ch_stride + fa * RW + m;
             float* rowb = rowa + RW;
