@@ -52,6 +52,16 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_power_device(vv_dsp_stft* h, const vv
                                                         size_t n, size_t nch, size_t ch_stride,
                                                         vv_dsp_real* d_out_power, size_t out_ch_stride,
                                                         void* stream, size_t* out_frames);
+/* The same power rows placed row_pitch floats apart (row_pitch >= fft_size/2+1;
+ * the pad floats past bin fft_size/2 are not written; out_ch_stride >= frames x
+ * row_pitch).  A pitch of a whole number of 128 B lines -- 544 for fft_size
+ * 1024: 17 lines -- starts every row on a line, so the rows leave as whole-line
+ * stores; the values equal vv_dsp_stft_power_device's bit for bit.  The
+ * reference's packed layout (mel.h:156-161) is row_pitch = fft_size/2+1. */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_stft_power_pitched_device(vv_dsp_stft* h, const vv_dsp_real* d_signal,
+                                                                size_t n, size_t nch, size_t ch_stride,
+                                                                vv_dsp_real* d_out_power, size_t out_ch_stride,
+                                                                size_t row_pitch, void* stream, size_t* out_frames);
 /* One shard of a long signal's frames: rows of frames [frame0, frame0 + nframes)
  * of the same spectrogram, row of frame f at d_out + (f - frame0) * row.
  * out_kind 0: magnitudes [fft_size] floats, 1: complex spectrum [fft_size]
@@ -153,6 +163,15 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_mfcc_process_device(const vv_dsp_mfcc_plan
                                                           size_t num_frames, vv_dsp_real* d_out_mfcc, void* stream);
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_log_mel_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
                                                      size_t num_frames, vv_dsp_real* d_out_log_mel, void* stream);
+/* the same on power rows row_pitch >= n_fft/2+1 floats apart (e.g.
+ * vv_dsp_stft_power_pitched_device's); the values do not depend on the pitch */
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_mfcc_process_pitched_device(const vv_dsp_mfcc_plan* plan,
+                                                                  const vv_dsp_real* d_power, size_t num_frames,
+                                                                  size_t row_pitch, vv_dsp_real* d_out_mfcc,
+                                                                  void* stream);
+VV_DSP_NODISCARD vv_dsp_status vv_dsp_log_mel_pitched_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
+                                                             size_t num_frames, size_t row_pitch,
+                                                             vv_dsp_real* d_out_log_mel, void* stream);
 /* Signal -> log-mel / MFCC rows without the power spectrogram in HBM:
  * d_signal [nch][n] (ch_stride floats apart) -> d_out [nch][frames][n_mels]
  * (log-mel) or [nch][frames][num_mfcc_coeffs] (MFCC), out_ch_stride floats

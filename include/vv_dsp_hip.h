@@ -113,6 +113,10 @@ int vvhip_stft_spectrogram_host(vvhip_stft* h, const float* signal, size_t n, fl
 int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
                                   size_t ch_stride, void* d_out, size_t out_ch_stride,
                                   int out_kind, void* stream);
+/* Power rows (kind 2) with rows row_pitch >= nfft/2+1 floats apart (the pad
+ * floats are not written); out_ch_stride >= frames * row_pitch. */
+int vvhip_stft_power_pitched_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch, size_t ch_stride,
+                                    float* d_out, size_t out_ch_stride, size_t row_pitch, void* stream);
 /* Frames [frame0, frame0 + nframes) of the same spectrogram (the row of frame
  * f is out + (f - frame0) * row): one shard of a long signal's frames.  With an
  * even frame0 the rows are bit-identical to the whole-signal call (frames are
@@ -171,6 +175,9 @@ void vvhip_mel_destroy(vvhip_mel* m);
  *      1: power rows -> MFCC [frames][n_coeffs]
  *      2: log-mel rows [frames][n_mels] -> MFCC [frames][n_coeffs] */
 int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_out, int kind, void* stream);
+/* the same with power rows row_pitch >= nbins floats apart (kinds 0 / 1; 0 = nbins) */
+int vvhip_mel_pitched_device(vvhip_mel* m, const float* d_in, size_t frames, size_t row_pitch, float* d_out, int kind,
+                             void* stream);
 /* signal [ch][n] (ch_stride floats apart) -> log-mel (kind 0) or MFCC (kind 1)
  * rows [ch][frame][n_mels | n_coeffs]: the stft's power rows feed the mel plan
  * in one kernel when nfft = 1024 (else two launches, same values) */

@@ -30,8 +30,17 @@ class StftParams(C.Structure):
     _fields_ = [("fft_size", C.c_size_t), ("hop_size", C.c_size_t), ("window", C.c_int)]
 
 
-def load(path):
+def load(spec):
+    """`path` or `path@KNOB=V+KNOB2=V2`: knobs set in that build (vvhip_debug_set);
+    to compare knob settings of one build, pass copies of the .so under other names
+    (one file is loaded once per process)"""
+    path, _, knobs = spec.partition("@")
     L = C.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_NOW)
+    L.vvhip_debug_set.argtypes = [C.c_char_p, C.c_longlong]
+    for kv in filter(None, knobs.split("+")):
+        k, v = kv.split("=")
+        if L.vvhip_debug_set(k.encode(), int(v)) != 0:
+            raise SystemExit(f"{path}: unknown knob {k}")
     L.vvhip_last_error.restype = C.c_char_p
     L.vv_dsp_fir_design_lowpass.argtypes = [vp, sz, C.c_float, C.c_int]
     L.vv_dsp_fir_plan_create.argtypes = [vp, sz, C.POINTER(vp)]
@@ -39,6 +48,8 @@ def load(path):
     L.vv_dsp_stft_create.argtypes = [C.POINTER(StftParams), C.POINTER(vp)]
     for f in ("spectrogram", "power"):
         getattr(L, f"vv_dsp_stft_{f}_device").argtypes = [vp, vp, sz, sz, sz, vp, sz, vp, C.POINTER(sz)]
+    if hasattr(L, "vv_dsp_stft_power_pitched_device"):
+        L.vv_dsp_stft_power_pitched_device.argtypes = [vp, vp, sz, sz, sz, vp, sz, sz, vp, C.POINTER(sz)]
     for f in ("log_mel", "mfcc"):
         getattr(L, f"vv_dsp_stft_{f}_device").argtypes = [vp, vp, vp, sz, sz, sz, vp, sz, vp, C.POINTER(sz)]
     L.vv_dsp_mfcc_init.argtypes = [sz, sz, sz, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, C.c_float,
@@ -83,14 +94,20 @@ def _stft(L):
 
 
 def case_stft_rows(L, s, kind, nch, seconds):
+    """kind mag / pow (packed 513-float rows) / pow544 (rows 544 floats apart;
+    bytes counted as the 513 floats written)"""
     n = seconds * 48000
     fr = frames_of(n)
-    w = {"mag": 1024, "pow": 513}[kind]
+    w = {"mag": 1024, "pow": 513, "pow544": 544}[kind]
     sig, out = buf(("stft", kind, nch, n), lambda: (torch.rand(nch, n, device="cuda") * 2 - 1,
                                                     torch.empty(nch, fr, w, device="cuda")))
     h = _stft(L)
-    f = L.vv_dsp_stft_spectrogram_device if kind == "mag" else L.vv_dsp_stft_power_device
     nf = sz()
+    if kind == "pow544":
+        f = L.vv_dsp_stft_power_pitched_device
+        run = lambda: ok(L, f(h, sig.data_ptr(), n, nch, n, out.data_ptr(), fr * w, w, s, C.byref(nf)), "stft")  # noqa
+        return run, nch * n * 4 + nch * fr * 513 * 4, (lambda: out[:, :, :513].clone())
+    f = L.vv_dsp_stft_spectrogram_device if kind == "mag" else L.vv_dsp_stft_power_device
     return (lambda: ok(L, f(h, sig.data_ptr(), n, nch, n, out.data_ptr(), fr * w, s, C.byref(nf)), "stft")), \
         nch * n * 4 + nch * fr * w * 4, (lambda: out.clone())
 
@@ -120,11 +137,24 @@ def case_c2c(L, s, n=1024, batch=65536):
         2 * batch * n * 8, (lambda: y.clone())
 
 
+def burst(case, k):
+    """k launches back to back per timed call (the per-launch time is ms / k)"""
+    fn, byts, get = case
+
+    def run():
+        for _ in range(k):
+            fn()
+    return run, byts * k, get
+
+
 CASES = {
     "fir": case_fir,
     "stft": lambda L, s: case_stft_rows(L, s, "mag", 32, 600),
     "stft60": lambda L, s: case_stft_rows(L, s, "mag", 1, 60),
+    "stft256ch": lambda L, s: case_stft_rows(L, s, "mag", 256, 600),
+    "stft60x10": lambda L, s: burst(case_stft_rows(L, s, "mag", 1, 60), 10),
     "stftpow": lambda L, s: case_stft_rows(L, s, "pow", 32, 600),
+    "stftpow544": lambda L, s: case_stft_rows(L, s, "pow544", 32, 600),
     "logmel": lambda L, s: case_mel(L, s, False),
     "mfcc": lambda L, s: case_mel(L, s, True),
     "c2c1024": case_c2c,
@@ -141,6 +171,8 @@ def main():
     a = ap.parse_args()
     libs = [load(p) for p in a.libs.split(",")]
     tags = [os.path.basename(p) for p in a.libs.split(",")]
+    if len(set(p.partition("@")[0] for p in a.libs.split(","))) != len(tags):
+        raise SystemExit("each build must be a distinct file (copy the .so to compare knob settings)")
     torch.cuda.init()
     s = torch.cuda.current_stream()
     sp = s.cuda_stream

@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256)
 k_mel_grp(const float* __restrict__ in, long long frames, int in_len, int n_mels, int n_coeffs,
           const float* __restrict__ W, int nnz, const int* __restrict__ chunks, int nc,
           const int* __restrict__ cbeg, const float* __restrict__ D, const float* __restrict__ lift, float eps,
-          float* __restrict__ out, int waves_per_block, int row_floats, int dma) {
+          float* __restrict__ out, int waves_per_block, int row_floats, int dma, int row_len) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr bool FILT = MODE != 2, DCT = MODE != 0;
     const int M = n_mels, C = n_coeffs;
@@ -72,9 +72,10 @@ k_mel_grp(const float* __restrict__ in, long long frames, int in_len, int n_mels
     for (long long g = (long long)blockIdx.x * waves_per_block + wv; g < groups; g += stride) {
         const long long f0 = g * FR;
         const int nf = (int)(frames - f0 < FR ? frames - f0 : FR);
-        // FR consecutive rows = one contiguous block; missing rows read as 0
+        // FR consecutive rows = one contiguous block (rows in_len floats apart, the
+        // last one read up to its row_len data floats only); missing rows read as 0
         const float* src = in + f0 * in_len;
-        const int valid = nf * in_len;
+        const int valid = (nf - 1) * in_len + row_len;
         if (dma && nf == FR && (g + 1 < groups || (valid & 3) == 0)) {
             // full group: HBM -> LDS by 16 B/lane LDS-DMA, every piece in flight
             // at once (a load-then-store loop would serialise on each load)
@@ -197,10 +198,12 @@ int mel_chunk_schedule(const int* meta, int n_mels, std::vector<int>* chunks, st
 
 hipError_t launch_mel_grp(int mode, const float* in, long long frames, int nbins, int n_mels, int n_coeffs,
                           const float* W, int nnz, const int* chunks, int nc, const int* cbeg, const float* D,
-                          const float* lift, float eps, float* out, hipStream_t s) {
+                          const float* lift, float eps, float* out, hipStream_t s, int in_pitch) {
     if (frames <= 0) return hipSuccess;
     const bool filt = mode != 2, dct = mode != 0;
-    const int in_len = mode == 2 ? n_mels : nbins;
+    // floats per input row: power rows may sit in_pitch apart (a group of FR rows
+    // is still one contiguous block; the pad floats come along and are never read)
+    const int in_len = mode == 2 ? n_mels : (in_pitch > 0 ? in_pitch : nbins);
     // layout as in k_mel_grp: DCT table and per-wave areas 16 B aligned
     const size_t dpos = ((filt ? (size_t)nnz + 3 * (size_t)nc + n_mels + 1 : 0) + 3) & ~(size_t)3;
     const size_t shared = sizeof(float) * ((dpos + (dct ? (size_t)n_coeffs * n_mels + n_coeffs : 0) + 3) & ~(size_t)3);
@@ -224,7 +227,7 @@ hipError_t launch_mel_grp(int mode, const float* in, long long frames, int nbins
     const dim3 grid((unsigned)blocks), block(64 * wpb);
 #define L(MM, FF)                                                                                            \
     hipLaunchKernelGGL((k_mel_grp<MM, FF>), grid, block, lds, s, in, frames, in_len, n_mels, n_coeffs, W, nnz, \
-                       chunks, nc, cbeg, D, lift, eps, out, wpb, row_floats(FF), dma)
+                       chunks, nc, cbeg, D, lift, eps, out, wpb, row_floats(FF), dma, mode == 2 ? in_len : nbins)
 #define LF(MM) \
     if (fr == 4) L(MM, 4); else if (fr == 2) L(MM, 2); else L(MM, 1);
     if (mode == 0) { LF(0) }

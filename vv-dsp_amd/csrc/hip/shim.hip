@@ -638,6 +638,38 @@ int vvhip_stft_spectrogram_device(vvhip_stft* h, const float* d_signal, size_t n
                            (hipStream_t)stream);
 }
 
+// power rows [ch][frame][nfft/2+1] with rows row_pitch floats apart: in the
+// kernel for power-of-two nfft; other lengths write packed rows to scratch and
+// place them with one strided copy (the same values)
+int vvhip_stft_power_pitched_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch, size_t ch_stride,
+                                    float* d_out, size_t out_ch_stride, size_t row_pitch, void* stream) {
+    if (!h || !d_signal || !d_out) return ST_NULL;
+    const size_t nb = h->nfft / 2 + 1, frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    if (row_pitch < nb) return fail(ST_SIZE, "power row pitch below nfft/2+1");
+    if (nch > 1 && out_ch_stride < frames * row_pitch) return fail(ST_SIZE, "channel stride below frames x row pitch");
+    if (nch == 0) return ST_OK;
+    const hipStream_t s = (hipStream_t)stream;
+    if (row_pitch == nb)
+        return stft_frames_run(h, d_signal, n, nch, ch_stride, d_out, out_ch_stride, 2, s);
+    const float* win = stft_window_here(h);
+    if (!win) return fail(ST_INTERNAL, "stft window on the current device");
+    if (stft_fused_supported((long long)h->nfft)) {
+        HIPCHK(launch_stft((long long)h->nfft, (long long)h->hop, 2, d_signal, (long long)n, (long long)nch,
+                           (long long)ch_stride, (long long)frames, win, d_out, (long long)out_ch_stride, s,
+                           (long long)row_pitch),
+               ST_INTERNAL);
+        return ST_OK;
+    }
+    Scratch pw(s);
+    HIPCHK(pw.alloc(sizeof(float) * nch * frames * nb), ST_INTERNAL);
+    if (int st = stft_frames_run(h, d_signal, n, nch, ch_stride, pw.p, frames * nb, 2, s)) return st;
+    for (size_t c = 0; c < nch; ++c)
+        HIPCHK(hipMemcpy2DAsync(d_out + c * out_ch_stride, sizeof(float) * row_pitch, (const float*)pw.p + c * frames * nb,
+                                sizeof(float) * nb, sizeof(float) * nb, frames, hipMemcpyDeviceToDevice, s),
+               ST_INTERNAL);
+    return ST_OK;
+}
+
 int vvhip_stft_spectrogram_range_device(vvhip_stft* h, const float* d_signal, size_t n, size_t nch,
                                         size_t ch_stride, size_t frame0, size_t nframes, void* d_out,
                                         size_t out_ch_stride, int out_kind, void* stream) {
@@ -1438,15 +1470,23 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
 static size_t mel_in_len(const vvhip_mel* m, int kind) { return kind == 2 ? (size_t)m->n_mels : (size_t)m->nbins; }
 static size_t mel_out_len(const vvhip_mel* m, int kind) { return kind == 0 ? (size_t)m->n_mels : (size_t)m->n_coeffs; }
 
-int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_out, int kind, void* stream) {
+// row_pitch (kinds 0 / 1): floats from one power row's start to the next, >= nbins (0: nbins)
+int vvhip_mel_pitched_device(vvhip_mel* m, const float* d_in, size_t frames, size_t row_pitch, float* d_out, int kind,
+                             void* stream) {
     if (!m || !d_in || !d_out) return ST_NULL;
     if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
     if ((kind != 2 && m->nbins == 0) || (kind != 0 && m->n_coeffs == 0)) return fail(ST_RANGE, "mel plan lacks tables");
+    if (kind == 2) row_pitch = 0;
+    if (row_pitch != 0 && (row_pitch < (size_t)m->nbins || row_pitch > (1u << 20)))
+        return fail(ST_SIZE, "mel input row pitch below the row length");
     if (frames == 0) return ST_OK;
     HIPCHK(launch_mel_grp(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->nnz, m->chunks,
-                          m->nc, m->cbeg, m->D, m->lift, m->eps, d_out, (hipStream_t)stream),
+                          m->nc, m->cbeg, m->D, m->lift, m->eps, d_out, (hipStream_t)stream, (int)row_pitch),
            ST_INTERNAL);
     return ST_OK;
+}
+int vvhip_mel_device(vvhip_mel* m, const float* d_in, size_t frames, float* d_out, int kind, void* stream) {
+    return vvhip_mel_pitched_device(m, d_in, frames, 0, d_out, kind, stream);
 }
 
 // Signal -> log-mel (kind 0) / MFCC (kind 1) rows [ch][frame][n_mels or

@@ -430,8 +430,8 @@ template <int N, int MODE, int VAR>
 __global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ? 3 : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
-            long long out_ch_stride, const float2* gpass, const float2* gtab, long long chunk, float* sink,
-            unsigned* ctrs, MelArgs mel) {
+            long long out_ch_stride, long long row_pitch, const float2* gpass, const float2* gtab, long long chunk,
+            float* sink, unsigned* ctrs, MelArgs mel) {
     using G = Geo<N>;
     using Mi = Mirror<N>;
     // MODE 3 / 4: log-mel / MFCC rows from the power rows, which stay in LDS
@@ -495,7 +495,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     for (int i = 0; i < G::NPT; ++i) kb[i] = bfly<N, G::NPASS - 1, true>(t, i);
     constexpr long long ES = MODE == 1 ? 8 : 4;            // bytes per bin
     constexpr long long ROW = MODE == 2 ? N / 2 + 1 : N;   // bins per row
-    const long long ROWR = MODE == 3 ? (long long)mel.M : MODE == 4 ? (long long)mel.C : ROW;
+    // floats (MODE 1: complex values) from one row's start to the next: power rows
+    // may sit `row_pitch` floats apart (>= N/2 + 1, e.g. 544 = 17 whole lines)
+    const long long ROWR = MODE == 3 ? (long long)mel.M : MODE == 4 ? (long long)mel.C : MODE == 2 ? row_pitch : ROW;
     // MEL: the plan's tables in dynamic LDS: W [nnz], chunks [3 nc], cbeg [M + 1], then (MODE 4) D [C M], lift [C]
     extern __shared__ __attribute__((aligned(16))) float mel_lds[];
     const int mel_dpos = MEL ? (mel.nnz + 3 * mel.nc + mel.M + 1 + 3) & ~3 : 0;
@@ -884,8 +886,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
 template <int N, int MODE>
 __global__ void __launch_bounds__(Wg<N>::value)
 k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
-                long long hop, const float* win, void* out, long long out_ch_stride, const float2* gpass,
-                const float2* gtab) {
+                long long hop, const float* win, void* out, long long out_ch_stride, long long row_pitch,
+                const float2* gpass, const float2* gtab) {
     using G = Geo<N>;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     __shared__ float2 lds[F * G::LDS];
@@ -939,8 +941,9 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
 #pragma unroll
         for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<N>(t, q))] = v[q];
         xsync<G::T>();
-        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROW) * ES;
-        char* rowb = rowa + ROW * ES;
+        const long long rp = MODE == 2 ? row_pitch : ROW;   // power rows: row_pitch floats apart
+        char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * rp) * ES;
+        char* rowb = rowa + rp * ES;
 #pragma unroll
         for (int j = 0; j < G::P; ++j) {
             const int k = t + G::T * j;
@@ -981,9 +984,10 @@ constexpr int R33_BUF = 33 * R32_ROW;   // 33 rows: the mirror read of lane 0 to
 template <int MODE>
 __global__ void __launch_bounds__(256, 2)
 k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, long long frames, const float* win,
-           float* out, long long out_ch_stride, const float2* tw1024) {
+           float* out, long long out_ch_stride, long long row_pitch, const float2* tw1024) {
     static_assert(MODE == 0 || MODE == 2, "magnitude or power rows");
     constexpr int N = 1024, HOP = 256, F = 4, RW = MODE == 2 ? N / 2 + 1 : N, SPAN = N + HOP;
+    const long long RP = MODE == 2 ? row_pitch : RW;   // floats from one row's start to the next
     __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R33_BUF];
     __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r)
     for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
@@ -1020,8 +1024,8 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
         *c = half ? c1 : c0;
         *q = half ? q1 : q0;
         *edge_any = 2 * q0 * HOP + SPAN > n || 2 * q1 * HOP + SPAN > n;
-        rw->oa = c0 * out_ch_stride + 2 * q0 * RW;
-        rw->ob = c1 * out_ch_stride + 2 * q1 * RW;
+        rw->oa = c0 * out_ch_stride + 2 * q0 * RP;
+        rw->ob = c1 * out_ch_stride + 2 * q1 * RP;
         rw->two = two;
         rw->ha = 2 * q0 + 1 < frames;
         rw->hb = 2 * q1 + 1 < frames;
@@ -1150,8 +1154,8 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
         }
         if constexpr (MODE == 2) {
             const long long fa = 2 * q;
-            float* rowa = out + c * out_ch_stride + fa * RW + m;
-            float* rowb = rowa + RW;
+            float* rowa = out + c * out_ch_stride + fa * RP + m;
+            float* rowb = rowa + RP;
             const bool hb = fa + 1 < frames;
             float A[16], B[16];
 #pragma unroll
@@ -1185,11 +1189,11 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
             }
             if (rw.ha) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) pa[RW + 64 * j] = B[2 * j];
+                for (int j = 0; j < 8; ++j) pa[RP + 64 * j] = B[2 * j];
             }
             if (rw.two && rw.hb) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) pb[RW + 64 * j] = B[2 * j + 1];
+                for (int j = 0; j < 8; ++j) pb[RP + 64 * j] = B[2 * j + 1];
             }
         }
         c = cn;
@@ -1203,7 +1207,8 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
 template <int N, int MODE>
 static hipError_t run_stft(const float* sig, long long n, long long nch, long long ch_stride,
                            long long frames, long long hop, const float* win, void* out,
-                           long long out_ch_stride, hipStream_t s) {
+                           long long out_ch_stride, hipStream_t s, long long row_pitch) {
+    if (MODE != 2 || row_pitch <= 0) row_pitch = MODE == 2 ? N / 2 + 1 : N;   // packed rows
     if constexpr (Geo<N>::CAN_PAIR) {
         const float2* tN = twiddle_table(N);
         const float2* pN = pass_twiddles(N);
@@ -1257,7 +1262,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 chunk |= rl << 40;
             }
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames, hop, pair0,
-                               cnt, win, out, out_ch_stride, pN, tN, chunk, sink, ctrs, MelArgs{});
+                               cnt, win, out, out_ch_stride, row_pitch, pN, tN, chunk, sink, ctrs, MelArgs{});
         };
         // 16 B aligned output rows allow the staged 16 B/lane stores
         // (power rows are n/2+1 floats: their direct stores are dwords, 4 B suffice;
@@ -1299,7 +1304,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 if (grid < 1) return hipSuccess;
                 stat_inc(STAT_POW_R32);
                 hipLaunchKernelGGL((k_stft_r32<2>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, win,
-                                   (float*)out, out_ch_stride, tN);
+                                   (float*)out, out_ch_stride, row_pitch, tN);
                 return hipGetLastError();
             }
         }
@@ -1313,7 +1318,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 if (grid < 1) return hipSuccess;
                 stat_inc(STAT_MAG_R32);
                 hipLaunchKernelGGL((k_stft_r32<0>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, win,
-                                   (float*)out, out_ch_stride, tN);
+                                   (float*)out, out_ch_stride, row_pitch, tN);
                 return hipGetLastError();
             }
         }
@@ -1364,7 +1369,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const int grid = (int)(need < cap ? need : cap);
         if (grid < 1) return hipSuccess;
         hipLaunchKernelGGL((k_stft_pair_lds<N, MODE>), dim3(grid), dim3(WG), 0, s, sig, n, nch, ch_stride, frames,
-                           hop, win, out, out_ch_stride, pN, tN);
+                           hop, win, out, out_ch_stride, row_pitch, pN, tN);
     }
     return hipGetLastError();
 }
@@ -1414,10 +1419,10 @@ static hipError_t run_stft_mel(const float* sig, long long n, long long nch, lon
     }
     if (dyn_walk)
         hipLaunchKernelGGL((k_stft_pair<N, MODE, 4>), dim3((unsigned)grid), dim3(WG), dyn, s, sig, n, nch, ch_stride,
-                           frames, hop, 0LL, ppc, win, (void*)out, out_ch_stride, pN, tN, chunk, sink, ctrs, mel);
+                           frames, hop, 0LL, ppc, win, (void*)out, out_ch_stride, 0LL, pN, tN, chunk, sink, ctrs, mel);
     else
         hipLaunchKernelGGL((k_stft_pair<N, MODE, 0>), dim3((unsigned)grid), dim3(WG), dyn, s, sig, n, nch, ch_stride,
-                           frames, hop, 0LL, ppc, win, (void*)out, out_ch_stride, pN, tN, chunk, sink, ctrs, mel);
+                           frames, hop, 0LL, ppc, win, (void*)out, out_ch_stride, 0LL, pN, tN, chunk, sink, ctrs, mel);
     return hipGetLastError();
 }
 
@@ -1436,11 +1441,11 @@ hipError_t launch_stft_mel(int kind, long long nfft, long long hop, const float*
 
 hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,
                        long long nch, long long ch_stride, long long frames, const float* win,
-                       void* out, long long out_ch_stride, hipStream_t s) {
-#define CALL(NN)                                                                                     \
-    (mode == 0   ? run_stft<NN, 0>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s) \
-     : mode == 1 ? run_stft<NN, 1>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s) \
-                 : run_stft<NN, 2>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s))
+                       void* out, long long out_ch_stride, hipStream_t s, long long row_pitch) {
+#define CALL(NN)                                                                                                \
+    (mode == 0   ? run_stft<NN, 0>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s, 0)         \
+     : mode == 1 ? run_stft<NN, 1>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s, 0)         \
+                 : run_stft<NN, 2>(sig, n, nch, ch_stride, frames, hop, win, out, out_ch_stride, s, row_pitch))
     switch (nfft) {
         case 2: return CALL(2); case 4: return CALL(4); case 8: return CALL(8); case 16: return CALL(16);
         case 32: return CALL(32); case 64: return CALL(64); case 128: return CALL(128);

@@ -66,9 +66,10 @@ hipError_t launch_promote_real(const float* in, float2* out, long long count, hi
 // ---- mel / MFCC (mel_kernels.hip) ---------------------------------------
 // mode 0: power rows [frames][nbins] -> log-mel [frames][n_mels]
 //      1: power rows -> MFCC [frames][n_coeffs];  2: log-mel rows -> MFCC
+// in_pitch (modes 0 / 1): floats from one power row's start to the next (0: nbins)
 hipError_t launch_mel_grp(int mode, const float* in, long long frames, int nbins, int n_mels, int n_coeffs,
                           const float* W, int nnz, const int* chunks, int nc, const int* cbeg, const float* D,
-                          const float* lift, float eps, float* out, hipStream_t s);
+                          const float* lift, float eps, float* out, hipStream_t s, int in_pitch = 0);
 // host: chunk schedule of the filters' non-zero ranges {lo, len, off}[n_mels] for
 // launch_mel_grp (chunks {lo, len, off}, cbeg[n_mels+1]); returns the chunk length
 int mel_chunk_schedule(const int* meta, int n_mels, std::vector<int>* chunks, std::vector<int>* cbeg);
@@ -129,11 +130,11 @@ hipError_t launch_zero_nyquist_imag(float2* out, long long n, long long batch, l
 
 // ---- STFT (stft_kernels.hip) -------------------------------------------
 // mode 0: magnitude rows [frames][nfft]; 1: complex rows [frames][nfft];
-// 2: power rows [frames][nfft/2+1]
+// 2: power rows [frames][nfft/2+1], row_pitch floats apart (0: packed, nfft/2+1)
 bool stft_fused_supported(long long nfft);
 hipError_t launch_stft(long long nfft, long long hop, int mode, const float* sig, long long n,
                        long long nch, long long ch_stride, long long frames, const float* win,
-                       void* out, long long out_ch_stride, hipStream_t s);
+                       void* out, long long out_ch_stride, hipStream_t s, long long row_pitch = 0);
 // Mel filterbank / log / DCT tables of an MFCC plan (vvhip_mel, device
 // pointers) for the fused signal -> log-mel / MFCC launch
 struct MelArgs {

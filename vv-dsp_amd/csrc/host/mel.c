@@ -203,3 +203,23 @@ vv_dsp_status vv_dsp_log_mel_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_r
     if (!plan->dev) return VV_DSP_ERROR_OUT_OF_RANGE;
     return (vv_dsp_status)vvhip_mel_device(plan->dev, d_power, num_frames, d_out_log_mel, 0, stream);
 }
+
+/* power rows row_pitch floats apart (vv_dsp_stft_power_pitched_device's layout) */
+vv_dsp_status vv_dsp_mfcc_process_pitched_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
+                                                 size_t num_frames, size_t row_pitch, vv_dsp_real* d_out_mfcc,
+                                                 void* stream) {
+    if (!plan || !d_power || !d_out_mfcc) return VV_DSP_ERROR_NULL_POINTER;
+    if (!plan->dev) return VV_DSP_ERROR_OUT_OF_RANGE;
+    if (row_pitch == 0) return VV_DSP_ERROR_INVALID_SIZE;
+    return (vv_dsp_status)vvhip_mel_pitched_device(plan->dev, d_power, num_frames, row_pitch, d_out_mfcc, 1, stream);
+}
+
+vv_dsp_status vv_dsp_log_mel_pitched_device(const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_power,
+                                            size_t num_frames, size_t row_pitch, vv_dsp_real* d_out_log_mel,
+                                            void* stream) {
+    if (!plan || !d_power || !d_out_log_mel) return VV_DSP_ERROR_NULL_POINTER;
+    if (!plan->dev) return VV_DSP_ERROR_OUT_OF_RANGE;
+    if (row_pitch == 0) return VV_DSP_ERROR_INVALID_SIZE;
+    return (vv_dsp_status)vvhip_mel_pitched_device(plan->dev, d_power, num_frames, row_pitch, d_out_log_mel, 0,
+                                                   stream);
+}

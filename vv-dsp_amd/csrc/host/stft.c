@@ -111,6 +111,15 @@ vv_dsp_status vv_dsp_stft_power_device(vv_dsp_stft* h, const vv_dsp_real* d_sign
                                                         out_ch_stride, 2, stream);
 }
 
+vv_dsp_status vv_dsp_stft_power_pitched_device(vv_dsp_stft* h, const vv_dsp_real* d_signal, size_t n, size_t nch,
+                                               size_t ch_stride, vv_dsp_real* d_out_power, size_t out_ch_stride,
+                                               size_t row_pitch, void* stream, size_t* out_frames) {
+    if (!h || !d_signal || !d_out_power) return VV_DSP_ERROR_NULL_POINTER;
+    if (out_frames) *out_frames = vvhip_stft_num_frames(n, h->nfft, h->hop);
+    return (vv_dsp_status)vvhip_stft_power_pitched_device(h->dev, d_signal, n, nch, ch_stride, d_out_power,
+                                                          out_ch_stride, row_pitch, stream);
+}
+
 __attribute__((visibility("hidden"))) vvhip_mel* vv_amd_mfcc_device_plan(const vv_dsp_mfcc_plan* plan);
 
 static vv_dsp_status stft_mel(vv_dsp_stft* h, const vv_dsp_mfcc_plan* plan, const vv_dsp_real* d_signal, size_t n,

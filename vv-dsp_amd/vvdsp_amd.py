@@ -57,6 +57,9 @@ def lib():
     L.vv_dsp_stft_spectrogram_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_spectrum_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_power_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_stft_power_pitched_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _sz, _vp, C.POINTER(_sz)]
+    L.vv_dsp_mfcc_process_pitched_device.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp]
+    L.vv_dsp_log_mel_pitched_device.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp]
     L.vv_dsp_stft_log_mel_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_mfcc_device.argtypes = [_vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, C.POINTER(_sz)]
     L.vv_dsp_stft_frames_range_device.argtypes = [_vp, _vp, _sz, _sz, _sz, _sz, _sz, _vp, _sz, C.c_int, _vp]
@@ -238,19 +241,27 @@ class Stft:
         assert nf.value == fr
         return out if sig.dim() == 2 else out[0]
 
-    def power(self, sig, out=None, stream=None):
-        """sig: (nch, n) or (n,) float32 -> power spectrogram (nch, frames, nfft//2 + 1)."""
+    def power(self, sig, out=None, stream=None, pitch=None):
+        """sig: (nch, n) or (n,) float32 -> power spectrogram (nch, frames, nfft//2 + 1).
+        pitch: rows `pitch` >= nfft//2 + 1 floats apart (vv_dsp_stft_power_pitched_device):
+        returns the (nch, frames, pitch) buffer, bins 0..nfft//2 of each row written."""
         sig2 = sig if sig.dim() == 2 else sig.unsqueeze(0)
         nch, n = sig2.shape
         fr, nh = self.frames(n), self.nfft // 2 + 1
         if sig2.dtype != torch.float32 or sig2.stride(1) != 1:
             raise VvError("stft signal: float32 rows with unit sample stride")
+        w = nh if pitch is None else int(pitch)
         if out is None:
-            out = torch.empty((nch, fr, nh), dtype=torch.float32, device=sig.device)
-        _expect(out, torch.float32, nch * fr * nh, "stft power output")
+            out = torch.empty((nch, fr, w), dtype=torch.float32, device=sig.device)
+        _expect(out, torch.float32, nch * fr * w, "stft power output")
         nf = _sz(0)
-        _check(lib().vv_dsp_stft_power_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * nh,
-                                               _stream(stream), C.byref(nf)), "stft_power_device")
+        if pitch is None:
+            _check(lib().vv_dsp_stft_power_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out), fr * nh,
+                                                   _stream(stream), C.byref(nf)), "stft_power_device")
+        else:
+            _check(lib().vv_dsp_stft_power_pitched_device(self.h, _ptr(sig2), n, nch, sig2.stride(0), _ptr(out),
+                                                           fr * w, w, _stream(stream), C.byref(nf)),
+                   "stft_power_pitched_device")
         assert nf.value == fr
         return out if sig.dim() == 2 else out[0]
 
@@ -311,19 +322,30 @@ class Mfcc:
         _check(lib().vv_dsp_mfcc_init(n_fft, n_mels, n_coeffs, sample_rate, fmin, fmax, 0, 2, lifter, eps,
                                       C.byref(self.h)), "mfcc_init")
 
-    def _run(self, power, width, f, what, stream):
+    def _run(self, power, width, f, fp, what, stream, pitched):
         nb = self.n_fft // 2 + 1
+        if pitched:   # rows power.shape[-1] >= nb floats apart, bins 0..nb-1 used
+            w = power.shape[-1]
+            if w < nb:
+                raise VvError(f"pitched power rows: pitch {w} below {nb} bins")
+            p2 = power.reshape(-1, w)
+            out = torch.empty((p2.shape[0], width), dtype=torch.float32, device=power.device)
+            _check(fp(self.h, _ptr(p2), p2.shape[0], w, _ptr(out), _stream(stream)), what)
+            return out.reshape(*power.shape[:-1], width)
         assert power.shape[-1] == nb, f"power rows must have {nb} bins"
         p2 = power.reshape(-1, nb)
         out = torch.empty((p2.shape[0], width), dtype=torch.float32, device=power.device)
         _check(f(self.h, _ptr(p2), p2.shape[0], _ptr(out), _stream(stream)), what)
         return out.reshape(*power.shape[:-1], width)
 
-    def __call__(self, power, stream=None):
-        return self._run(power, self.n_coeffs, lib().vv_dsp_mfcc_process_device, "mfcc_process_device", stream)
+    def __call__(self, power, stream=None, pitched=False):
+        """pitched: power's last dimension is the row pitch (vv_dsp_mfcc_process_pitched_device)"""
+        return self._run(power, self.n_coeffs, lib().vv_dsp_mfcc_process_device,
+                         lib().vv_dsp_mfcc_process_pitched_device, "mfcc_process_device", stream, pitched)
 
-    def log_mel(self, power, stream=None):
-        return self._run(power, self.n_mels, lib().vv_dsp_log_mel_device, "log_mel_device", stream)
+    def log_mel(self, power, stream=None, pitched=False):
+        return self._run(power, self.n_mels, lib().vv_dsp_log_mel_device, lib().vv_dsp_log_mel_pitched_device,
+                         "log_mel_device", stream, pitched)
 
     def from_signal(self, stft, sig, log_mel=False, out=None, stream=None):
         """Signal (nch, n) or (n,) float32 -> MFCC (nch, frames, n_coeffs), or log-mel
