@@ -156,6 +156,7 @@ CASES = {
     "stftpow": lambda L, s: case_stft_rows(L, s, "pow", 32, 600),
     "stftpow544": lambda L, s: case_stft_rows(L, s, "pow544", 32, 600),
     "logmel": lambda L, s: case_mel(L, s, False),
+    "logmel8": lambda L, s: case_mel(L, s, False, nch=8),
     "mfcc": lambda L, s: case_mel(L, s, True),
     "c2c1024": case_c2c,
 }

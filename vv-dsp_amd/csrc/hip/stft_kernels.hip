@@ -256,6 +256,10 @@ __device__ __forceinline__ void direct_rows(const float2* v, int t, char* rowa, 
 // C <= 64); lanes without a row element write to the sink.
 constexpr int MEL_MAX_ROUNDS = 4;   // chunks <= 256
 constexpr int MEL_LM_OFF = 1028;    // MODE 4: log-mel rows in P past the two power rows (16 B aligned)
+template <int MODE, bool COUNTED>
+__device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, bool has_b, float* sink,
+                                         const float* sW, const int* sCh, const int* sCb, const float* sD,
+                                         const float* sL, const MelArgs& mel);
 template <int N, int MODE>
 __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, float* fb, bool has_b, float* sink,
                                          float* P, const float* sW, const int* sCh, const int* sCb,
@@ -314,6 +318,24 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
     });
     if (t == 0) put(N / 2, ea[0][R / 2], eb[0][R / 2]);
     xsync<T>();
+    mel_tail<MODE, true>(t, P, fa, fb, has_b, sink, sW, sCh, sCb, sD, sL, mel);
+}
+
+// The mel stage of one frame pair (MODE 3 log-mel, MODE 4 MFCC) over the 64
+// lanes of a wave, from the pair's power rows in LDS interleaved bin by bin,
+// P[2k] = |Xa[k]|^2, P[2k + 1] = |Xb[k]|^2 (k <= N/2): k_mel_grp's steps with
+// FR = 2 frames -- chunk partials (FMA in bin order; lane c % 64 holds chunk c
+// in round c / 64), per-filter sums of the partials in chunk order (fetched
+// across lanes by ds_bpermute), logf(e + eps), and for MODE 4 the DCT-II and
+// lifter over the log-mel rows (kept at P + MEL_LM_OFF) -- the same operations
+// in the same order, so the rows equal the power rows followed by
+// launch_mel_grp bit for bit.  Stores: MODE 3 rows a, b x filters t, t + 64
+// (M <= 128), MODE 4 (frame, coefficient) pairs t, t + 64 (C <= 64).
+template <int MODE, bool COUNTED>
+__device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, bool has_b, float* sink,
+                                         const float* sW, const int* sCh, const int* sCb, const float* sD,
+                                         const float* sL, const MelArgs& mel) {
+    constexpr int T = 64;
     const int nc = mel.nc, M = mel.M, C = mel.C;
     float pa[MEL_MAX_ROUNDS], pb[MEL_MAX_ROUNDS];
 #pragma unroll
@@ -364,12 +386,18 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
         la[u] = on ? logf(e0 + mel.eps) : 0.0f;
         lb[u] = on ? logf(e1 + mel.eps) : 0.0f;
     }
-    float* const snk = sink + t;
+    float* const snk = COUNTED ? sink + t : nullptr;
+    // COUNTED: every lane issues each store (the sink when it has no element) so
+    // k_stft_pair's hand-counted vmcnt stays exact; otherwise predicated stores
+    auto put_out = [&](bool on, float* dst, float v) {
+        if constexpr (COUNTED) st4_counted(on ? dst : snk, v);
+        else if (on) *dst = v;
+    };
     if constexpr (MODE == 3) {
-        st4_counted(t < M ? fa + t : snk, la[0]);
-        st4_counted(t + T < M ? fa + t + T : snk, la[1]);
-        st4_counted(has_b && t < M ? fb + t : snk, lb[0]);
-        st4_counted(has_b && t + T < M ? fb + t + T : snk, lb[1]);
+        put_out(t < M, fa + t, la[0]);
+        put_out(t + T < M, fa + t + T, la[1]);
+        put_out(has_b && t < M, fb + t, lb[0]);
+        put_out(has_b && t + T < M, fb + t + T, lb[1]);
     } else {
         float* const lm = P + MEL_LM_OFF;   // [2][M], M <= (ri_floats - MEL_LM_OFF) / 2
 #pragma unroll
@@ -385,7 +413,7 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
         for (int u = 0; u < 2; ++u) {
             const int idx = t + T * u;
             float res = 0.0f;
-            float* dst = snk;
+            float* dst = snk;   // COUNTED: the sink; otherwise nullptr (no store)
             if (idx < 2 * C) {
                 const int f = idx >= C ? 1 : 0, i = idx - f * C;
                 const float* l = lm + f * M;
@@ -413,7 +441,8 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
                 if (f == 0) dst = fa + i;
                 else if (has_b) dst = fb + i;
             }
-            st4_counted(dst, res);
+            if constexpr (COUNTED) st4_counted(dst, res);
+            else if (dst) *dst = res;
         }
     }
 }
@@ -980,17 +1009,39 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
 // rule, in the same loop.  Persistent grid, static XCD walk over frame-pair
 // couples.
 // ------------------------------------------------------------------------
+// MODE 3 / 4 (log-mel / MFCC rows, launch_stft_mel): the power rows of each
+// half's pair go to that half's (now idle) transpose buffer, interleaved bin by
+// bin, and the wave runs mel_tail over its two pairs in turn -- the rows equal
+// MODE 2's power rows followed by launch_mel_grp, bit for bit.  The plan's
+// tables ride in dynamic LDS, so these modes take 8 transform slots per
+// workgroup (512 threads, one workgroup and two waves per SIMD per CU) instead of
+// two workgroups of 4: the same occupancy with one copy of the tables.
 constexpr int R33_BUF = 33 * R32_ROW;   // 33 rows: the mirror read of lane 0 touches row 32
 template <int MODE>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(MODE >= 3 ? 512 : 256, MODE >= 3 ? 1 : 2)
 k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, long long frames, const float* win,
-           float* out, long long out_ch_stride, long long row_pitch, const float2* tw1024) {
-    static_assert(MODE == 0 || MODE == 2, "magnitude or power rows");
-    constexpr int N = 1024, HOP = 256, F = 4, RW = MODE == 2 ? N / 2 + 1 : N, SPAN = N + HOP;
-    const long long RP = MODE == 2 ? row_pitch : RW;   // floats from one row's start to the next
+           float* out, long long out_ch_stride, long long row_pitch, const float2* tw1024, MelArgs mel) {
+    static_assert(MODE == 0 || MODE >= 2, "magnitude, power, log-mel or MFCC rows");
+    constexpr bool MEL = MODE >= 3;
+    constexpr int N = 1024, HOP = 256, F = MEL ? 8 : 4, WG = 64 * F, RW = MODE == 0 ? N : N / 2 + 1, SPAN = N + HOP;
+    // floats from one output row's start to the next
+    const long long RP = MODE == 2 ? row_pitch : MODE == 3 ? (long long)mel.M : MODE == 4 ? (long long)mel.C : RW;
     __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R33_BUF];
     __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r)
-    for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
+    for (int i = threadIdx.x; i < 32 * 32; i += WG) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
+    // MEL: the plan's tables in dynamic LDS: W [nnz], chunks [3 nc], cbeg [M + 1], then (MODE 4) D [C M], lift [C]
+    extern __shared__ __attribute__((aligned(16))) float mel_lds[];
+    const int mel_dpos = MEL ? (mel.nnz + 3 * mel.nc + mel.M + 1 + 3) & ~3 : 0;
+    if constexpr (MEL) {
+        int* const mi = reinterpret_cast<int*>(mel_lds);
+        for (int i = threadIdx.x; i < mel.nnz; i += WG) mel_lds[i] = mel.W[i];
+        for (int i = threadIdx.x; i < 3 * mel.nc; i += WG) mi[mel.nnz + i] = mel.chunks[i];
+        for (int i = threadIdx.x; i <= mel.M; i += WG) mi[mel.nnz + 3 * mel.nc + i] = mel.cbeg[i];
+        if constexpr (MODE == 4) {
+            for (int i = threadIdx.x; i < mel.C * mel.M; i += WG) mel_lds[mel_dpos + i] = mel.D[i];
+            for (int i = threadIdx.x; i < mel.C; i += WG) mel_lds[mel_dpos + mel.C * mel.M + i] = mel.lift[i];
+        }
+    }
     const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
     const int mr = 2 * (m & 15) + (m >> 4);   // this lane's input residue
     float2* buf = xch + (2 * slot + half) * R33_BUF;
@@ -1196,12 +1247,44 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
                 for (int j = 0; j < 8; ++j) pb[RP + 64 * j] = B[2 * j + 1];
             }
         }
+        if constexpr (MEL) {
+            // this half's pair: power of bins m + 32 k2 (k2 < 16) and bin 512 (lane
+            // 0) into its buffer as P[2k] = |Xa[k]|^2, P[2k + 1] = |Xb[k]|^2
+            float* P = reinterpret_cast<float*>(buf);
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) {
+                float2 pa, pb;
+                pair_post<2>(v[k2], (k2 == 0 && m == 0) ? v[0] : zm[15 - k2], &pa, &pb);
+                *reinterpret_cast<vf2_t*>(P + 2 * (m + 32 * k2)) = vf2_t{pa.x, pb.x};
+            }
+            float2 na, nb;   // bin 512: Z[512] is its own mirror (lane 0, register 16)
+            pair_post<2>(v[16], v[16], &na, &nb);
+            if (m == 0) *reinterpret_cast<vf2_t*>(P + 2 * (N / 2)) = vf2_t{na.x, nb.x};
+            xsync<64>();
+            const int* mi = reinterpret_cast<const int*>(mel_lds);
+            for (int h = 0; h < 2; ++h) {   // the two pairs in turn, each over the whole wave
+                if (h == 1 && !rw.two) break;
+                float* Ph = reinterpret_cast<float*>(xch + (2 * slot + h) * R33_BUF);
+                float* fa_row = out + (h ? rw.ob : rw.oa);
+                mel_tail<MODE, false>(lane, Ph, fa_row, fa_row + RP, h ? rw.hb : rw.ha, nullptr, mel_lds,
+                                      mi + mel.nnz, mi + mel.nnz + 3 * mel.nc, mel_lds + mel_dpos,
+                                      mel_lds + mel_dpos + mel.C * mel.M, mel);
+            }
+            xsync<64>();   // the next couple's transpose writes stay behind the tails' reads
+        }
         c = cn;
         q = qn;
         valid = validn;
         edge = edgen;
         rw = rwn;
     }
+}
+
+// The 32 x 32 kernels' shape (k_stft_r32): hop 256, 8 B aligned channel starts.
+// Power rows and the fused log-mel / MFCC rows share this rule, so the fused
+// rows always come from the same FFT as the power rows they must equal.
+static bool stft_r32_ok(long long hop, const float* sig, long long nch, long long ch_stride) {
+    return hop == 256 && ((uintptr_t)sig & 7) == 0 && (nch == 1 || (ch_stride & 1) == 0);
 }
 
 template <int N, int MODE>
@@ -1294,9 +1377,9 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // 2.760 chunked, profiles/r03_kbench_dyn_modes.jsonl).  Knob STFT_DYN =
         // 1 forces it for every row kind (A/B).
         // power rows, nfft 1024 / hop 256, 8 B aligned channels: the 32 x 32 split
-        // (k_stft_r32) when knob POW_R32 = 1 (A/B)
+        // (k_stft_r32; knob POW_R32 = 0: the ring walk below, A/B)
         if constexpr (N == 1024 && MODE == 2) {
-            if (hop == 256 && knob(KNOB_POW_R32, 0) == 1 && ((uintptr_t)sig & 7) == 0 && (nch == 1 || (ch_stride & 1) == 0)) {
+            if (stft_r32_ok(hop, sig, nch, ch_stride) && knob(KNOB_POW_R32, 1) != 0) {
                 static std::atomic<int> capr;
                 const int cap = cached_grid(capr, (const void*)k_stft_r32<2>, 256, 0, 1LL << 40);
                 const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
@@ -1304,7 +1387,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 if (grid < 1) return hipSuccess;
                 stat_inc(STAT_POW_R32);
                 hipLaunchKernelGGL((k_stft_r32<2>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, win,
-                                   (float*)out, out_ch_stride, row_pitch, tN);
+                                   (float*)out, out_ch_stride, row_pitch, tN, MelArgs{});
                 return hipGetLastError();
             }
         }
@@ -1318,7 +1401,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                 if (grid < 1) return hipSuccess;
                 stat_inc(STAT_MAG_R32);
                 hipLaunchKernelGGL((k_stft_r32<0>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, win,
-                                   (float*)out, out_ch_stride, row_pitch, tN);
+                                   (float*)out, out_ch_stride, row_pitch, tN, MelArgs{});
                 return hipGetLastError();
             }
         }
@@ -1396,6 +1479,22 @@ static hipError_t run_stft_mel(const float* sig, long long n, long long nch, lon
     // the plan's tables in dynamic LDS (the kernel's layout); occupancy per call
     const long long dpos = (mel.nnz + 3LL * mel.nc + mel.M + 1 + 3) & ~3LL;
     const size_t dyn = sizeof(float) * (size_t)(dpos + (MODE == 4 ? (long long)mel.C * mel.M + mel.C : 0));
+    // the 32 x 32 split where the power rows take it too (stft_r32_ok), so the
+    // fused rows stay bit-identical to the power rows + launch_mel_grp
+    if (stft_r32_ok(hop, sig, nch, ch_stride) && knob(KNOB_MEL_R32, 1) != 0) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_stft_r32<MODE>, 512, dyn) ==
+                hipSuccess &&
+            per_cu >= 1) {
+            const int cap = persistent_grid((const void*)k_stft_r32<MODE>, 512, dyn, 1LL << 40);
+            const long long couples = (pairs + 1) / 2, need = (couples + 7) / 8;
+            const int grid = (int)(need < cap ? need : cap);
+            stat_inc(STAT_MEL_R32);
+            hipLaunchKernelGGL((k_stft_r32<MODE>), dim3(grid), dim3(512), dyn, s, sig, n, nch, ch_stride, frames, win,
+                               out, out_ch_stride, 0LL, tN, mel);
+            return hipGetLastError();
+        }
+    }
     const int cap = persistent_grid((const void*)k_stft_pair<N, MODE, 0>, WG, dyn, 1LL << 40);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_stft_pair<N, MODE, 0>, WG, dyn) !=

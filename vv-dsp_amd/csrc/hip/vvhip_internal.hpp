@@ -17,12 +17,12 @@ enum Knob : int {
     KNOB_FS_VAR, KNOB_FS_CHUNK_MB, KNOB_FS_OLD, KNOB_BLUE_UNFUSED, KNOB_C2C_MAX, KNOB_STFT_SQ, KNOB_MIX_VAR,
     KNOB_MIX_CHUNK_MB, KNOB_MIX_R2C_FULL, KNOB_FIR_OLD, KNOB_FIR_DYN, KNOB_FIR_DIRECT_LDS, KNOB_FIR_BLOCK,
     KNOB_HOST_CHUNK_MB, KNOB_NO_MIXED, KNOB_REAL_PROMOTE, KNOB_ISTFT_OLD, KNOB_MEL_FUSED, KNOB_CZT_UNFUSED,
-    KNOB_CEPS_UNFUSED, KNOB_FIR_R32, KNOB_DIST_SLAB_KB, KNOB_POW_R32, KNOB_MAG_R32,
+    KNOB_CEPS_UNFUSED, KNOB_FIR_R32, KNOB_DIST_SLAB_KB, KNOB_POW_R32, KNOB_MAG_R32, KNOB_MEL_R32,
     KNOB_COUNT
 };
 long long knob(Knob k, long long dflt);
 // launches of the paths the tests must see taken (vvhip_debug_get("STAT_..."))
-enum Stat : int { STAT_STFT_DYN, STAT_FIR_DYN, STAT_FIR_STATIC, STAT_MEL_FUSED, STAT_MEL_SPLIT, STAT_FIR_R32, STAT_POW_R32, STAT_MAG_R32, STAT_COUNT };
+enum Stat : int { STAT_STFT_DYN, STAT_FIR_DYN, STAT_FIR_STATIC, STAT_MEL_FUSED, STAT_MEL_SPLIT, STAT_FIR_R32, STAT_POW_R32, STAT_MAG_R32, STAT_MEL_R32, STAT_COUNT };
 void stat_inc(Stat s);
 
 // Device-resident W_N^k = exp(-2*pi*i*k/N) table, k < N, f32 rounded from double.
