@@ -105,8 +105,8 @@ def fft_c2c_roofline(reps=50):
             "achieved_GBs": round(byts / (avg * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
             "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ffts_per_s": round(B / (avg * 1e-3), 1),
-            "kernel": "vvh::k_c2c<1024, true, 0> (one launch)",
-            **dict(zip(("traffic", "traffic_source"), kernel_traffic(["vvh::k_c2c<1024, true,"]))),
+            "kernel": "vvh::k_c2c<1024, true> (one launch)",
+            **dict(zip(("traffic", "traffic_source"), kernel_traffic(["vvh::k_c2c<1024, true>", "vvh::k_c2c<1024, true,"]))),
             "backward": {"ms_avg": round(bavg, 4), "ms_min": round(bbest, 4),
                          "frac": round(byts / (bavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
@@ -161,7 +161,7 @@ def fir_roofline(reps=50):
             "achieved_GBs": round(byts / (avg * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
             "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "samples_per_s": round(nch * n / (avg * 1e-3), 1),
-            "kernel": "vvh::k_fir_r32<true, 0> (1024-point blocks as 32 x 32 on half-waves: one LDS transpose per "
+            "kernel": "vvh::k_fir_r32<true> (1024-point blocks as 32 x 32 on half-waves: one LDS transpose per "
                       "FFT, radix 4 x 8 DFT_32; samples moved as 8 B per lane re-laid by v_permlane16_swap; two blocks "
                       "per complex FFT, two pairs per wave, every pair of every channel in one persistent launch, the "
                       "edge pairs bounds-checked in the same loop), one step",

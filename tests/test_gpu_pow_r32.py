@@ -1,6 +1,6 @@
 """k_stft_r32 (stft_kernels.hip): power rows of nfft 1024 / hop 256 with the
-transform split 32 x 32 on half-waves (the default for hop 256 since round 5;
-knob POW_R32 = 0 selects the 16 x 16 x 4 ring kernel), against NumPy f64 per
+transform split 32 x 32 on half-waves (knob POW_R32 = 1; the default is the
+16 x 16 x 4 ring kernel), against NumPy f64 per
 bin at the power-row tolerance of test_gpu_parity.test_stft_power_rows, against
 the default kernel, and with the path counter proving the kernel ran.  Shapes:
 odd channel counts (a frame-pair couple spanning two channels, a missing last
@@ -37,7 +37,7 @@ def test_pow_r32_vs_f64(vdev, orc, knob, nch, n, off):
     st.power(sig, out=out)
     torch.cuda.synchronize()
     assert vv.debug_get("STAT_POW_R32") == 1, "k_stft_r32 did not run"
-    knob("POW_R32", 0)   # the 16 x 16 x 4 ring kernel (the default before round 5)
+    knob("POW_R32", 0)   # the 16 x 16 x 4 ring kernel (the default)
     ref16 = st.power(sig).cpu().numpy()
     b = buf.cpu().numpy()
     assert np.all(b[:off] == -7.0) and np.all(b[off + nch * fr * nh:] == -7.0), "stores outside the rows"

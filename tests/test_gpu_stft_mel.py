@@ -52,12 +52,11 @@ def test_stft_mel_equals_two_step(vdev, nfft, hop, sr, n_mels, n_coeffs, nch, n,
     finally:
         vv.debug_clear("MEL_FUSED")
     assert torch.equal(two, ref)
-    # the 32 x 32 FFT's fused rows (hop 256) against the 16 x 16 x 4 path's: both
-    # pipelines, power rows + mel and fused, switched together (knobs POW_R32 = 0
-    # and MEL_R32 = 0), agree with each other bit for bit, and with the default
-    # within the FFTs' rounding
+    # the 32 x 32 FFT's pipelines (hop 256; knobs POW_R32 = 1 and MEL_R32 = 1):
+    # power rows + mel and the fused rows agree with each other bit for bit, and
+    # with the default 16 x 16 x 4 path within the FFTs' rounding
     if nfft == 1024 and hop == 256:
-        with vv.knobs(POW_R32=0, MEL_R32=0):
+        with vv.knobs(POW_R32=1, MEL_R32=1):
             ref16 = _two_step(vdev, st, mf, sig, log_mel)
             got16 = mf.from_signal(st, sig, log_mel=log_mel)
         torch.cuda.synchronize()
@@ -67,18 +66,20 @@ def test_stft_mel_equals_two_step(vdev, nfft, hop, sr, n_mels, n_coeffs, nch, n,
 
 @pytest.mark.parametrize("log_mel", [True, False])
 def test_stft_mel_r32_path_taken(vdev, log_mel):
-    """hop 256 with 8 B aligned channels: the fused rows come from k_stft_r32's
-    MEL modes (STAT_MEL_R32), bit-identical to power rows + mel"""
+    """knobs POW_R32 = MEL_R32 = 1, hop 256, 8 B aligned channels: the fused rows
+    come from k_stft_r32's MEL modes (STAT_MEL_R32), bit-identical to its power
+    rows + mel"""
     import torch
     g = torch.Generator(device="cuda").manual_seed(3)
     sig = torch.rand(5, 48000 * 7 + 512, device="cuda", generator=g) * 2 - 1
     st = vdev.Stft(1024, 256)
     mf = vdev.Mfcc(1024, 40, 13, 48000.0, 20.0, 20000.0, lifter=22.0)
-    vv.debug_clear("STAT_MEL_R32")
-    got = mf.from_signal(st, sig, log_mel=log_mel)
-    torch.cuda.synchronize()
-    assert vv.debug_get("STAT_MEL_R32") == 1
-    assert torch.equal(got, _two_step(vdev, st, mf, sig, log_mel))
+    with vv.knobs(POW_R32=1, MEL_R32=1):
+        vv.debug_clear("STAT_MEL_R32")
+        got = mf.from_signal(st, sig, log_mel=log_mel)
+        torch.cuda.synchronize()
+        assert vv.debug_get("STAT_MEL_R32") == 1
+        assert torch.equal(got, _two_step(vdev, st, mf, sig, log_mel))
 
 
 @pytest.mark.parametrize("log_mel", [True, False])

@@ -1377,9 +1377,11 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // 2.760 chunked, profiles/r03_kbench_dyn_modes.jsonl).  Knob STFT_DYN =
         // 1 forces it for every row kind (A/B).
         // power rows, nfft 1024 / hop 256, 8 B aligned channels: the 32 x 32 split
-        // (k_stft_r32; knob POW_R32 = 0: the ring walk below, A/B)
+        // (k_stft_r32) on knob POW_R32 = 1 (A/B; round 5, same buffers: 3.02 ms
+        // against the ring walk's 2.70 for 32 ch x 10 min -- its 128 B half-wave
+        // stores leave in a burst at two waves per SIMD)
         if constexpr (N == 1024 && MODE == 2) {
-            if (stft_r32_ok(hop, sig, nch, ch_stride) && knob(KNOB_POW_R32, 1) != 0) {
+            if (stft_r32_ok(hop, sig, nch, ch_stride) && knob(KNOB_POW_R32, 0) == 1) {
                 static std::atomic<int> capr;
                 const int cap = cached_grid(capr, (const void*)k_stft_r32<2>, 256, 0, 1LL << 40);
                 const long long couples = (nch * ppc + 1) / 2, need = (couples + 3) / 4;
@@ -1479,9 +1481,11 @@ static hipError_t run_stft_mel(const float* sig, long long n, long long nch, lon
     // the plan's tables in dynamic LDS (the kernel's layout); occupancy per call
     const long long dpos = (mel.nnz + 3LL * mel.nc + mel.M + 1 + 3) & ~3LL;
     const size_t dyn = sizeof(float) * (size_t)(dpos + (MODE == 4 ? (long long)mel.C * mel.M + mel.C : 0));
-    // the 32 x 32 split where the power rows take it too (stft_r32_ok), so the
-    // fused rows stay bit-identical to the power rows + launch_mel_grp
-    if (stft_r32_ok(hop, sig, nch, ch_stride) && knob(KNOB_MEL_R32, 1) != 0) {
+    // knob MEL_R32 = 1 (with POW_R32 = 1, so the fused rows stay bit-identical to
+    // the power rows + launch_mel_grp): the 32 x 32 split (A/B; round 5, same
+    // buffers: log-mel 3.38 / MFCC 4.02 ms against 3.21 / 3.52 for 32 ch x 10 min
+    // -- two serial mel tails per wave at two waves per SIMD)
+    if (stft_r32_ok(hop, sig, nch, ch_stride) && knob(KNOB_MEL_R32, 0) == 1 && knob(KNOB_POW_R32, 0) == 1) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_stft_r32<MODE>, 512, dyn) ==
                 hipSuccess &&
