@@ -615,9 +615,13 @@ def main_dist(args, mode, world):
                 root_slot = s
             else:
                 out = torch.empty(cnt, nfr, NFFT, device=dev)
-        slots.append({"rank": r, "dev": dev, "lo": lo, "cnt": cnt, "sig": sig, "out": out,
-                      "stream": torch.cuda.current_stream(dev)})
+            # an explicit stream per device for the launches, the events and the RCCL
+            # send / receive of the gather (RCCL gets a real stream of the comm's device)
+            stream = torch.cuda.Stream(device=dev)
+        slots.append({"rank": r, "dev": dev, "lo": lo, "cnt": cnt, "sig": sig, "out": out, "stream": stream})
     st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
+    for x in slots:   # inputs generated on each device's default stream: complete before the launch streams read them
+        torch.cuda.synchronize(x["dev"])
 
     def step():
         d.stft(st, [x["sig"] for x in slots], SAMPLES, total_ch, SAMPLES, [x["out"] for x in slots],

@@ -184,3 +184,54 @@ def test_dynamic_walks_under_graph_capture(job, vdev, orc):
         assert torch.equal(y, yref)
         assert torch.equal(eager, ref)
     del g
+
+
+def test_capture_blocks_come_back(job):
+    """every capture took a counter block for good, so after 256
+    captures the dynamic walks silently fell back to the static ones.  A
+    capture's block is now tied to its graph (hipGraphRetainUserObject) and
+    returns to a free list when the graph is destroyed: 300 capture/destroy
+    cycles later a capture still takes the dynamic walk, and its replay gives
+    the eager rows."""
+    import gc
+    import torch
+    sig, st, ref = job
+    out = torch.empty_like(ref)
+    torch.cuda.synchronize()
+    for _ in range(300):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            st.spectrogram(sig, out=out)
+        del g
+        gc.collect()
+        torch.cuda.synchronize()
+    d0 = vv.debug_get("STAT_STFT_DYN")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        st.spectrogram(sig, out=out)
+    assert vv.debug_get("STAT_STFT_DYN") - d0 == 1, "the capture fell back to the static walk"
+    out.fill_(-1.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    del g
+
+
+def test_many_streams_each_get_a_block(job):
+    """more streams than one chunk of counter blocks (256): each still takes the
+    dynamic walk with a block of its own (the pool grows by chunks)"""
+    import torch
+    sig, st, ref = job
+    one = sig[:2]   # 78,750 pairs: enough for the dynamic walk
+    ref1 = ref[:2]
+    out = torch.empty_like(ref1)
+    torch.cuda.synchronize()
+    d0 = vv.debug_get("STAT_STFT_DYN")
+    streams = [torch.cuda.Stream() for _ in range(300)]
+    for s in streams:
+        with torch.cuda.stream(s):
+            st.spectrogram(one, out=out, stream=s)
+        s.synchronize()
+    assert vv.debug_get("STAT_STFT_DYN") - d0 == 300
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref1)

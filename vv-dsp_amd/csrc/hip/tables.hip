@@ -105,45 +105,61 @@ const float2* twiddle_split(long long n, int* lo_bits) {
 }
 
 // Work counters of the dynamically scheduled launches (k_stft_pair VAR 4/5,
-// k_fir_bulk_reg's band walk): blocks of STFT_CTR_WORDS words from a per-device
-// pool allocated and zeroed ONCE (hipMalloc + synchronous memset, on the first
-// dynamic launch of the device outside a graph capture).
+// k_fir_bulk_reg's band walk): blocks of STFT_CTR_WORDS words from per-device
+// chunks of CTR_POOL_BLOCKS blocks, each allocated and zeroed ONCE (hipMalloc +
+// synchronous memset, outside any graph capture).
 //  * eager launches: one block per (device, stream), handed out on the stream's
 //    first dynamic launch and kept; the kernel's last wave of each counter
 //    stream resets it, so launches ordered on one stream find it zero, and
-//    launches on different streams never share one;
+//    launches on different streams never share one.  A destroyed stream's
+//    handle that comes back for a new stream finds its block reset.  When a
+//    chunk is used up the next eager request allocates another, so any number
+//    of streams gets its own block.
 //  * launches recorded into a HIP graph (hipStreamIsCapturing): a block of the
-//    capture's own that no other launch ever uses, zeroed by a captured
-//    one-block kernel ahead of the launch, so every replay starts from zero and a
-//    replay never shares counters with eager work on the capture stream.
-// Nothing here blocks inside a capture.  When the pool is exhausted (or a
-// capture comes before the pool exists) it returns nullptr and the launcher
-// takes its static walk (bit-identical results).
+//    capture's own that no other launch uses, zeroed by a captured one-block
+//    kernel ahead of the launch, so every replay starts from zero and a replay
+//    never shares counters with eager work on the capture stream.  The block is
+//    tied to the captured graph by a user object (hipGraphRetainUserObject):
+//    when the last graph (and executable graph) holding it is destroyed the
+//    block returns to a free list for later captures.  Executable graphs
+//    instantiated from ONE captured graph share its blocks: replays of them must
+//    not run concurrently (one replay at a time per captured graph, as with any
+//    graph whose nodes read and write the same memory).
+// Nothing here blocks inside a capture.  When no block is available (a capture
+// with every block taken and none freed, or no chunk yet on the device) it
+// returns nullptr and the launcher takes its static walk (bit-identical results).
 namespace {
 // the captured zeroing of a capture's counter block (a kernel node)
 __global__ void k_zero_words(unsigned* p, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0u;
 }
-constexpr int CTR_POOL_BLOCKS = 256;   // 256 x 4 KB per device
+constexpr int CTR_POOL_BLOCKS = 256;   // 256 x 4 KB per chunk
 struct CtrPool {
-    unsigned* base = nullptr;
-    int used = 0;
+    std::vector<unsigned*> chunks;
+    int used = 0;                           // blocks handed out of the newest chunk
     bool failed = false;
     std::map<hipStream_t, unsigned*> by_stream;
+    std::vector<unsigned*> free_capture;    // capture blocks whose graphs are gone
 };
 std::map<int, CtrPool> g_ctr;
-}  // namespace
-
-unsigned* stream_counters(hipStream_t s) {
+struct CaptureBlock {   // a user object's payload: the block and its pool's device
+    int dev;
+    unsigned* block;
+};
+// hipUserObject destructor (runs on a runtime thread once no graph holds it)
+void release_capture_block(void* p) {
+    CaptureBlock* cb = static_cast<CaptureBlock*>(p);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_ctr[cb->dev].free_capture.push_back(cb->block);
+    }
+    delete cb;
+}
+// a fresh block from the chunks; a new chunk only when `grow` (outside captures)
+unsigned* bump_block(CtrPool& p, bool grow) {
     constexpr size_t bytes = sizeof(unsigned) * STFT_CTR_WORDS;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
-    const bool capturing = cs != hipStreamCaptureStatusNone;
-    const int dev = current_device();
-    std::lock_guard<std::mutex> lk(g_mu);
-    CtrPool& p = g_ctr[dev];
-    if (!p.base) {
-        if (capturing || p.failed) return nullptr;
+    if (p.chunks.empty() || p.used >= CTR_POOL_BLOCKS) {
+        if (!grow || p.failed) return nullptr;
         void* d = nullptr;
         if (hipMalloc(&d, bytes * CTR_POOL_BLOCKS) != hipSuccess) {
             p.failed = true;
@@ -154,21 +170,58 @@ unsigned* stream_counters(hipStream_t s) {
             p.failed = true;
             return nullptr;
         }
-        p.base = (unsigned*)d;
+        p.chunks.push_back((unsigned*)d);
+        p.used = 0;
     }
+    return p.chunks.back() + (size_t)p.used++ * STFT_CTR_WORDS;
+}
+}  // namespace
+
+unsigned* stream_counters(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipGraph_t graph = nullptr;
+    if (hipStreamGetCaptureInfo_v2(s, &cs, nullptr, &graph, nullptr, nullptr) != hipSuccess)
+        cs = hipStreamCaptureStatusNone;
+    const bool capturing = cs == hipStreamCaptureStatusActive;
+    if (cs != hipStreamCaptureStatusNone && !capturing) return nullptr;   // an invalidated capture
+    const int dev = current_device();
     if (capturing) {
-        if (p.used >= CTR_POOL_BLOCKS) return nullptr;
-        unsigned* b = p.base + (size_t)p.used * STFT_CTR_WORDS;
+        if (!graph) return nullptr;
+        unsigned* b = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            CtrPool& p = g_ctr[dev];
+            if (!p.free_capture.empty()) {
+                b = p.free_capture.back();
+                p.free_capture.pop_back();
+            } else {
+                b = bump_block(p, false);
+            }
+        }
+        if (!b) return nullptr;
+        // tie the block to the captured graph (outside the lock: the destructor
+        // takes it): the block comes back when the last graph holding it goes
+        CaptureBlock* cb = new (std::nothrow) CaptureBlock{dev, b};
+        hipUserObject_t obj = nullptr;
+        if (!cb || hipUserObjectCreate(&obj, cb, release_capture_block, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+            if (cb) release_capture_block(cb);   // back to the free list
+            return nullptr;
+        }
+        if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+            (void)hipUserObjectRelease(obj, 1);   // the destructor files the block as free
+            return nullptr;
+        }
         (void)hipGetLastError();   // a stale error must not read as this launch's
         hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, b, (int)STFT_CTR_WORDS);
-        if (hipGetLastError() != hipSuccess) return nullptr;
-        ++p.used;
+        if (hipGetLastError() != hipSuccess) return nullptr;   // the graph still returns it later
         return b;
     }
+    std::lock_guard<std::mutex> lk(g_mu);
+    CtrPool& p = g_ctr[dev];
     auto it = p.by_stream.find(s);
     if (it != p.by_stream.end()) return it->second;
-    if (p.used >= CTR_POOL_BLOCKS) return nullptr;
-    unsigned* b = p.base + (size_t)p.used++ * STFT_CTR_WORDS;
+    unsigned* b = bump_block(p, true);
+    if (!b) return nullptr;
     p.by_stream[s] = b;
     return b;
 }
