@@ -355,33 +355,31 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
             pb[u] = ab.y;
         }
     }
-    const int nr = (nc + T - 1) / T;   // rounds holding chunks (wave-uniform)
+    // the chunk partials go to LDS over P (every lane has read its power bins
+    // above), pair c at P[2c], P[2c + 1]; then lane m adds its filter's chunks
+    // in chunk order -- independent ds_read_b64s instead of a chain of
+    // cross-lane permutes (2 per round per chunk), the same sums bit for bit
+    xsync<T>();
+#pragma unroll
+    for (int u = 0; u < MEL_MAX_ROUNDS; ++u) {
+        const int c = t + T * u;
+        if (c < nc) *reinterpret_cast<vf2_t*>(P + 2 * c) = vf2_t{pa[u], pb[u]};
+    }
+    xsync<T>();
+    const vf2_t* part = reinterpret_cast<const vf2_t*>(P);
     float la[2] = {0.0f, 0.0f}, lb[2] = {0.0f, 0.0f};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        if (T * u >= M) break;   // no filter in this round (M <= 64): skip its reduction and logf
+        if (T * u >= M) break;   // no filter in this round (M <= 64): skip its sums and logf
         const int m = t + T * u;
         const bool on = m < M;
         const int cb = on ? sCb[m] : 0, ce = on ? sCb[m + 1] : 0;
-        const int kmax = mel.kmax[u];   // the round's longest filter (in chunks, from the plan) sets the trip count
         float e0 = 0.0f, e1 = 0.0f;
-        for (int k = 0; k < kmax; ++k) {   // chunk cb + k of this lane's filter, in order
-            const int c = cb + k < ce ? cb + k : 0;
-            const int addr = (c & (T - 1)) << 2, rd = c / T;
-            float ga = 0.0f, gb = 0.0f;
-#pragma unroll
-            for (int r = 0; r < MEL_MAX_ROUNDS; ++r) {
-                if (r < nr) {   // every lane joins each permute (wave-uniform condition)
-                    const float xa = __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(pa[r])));
-                    const float xb = __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(pb[r])));
-                    ga = rd == r ? xa : ga;
-                    gb = rd == r ? xb : gb;
-                }
-            }
-            if (cb + k < ce) {
-                e0 += ga;
-                e1 += gb;
-            }
+#pragma unroll 4
+        for (int c = cb; c < ce; ++c) {   // this lane's filter's chunks, in order
+            const vf2_t q = part[c];
+            e0 += q.x;
+            e1 += q.y;
         }
         la[u] = on ? logf(e0 + mel.eps) : 0.0f;
         lb[u] = on ? logf(e1 + mel.eps) : 0.0f;
