@@ -1377,7 +1377,6 @@ struct vvhip_mel {
     int* chunks = nullptr;  // balanced chunk schedule of the filters (mel_chunk_schedule)
     int* cbeg = nullptr;    // first chunk of each filter, [n_mels + 1]
     int nc = 0;
-    int kmax[2] = {0, 0};   // most chunks of one filter per 64-filter round (the fused kernel's trip counts)
     float* D = nullptr;     // DCT-II table [n_coeffs][n_mels]
     float* lift = nullptr;  // lifter factors [n_coeffs]
     hipStream_t stream = nullptr;
@@ -1436,10 +1435,6 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
     std::vector<int> chunks, cbeg;
     mel_chunk_schedule(meta.data(), (int)n_mels, &chunks, &cbeg);
     m->nc = (int)(chunks.size() / 3);
-    for (size_t f = 0; f < n_mels && f < 128; ++f) {
-        const int k = cbeg[f + 1] - cbeg[f];
-        if (k > m->kmax[f / 64]) m->kmax[f / 64] = k;
-    }
     // DCT-II rows cos(pi (j + 1/2) i / M) (dct.c:21-30), and the lifter of mel.c:300-302
     std::vector<float> D(n_coeffs * n_mels), L(n_coeffs, 1.0f);
     for (size_t i = 0; i < n_coeffs; ++i)
@@ -1515,8 +1510,6 @@ int vvhip_stft_mel_device(vvhip_stft* h, vvhip_mel* m, const float* d_signal, si
         a.M = m->n_mels;
         a.C = m->n_coeffs;
         a.eps = m->eps;
-        a.kmax[0] = m->kmax[0];
-        a.kmax[1] = m->kmax[1];
         const hipError_t e = launch_stft_mel(kind, (long long)h->nfft, (long long)h->hop, d_signal, (long long)n,
                                              (long long)nch, (long long)ch_stride, (long long)frames, win, a, d_out,
                                              (long long)out_ch_stride, s);

@@ -144,7 +144,6 @@ struct MelArgs {
     const float* D = nullptr;      // DCT-II rows [C][M]
     const float* lift = nullptr;   // lifter factors [C]
     int nnz = 0, nc = 0, M = 0, C = 0;
-    int kmax[2] = {0, 0};          // most chunks of any filter m in [64 u, 64 u + 64), per round u
     float eps = 0.0f;
 };
 // Log-mel (kind 0) or MFCC (kind 1) rows [ch][frame][M or C] straight from the
