@@ -25,6 +25,8 @@ def _run(args):
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert line, (p.returncode, p.stdout[-500:], p.stderr[-500:])
     res = json.loads(line[-1])
+    res["_stderr"] = p.stderr[-800:]
+    res["_lines"] = line
     return p.returncode, res
 
 

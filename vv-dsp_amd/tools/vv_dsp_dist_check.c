@@ -134,7 +134,9 @@ int main(int argc, char** argv) {
             float* d_out = NULL;
             CHECK(hipSetDevice(dev_of[rs]));
             CHECK(hipMalloc((void**)&d_out, sizeof(float) * NCH * rows_ch));
-            CHECK(hipMemset(d_out, 0xff, sizeof(float) * NCH * rows_ch));
+            /* poison on the root's stream: the streams are non-blocking, so a memset on
+             * the null stream would not be ordered before the gather's copies */
+            CHECK(hipMemsetAsync(d_out, 0xff, sizeof(float) * NCH * rows_ch, (hipStream_t)streams[rs]));
             hipEvent_t e0, e1;
             CHECK(hipEventCreate(&e0));
             CHECK(hipEventCreate(&e1));
