@@ -145,8 +145,9 @@ def test_loopback_distinct_streams(job):
     for half in (False, True):
         rows = [torch.full((c, fr, 1024), -3.0, device="cuda") for (_, c) in sl]
         torch.cuda.synchronize()
-        d.stft(st, [sig[f] for f, _ in sl], N, NCH, N, rows, streams=streams)
         out = torch.full_like(ref, -1.0)
+        torch.cuda.synchronize()   # torch's side streams do not wait for the null stream's fills
+        d.stft(st, [sig[f] for f, _ in sl], N, NCH, N, rows, streams=streams)
         d.gather_rows(rows, NCH, fr, 1024, out, root=1, half=half, streams=streams)
         torch.cuda.synchronize()
         assert torch.equal(out, ref)
