@@ -51,8 +51,10 @@ CH_SHARD = 32                # config 5 per-GPU shard at 8 GPUs (extra leg at N 
 SAMPLES = 10 * 60 * FS        # 10 min per channel
 PUBLISHED_CPU_FPS = 24903.0   # BASELINE.md §1 STFT_size_1024 (CPU, 1 thread) -- informational only:
                               # BASELINE.json "published" is empty, so vs_baseline is null
-# the newest round's committed PMC summary of this command (profiles/rNN_bench_pmc.json)
-TRAFFIC_JSON = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_pmc.json"))) or
+# the newest round's committed PMC summary of this command (profiles/rNN_bench_pmc.json,
+# or that round's rNN_final_pmc.json of its final tree, which sorts after it)
+TRAFFIC_JSON = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_pmc.json")) +
+                       glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_final_pmc.json"))) or
                 [os.path.join(ROOT, "profiles", "r01_bench_pmc.json")])[-1]
 METRIC = "STFT frames/sec (1024-pt, hop 256) at 1/2/4/8 GPU; achieved HBM GB/s vs peak"
 TIMING_NOTE = ("ms_avg: HIP events around the timed launches back to back / launches (the launch stream); "

@@ -159,6 +159,7 @@ CASES = {
     "logmel8": lambda L, s: case_mel(L, s, False, nch=8),
     "mfcc": lambda L, s: case_mel(L, s, True),
     "c2c1024": case_c2c,
+    **{f"c2c{n}": (lambda L, s, n=n: case_c2c(L, s, n, (1 << 26) // n)) for n in (64, 256, 2048, 4096, 8192)},
 }
 
 

@@ -34,7 +34,7 @@ namespace vvh {
 // N = 1024 exchanges through the half-size real/imaginary buffer
 // (pass_exchange_ri): 26 KB of LDS per workgroup instead of 43 KB, so four
 // workgroups (16 waves) fit per CU and keep more transforms' loads in flight.
-template <int N, bool FWD>
+template <int N, bool FWD, bool ONE = false>
 __global__ void __launch_bounds__(Wg<N>::value, N == 1024 ? 4 : 1)
 k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
       const float2* gpass, const float2* gtab, float scale) {
@@ -53,6 +53,21 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
     const long long stride = (long long)gridDim.x * F;
     long long f = uni<G::T>((long long)blockIdx.x * F + slot);
     const long long fend = batch;
+    if constexpr (ONE) {   // one transform per slot: no loop, no prefetch registers
+        if (f >= fend) return;
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = ld_nt(in + f * in_dist + t + r * G::T);
+        fft_regs<N, FWD, false, RI, TwTab<N>, false, false, 1>(v, t, my, tw);
+        float2* dst = out + f * out_dist;
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            float2 o = v[q];
+            if (!FWD) o = cscale(o, scale);
+            st_nt(o, dst + out_pos<N>(t, q));
+        }
+        return;
+    }
     float2 nx[G::P];
     if (f < fend) {
 #pragma unroll
@@ -87,9 +102,29 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     static std::atomic<int> capc;
     const int grid_cap = cached_grid(capc, (const void*)k_c2c<N, FWD>, WG, 0, 1LL << 40);
-    long long need = (batch + F - 1) / F;
-    const int grid = (int)(need < grid_cap ? need : grid_cap);
+    // 256 <= N <= 4096: one transform per wave slot, a grid of batch / F workgroups
+    // (not persistent), so the dispatcher hands out the next workgroup as one ends:
+    // config 2 (65536 x 1024) 0.1847 -> 0.1766 ms on the same buffers, 256 / 2048
+    // points -3.6 / -4.5 %, 4096 -0.5 %; 64 points +10 % and 8192 +32 % keep the
+    // persistent grid (profiles/r05_ab2_c2c_grid.jsonl).  Knob C2C_TPW = t > 0:
+    // t transforms per wave slot; 0: the persistent grid (A/B)
+    const long long tpw = knob(KNOB_C2C_TPW, N >= 256 && N <= 4096 ? 1 : -1);
+    long long need = (batch + F - 1) / F, cap = grid_cap;
+    if (tpw > 0) {
+        need = (batch + F * tpw - 1) / (F * tpw);
+        cap = 1LL << 30;
+    }
+    const int grid = (int)(need < cap ? need : cap);
     if (grid < 1) return hipSuccess;
+    // one transform per slot: the loop-free kernel (no prefetch registers: 58 instead
+    // of 98 VGPRs at 1024 points, 6 workgroups per CU): equal at 256 / 1024 points,
+    // -1.3 % at 2048, -6.4 % at 4096 (profiles/r05_ab2_c2c_grid.jsonl); knob C2C_ONE = 0
+    // keeps the looping kernel (A/B)
+    if (tpw == 1 && knob(KNOB_C2C_ONE, 1) == 1) {
+        hipLaunchKernelGGL((k_c2c<N, FWD, true>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pas,
+                           tab, scale);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((k_c2c<N, FWD>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pas, tab,
                        scale);
     return hipGetLastError();
