@@ -398,7 +398,7 @@ CASES = {
     **{f"rwc{w}u{u}l{l}s{s_}b{b}": (lambda w=w, u=u, l=l, s_=s_, b=b: case_rwc(w, u, l, s_, b))
        for (w, u, l, s_) in [(4, 1, 1, 1), (4, 2, 1, 1), (4, 4, 1, 1), (4, 1, 0, 0), (4, 2, 0, 0), (4, 4, 0, 0),
                              (4, 2, 0, 1), (4, 2, 1, 0), (1, 2, 1, 1), (1, 2, 0, 0), (4, 8, 1, 1)]
-       for b in (1024, 2048, 4096, 8192)},
+       for b in (1024, 2048, 4096, 8192, 16384, 32768, 65536)},
     **{f"ex{e}": (lambda e=e: case_stft_exp(e)) for e in range(8)},
     "rw1": lambda: case_rw(1), "rw4": lambda: case_rw(4),
     **{f"rw{w}b{b}": (lambda w=w, b=b: case_rw(w, blocks=b)) for w in (1, 4) for b in (256, 512, 1024, 2048, 16384)},
