@@ -93,6 +93,20 @@ def _stft(L):
     return h
 
 
+def case_stft_nfft(L, s, nfft, hop, nch=32, seconds=600, sr=48000):
+    """magnitude rows at any nfft (speech lengths: the mixed-radix register kernels)"""
+    n = seconds * sr
+    fr = frames_of(n, nfft, hop)
+    sig, out = buf(("stftn", nfft, hop, nch, n), lambda: (torch.rand(nch, n, device="cuda") * 2 - 1,
+                                                          torch.empty(nch, fr, nfft, device="cuda")))
+    h = vp()
+    ok(L, L.vv_dsp_stft_create(C.byref(StftParams(nfft, hop, 1)), C.byref(h)), "stft create")
+    nf = sz()
+    f = L.vv_dsp_stft_spectrogram_device
+    return (lambda: ok(L, f(h, sig.data_ptr(), n, nch, n, out.data_ptr(), fr * nfft, s, C.byref(nf)), "stft")), \
+        nch * n * 4 + nch * fr * nfft * 4, (lambda: out.clone())
+
+
 def case_stft_rows(L, s, kind, nch, seconds):
     """kind mag / pow (packed 513-float rows) / pow544 (rows 544 floats apart;
     bytes counted as the 513 floats written)"""
@@ -137,6 +151,43 @@ def case_c2c(L, s, n=1024, batch=65536):
         2 * batch * n * 8, (lambda: y.clone())
 
 
+def case_real(L, s, n, batch, kind):
+    """batched R2C (kind 1: real[n] -> cpx[n/2+1]) or C2R (kind 2, 1/n scaled)"""
+    h = n // 2 + 1
+    if kind == 1:
+        x, y = buf(("r2c", n, batch), lambda: (torch.rand(batch, n, device="cuda") - 0.5,
+                                               torch.empty(batch, h, dtype=torch.complex64, device="cuda")))
+    else:
+        x, y = buf(("c2r", n, batch), lambda: (torch.complex(torch.rand(batch, h, device="cuda") - 0.5,
+                                                             torch.rand(batch, h, device="cuda") - 0.5),
+                                               torch.empty(batch, n, device="cuda")))
+    p = vp()
+    ok(L, L.vv_dsp_fft_make_plan_many(n, kind, 1 if kind == 1 else -1, batch, C.byref(p)), "fft plan")
+    return (lambda: ok(L, L.vv_dsp_fft_execute_device(p, x.data_ptr(), y.data_ptr(), s), "fft")), \
+        batch * (n * 4 + h * 8), (lambda: y.clone())
+
+
+def case_hilbert(L, s, n=1024, batch=65536):
+    """batched Hilbert analytic rows real[batch][n] -> cpx[batch][n] (12 B per point)"""
+    x, z = buf(("hil", n, batch), lambda: (torch.rand(batch, n, device="cuda") - 0.5,
+                                           torch.empty(batch, n, dtype=torch.complex64, device="cuda")))
+    L.vv_dsp_hilbert_analytic_device.argtypes = [vp, sz, sz, vp, vp]
+    return (lambda: ok(L, L.vv_dsp_hilbert_analytic_device(x.data_ptr(), n, batch, z.data_ptr(), s), "hilbert")), \
+        batch * n * 12, (lambda: z.clone())
+
+
+def case_dct(L, s, n=1024, batch=131072):
+    """batched DCT-II forward rows (8 B per point)"""
+    x, y = buf(("dct", n, batch), lambda: (torch.rand(batch, n, device="cuda") - 0.5,
+                                           torch.empty(batch, n, device="cuda")))
+    L.vv_dsp_dct_make_plan.argtypes = [sz, C.c_int, C.c_int, C.POINTER(vp)]
+    L.vv_dsp_dct_execute_device.argtypes = [vp, vp, vp, sz, vp]
+    p = vp()
+    ok(L, L.vv_dsp_dct_make_plan(n, 2, 1, C.byref(p)), "dct plan")
+    return (lambda: ok(L, L.vv_dsp_dct_execute_device(p, x.data_ptr(), y.data_ptr(), batch, s), "dct")), \
+        batch * n * 8, (lambda: y.clone())
+
+
 def burst(case, k):
     """k launches back to back per timed call (the per-launch time is ms / k)"""
     fn, byts, get = case
@@ -160,6 +211,12 @@ CASES = {
     "mfcc": lambda L, s: case_mel(L, s, True),
     "c2c1024": case_c2c,
     **{f"c2c{n}": (lambda L, s, n=n: case_c2c(L, s, n, (1 << 26) // n)) for n in (64, 256, 2048, 4096, 8192)},
+    **{f"r2c{n}": (lambda L, s, n=n: case_real(L, s, n, (1 << 27) // n, 1)) for n in (256, 400, 480, 960, 1024, 4096)},
+    **{f"c2r{n}": (lambda L, s, n=n: case_real(L, s, n, (1 << 27) // n, 2)) for n in (256, 1024, 4096)},
+    **{f"hilbert{n}": (lambda L, s, n=n: case_hilbert(L, s, n, (1 << 26) // n)) for n in (256, 1024, 4096)},
+    **{f"dct{n}": (lambda L, s, n=n: case_dct(L, s, n, (1 << 27) // n)) for n in (256, 1024, 2048)},
+    **{f"c2c{n}": (lambda L, s, n=n: case_c2c(L, s, n, (1 << 26) // n)) for n in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960, 1000, 2000, 3000, 4000)},
+    **{f"stft{n}": (lambda L, s, n=n: case_stft_nfft(L, s, n, n // 4)) for n in (400, 480, 960)},
 }
 
 

@@ -47,3 +47,56 @@ def test_c2c_one_transform_in_place():
     y = x.clone()
     p(y, out=y)
     assert torch.equal(y.view(torch.int64), ref.view(torch.int64))
+
+
+@pytest.mark.parametrize("n", [256, 1024, 4096])
+@pytest.mark.parametrize("kind", ["r2c", "c2r"])
+def test_real_grid_shapes_bit_identical(n, kind):
+    """R2C / C2R (fft_kiss.c:120-174 semantics): C2R of n <= 1024 launches one
+    transform per slot on a non-persistent grid by default; knob REAL_TPW = 0 / 1
+    forces the persistent / one-per-slot grid -- the same values bit for bit."""
+    batch, h = 1029, n // 2 + 1
+    g = torch.Generator(device="cuda").manual_seed(n)
+    if kind == "r2c":
+        x = torch.rand(batch, n, device="cuda", generator=g) - 0.5
+        p = vv.FftPlan(n, vv.R2C, vv.FWD, batch=batch)
+    else:
+        x = torch.complex(torch.rand(batch, h, device="cuda", generator=g) - 0.5,
+                          torch.rand(batch, h, device="cuda", generator=g) - 0.5)
+        p = vv.FftPlan(n, vv.C2R, vv.BWD, batch=batch)
+    ref = p(x).clone()
+    for v in (0, 1):
+        with vv.knobs(REAL_TPW=v):
+            got = p(x).clone()
+        assert torch.equal(got.view(torch.int32) if got.dtype == torch.float32 else got.view(torch.int64),
+                           ref.view(torch.int32) if ref.dtype == torch.float32 else ref.view(torch.int64)), v
+    xn = x.cpu().numpy().astype(np.complex128 if kind == "c2r" else np.float64)
+    want = np.fft.rfft(xn, axis=1) if kind == "r2c" else np.fft.irfft(xn, n=n, axis=1)
+    err = np.abs(ref.cpu().numpy() - want).max() / np.abs(want).max()
+    assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("n", [400, 441, 960])
+@pytest.mark.parametrize("kind", ["c2c", "r2c"])
+def test_mixed_register_grid_bit_identical(n, kind):
+    """Speech-length C2C and R2C rows on the two-pass register kernel
+    (mixed_fft.hip k_stft_sq MODE 0 / 5): a non-persistent grid by default, knob
+    MIX_TPW = 0 the persistent one -- the same values bit for bit, and the
+    default against f64 (fft_kiss.c:76-92 / 120-147 semantics)."""
+    batch = 1037
+    g = torch.Generator(device="cuda").manual_seed(n)
+    if kind == "c2c":
+        x = torch.complex(torch.rand(batch, n, device="cuda", generator=g) - 0.5,
+                          torch.rand(batch, n, device="cuda", generator=g) - 0.5)
+        p = vv.FftPlan(n, vv.C2C, vv.FWD, batch=batch)
+    else:
+        x = torch.rand(batch, n, device="cuda", generator=g) - 0.5
+        p = vv.FftPlan(n, vv.R2C, vv.FWD, batch=batch)
+    ref = p(x).clone()
+    with vv.knobs(MIX_TPW=0):
+        got = p(x).clone()
+    assert torch.equal(got.view(torch.int64), ref.view(torch.int64))
+    xn = x.cpu().numpy().astype(np.complex128 if kind == "c2c" else np.float64)
+    want = np.fft.fft(xn, axis=1) if kind == "c2c" else np.fft.rfft(xn, axis=1)
+    err = np.abs(ref.cpu().numpy() - want).max() / np.abs(want).max()
+    assert err < 2e-5, err

@@ -95,7 +95,9 @@ hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long lon
         if (!tab || !pas) return hipErrorOutOfMemory;                                                       \
         constexpr int WG = Wg<NN>::value, F = Wg<NN>::F;                                                    \
         static std::atomic<int> capc;                                                                                 \
-        const int cap = cached_grid(capc, (const void*)k_hilbert_pair<NN>, WG, 0, 1LL << 40);                 \
+        const int cap0 = cached_grid(capc, (const void*)k_hilbert_pair<NN>, WG, 0, 1LL << 40);                \
+        /* knob ANA_TPW = 1: not persistent (A/B; Hilbert 1024 / 4096 +6 %, r05_ab2_analytic_mixed_grid) */ \
+        const long long cap = knob(KNOB_ANA_TPW, 0) == 1 ? (1LL << 30) : cap0;                              \
         const long long need = ((batch + 1) / 2 + F - 1) / F;                                               \
         const int grid = (int)(need < cap ? need : cap);                                                    \
         hipLaunchKernelGGL(k_hilbert_pair<NN>, dim3(grid), dim3(WG), 0, s, x, z, batch, n, n, pas, tab);    \
@@ -222,7 +224,9 @@ hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long ba
         if (!tab || !pas) return hipErrorOutOfMemory;                                                        \
         constexpr int WG = Wg<NN>::value, F = Wg<NN>::F;                                                     \
         static std::atomic<int> capc;                                                                                  \
-        const int cap = cached_grid(capc, (const void*)k_dct2_pair<NN, 0>, WG, 0, 1LL << 40);                  \
+        const int cap0 = cached_grid(capc, (const void*)k_dct2_pair<NN, 0>, WG, 0, 1LL << 40);                 \
+        /* knob ANA_TPW = 1: not persistent (A/B; DCT-II 2048 +22 %, r05_ab2_analytic_mixed_grid) */        \
+        const long long cap = knob(KNOB_ANA_TPW, 0) == 1 ? (1LL << 30) : cap0;                               \
         const long long need = ((batch + 1) / 2 + F - 1) / F;                                                \
         const int grid = (int)(need < cap ? need : cap);                                                     \
         if (policy == 1)                                                                                     \

@@ -300,6 +300,9 @@ static hipError_t run_r2c(const float* in, float2* out, long long batch, long lo
     const int cap = cached_grid(capc, (const void*)k_r2c<M>, WG, 0, 1LL << 40, 1);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < cap ? need : cap);
+    // knob REAL_TPW = 1: one transform per slot, not persistent (A/B; 3.6 % slower
+    // at 256 points, 9.8 % at 4096, equal at 1024: profiles/r05_ab2_real_grid.jsonl)
+    if (knob(KNOB_REAL_TPW, 0) == 1) grid = (int)(need < (1LL << 30) ? need : (1LL << 30));
     if (grid < 1) return hipSuccess;
     hipLaunchKernelGGL(k_r2c<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pM, tM, t2M);
     return hipGetLastError();
@@ -317,6 +320,10 @@ static hipError_t run_c2r(const float2* in, float* out, long long batch, long lo
     const int cap = cached_grid(capc, (const void*)k_c2r<M>, WG, 0, 1LL << 40);
     long long need = (batch + F - 1) / F;
     int grid = (int)(need < cap ? need : cap);
+    // n <= 1024: one transform per slot, not persistent -- 256 points -6.1 %, 1024
+    // -4.4 %, 4096 equal, bit-identical (profiles/r05_ab2_real_grid.jsonl); knob
+    // REAL_TPW = 0 / 1 forces the persistent / one-per-slot grid (A/B)
+    if (knob(KNOB_REAL_TPW, M <= 512 ? 1 : 0) == 1) grid = (int)(need < (1LL << 30) ? need : (1LL << 30));
     if (grid < 1) return hipSuccess;
     hipLaunchKernelGGL(k_c2r<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pM, tM, t2M,
                        1.0f / (float)M);

@@ -847,7 +847,14 @@ hipError_t run_stft_sq(const MixIO& io, long long pairs, hipStream_t s) {
     if (!tab) return hipErrorOutOfMemory;
     constexpr int TPW = Sq<N1, N2, MODE>::TPW;
     const long long work = (pairs + 4 * TPW - 1) / (4 * TPW);
-    const int grid = persistent_grid((const void*)k_stft_sq<N1, N2, MODE>, 256, 0, work);
+    // batched C2C (MODE 0) and R2C (MODE 5) rows: a non-persistent grid, each
+    // wave's transforms once -- -4..-11 % (C2C 320..960) and -7..-14 % (R2C 400 /
+    // 480 / 960) on the same buffers, bit-identical; the STFT modes measured 6-10 %
+    // slower that way and stay persistent (profiles/r05_ab2_analytic_mixed_grid.jsonl).
+    // Knob MIX_TPW = 0 / 1 forces the persistent / non-persistent grid (A/B)
+    const bool once = knob(KNOB_MIX_TPW, (MODE == 0 || MODE == 5) ? 1 : 0) == 1;
+    const int grid = once ? (int)(work < (1LL << 30) ? work : (1LL << 30))
+                          : persistent_grid((const void*)k_stft_sq<N1, N2, MODE>, 256, 0, work);
     hipLaunchKernelGGL((k_stft_sq<N1, N2, MODE>), dim3(grid), dim3(256), 0, s, io, pairs, tab);
     return hipGetLastError();
 }
@@ -930,7 +937,10 @@ hipError_t run_mixed_t(const MixedPlan& pl, const MixIO& io, long long batch, hi
     constexpr int F = 256 / T;
     const size_t lds = sizeof(float2) * (size_t)pl.n * (1 + F);
     const long long work = (batch + F - 1) / F;
-    const int grid = persistent_grid((const void*)k_fft_mixed<T, MODE>, 256, lds, work);
+    // knob MIX_TPW = 1: a non-persistent grid (A/B; 1000-4000-point C2C measured
+    // 8-22 % slower that way, profiles/r05_ab2_analytic_mixed_grid.jsonl)
+    const int grid = knob(KNOB_MIX_TPW, 0) == 1 ? (int)(work < (1LL << 30) ? work : (1LL << 30))
+                                                 : persistent_grid((const void*)k_fft_mixed<T, MODE>, 256, lds, work);
     hipLaunchKernelGGL((k_fft_mixed<T, MODE>), dim3(grid), dim3(256), lds, s, pl, io, batch, tab);
     return hipGetLastError();
 }
