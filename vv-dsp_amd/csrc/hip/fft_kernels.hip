@@ -120,7 +120,7 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     // of 98 VGPRs at 1024 points, 6 workgroups per CU): equal at 256 / 1024 points,
     // -1.3 % at 2048, -6.4 % at 4096 (profiles/r05_ab2_c2c_grid.jsonl); knob C2C_ONE = 0
     // keeps the looping kernel (A/B)
-    if (tpw == 1 && knob(KNOB_C2C_ONE, 1) == 1) {
+    if (tpw == 1 && need <= cap && knob(KNOB_C2C_ONE, 1) == 1) {   // (every slot's one transform in the grid)
         hipLaunchKernelGGL((k_c2c<N, FWD, true>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pas,
                            tab, scale);
         return hipGetLastError();
