@@ -45,19 +45,32 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
     constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
     __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
-    stage_twiddles<N, WG>(ltab, gpass, gtab);
-    __syncthreads();
-    const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
-    const long long stride = (long long)gridDim.x * F;
-    long long f = uni<G::T>((long long)blockIdx.x * F + slot);
+    const TwTab<N> tw{ltab};
     const long long fend = batch;
-    if constexpr (ONE) {   // one transform per slot: no loop, no prefetch registers
-        if (f >= fend) return;
+    if constexpr (ONE) {
+        // one transform per slot, no loop and no prefetch registers.  One-wave
+        // transforms (N <= 1024) issue their loads before the block stages its
+        // twiddles, so the load latency overlaps the staging: 1024 points 0.1815 ->
+        // 0.1739 ms, 256 -1.8 %; for 2048 / 4096 (a transform over several waves)
+        // that order measured +23 % / +2 %, so they load after the barrier
+        // (profiles/r05_ab2_c2c_grid.jsonl)
+        constexpr bool EARLY = G::T <= 64;
+        const long long f = uni<G::T>((long long)blockIdx.x * F + slot);
+        const bool act = f < fend;
         float2 v[G::P];
+        if (EARLY && act) {
 #pragma unroll
-        for (int r = 0; r < G::P; ++r) v[r] = ld_nt(in + f * in_dist + t + r * G::T);
+            for (int r = 0; r < G::P; ++r) v[r] = ld_nt(in + f * in_dist + t + r * G::T);
+        }
+        stage_twiddles<N, WG>(ltab, gpass, gtab);
+        __syncthreads();
+        if (!act) return;
+        if constexpr (!EARLY) {
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) v[r] = ld_nt(in + f * in_dist + t + r * G::T);
+        }
         fft_regs<N, FWD, false, RI, TwTab<N>, false, false, 1>(v, t, my, tw);
         float2* dst = out + f * out_dist;
 #pragma unroll
@@ -68,6 +81,10 @@ k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long lo
         }
         return;
     }
+    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    __syncthreads();
+    const long long stride = (long long)gridDim.x * F;
+    long long f = uni<G::T>((long long)blockIdx.x * F + slot);
     float2 nx[G::P];
     if (f < fend) {
 #pragma unroll
@@ -120,6 +137,8 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     // of 98 VGPRs at 1024 points, 6 workgroups per CU): equal at 256 / 1024 points,
     // -1.3 % at 2048, -6.4 % at 4096 (profiles/r05_ab2_c2c_grid.jsonl); knob C2C_ONE = 0
     // keeps the looping kernel (A/B)
+    // (two consecutive transforms per slot on this kernel measured +0.4 / +11 / +22 %
+    // at 1024 / 2048 / 4096 points)
     if (tpw == 1 && need <= cap && knob(KNOB_C2C_ONE, 1) == 1) {   // (every slot's one transform in the grid)
         hipLaunchKernelGGL((k_c2c<N, FWD, true>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pas,
                            tab, scale);
