@@ -1377,6 +1377,8 @@ struct vvhip_mel {
     int* chunks = nullptr;  // balanced chunk schedule of the filters (mel_chunk_schedule)
     int* cbeg = nullptr;    // first chunk of each filter, [n_mels + 1]
     int nc = 0;
+    float* Wf = nullptr;    // the fused kernels' chunk windows (MelArgs: rows of lc + 1 floats, lo last)
+    int lc = 0;             // window length (0: no fused layout)
     float* D = nullptr;     // DCT-II table [n_coeffs][n_mels]
     float* lift = nullptr;  // lifter factors [n_coeffs]
     hipStream_t stream = nullptr;
@@ -1393,6 +1395,7 @@ void vvhip_mel_destroy(vvhip_mel* m) {
         (void)hipStreamDestroy(m->stream);
     }
     if (m->W) (void)hipFree(m->W);
+    if (m->Wf) (void)hipFree(m->Wf);
     if (m->chunks) (void)hipFree(m->chunks);
     if (m->cbeg) (void)hipFree(m->cbeg);
     if (m->D) (void)hipFree(m->D);
@@ -1433,8 +1436,27 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
     }
     m->nnz = (int)w.size();
     std::vector<int> chunks, cbeg;
-    mel_chunk_schedule(meta.data(), (int)n_mels, &chunks, &cbeg);
+    const int lc = mel_chunk_schedule(meta.data(), (int)n_mels, &chunks, &cbeg);
     m->nc = (int)(chunks.size() / 3);
+    // the fused kernels' layout (MelArgs): chunk c's window of lc bins [lo', lo' + lc),
+    // lo' = min(lo, nbins - lc) so it stays inside the row, as a row of lc + 1 floats
+    // (weights of the chunk's own bins, zeros elsewhere, then lo' as int bits)
+    std::vector<float> wf;
+    if (fb && m->nc > 0 && lc % 4 == 0 && lc <= (int)nbins) {
+        const int lcs = lc + 1;
+        wf.assign((size_t)m->nc * lcs, 0.0f);
+        for (int c = 0; c < m->nc; ++c) {
+            const int lo = chunks[3 * c], len = chunks[3 * c + 1], off = chunks[3 * c + 2];
+            const int lo2 = lo < (int)nbins - lc ? lo : (int)nbins - lc;
+            for (int j = 0; j < lc; ++j) {
+                const int k = lo2 + j;
+                if (k >= lo && k < lo + len) wf[(size_t)c * lcs + j] = w[(size_t)off + (k - lo)];
+            }
+            int bits = lo2;
+            std::memcpy(&wf[(size_t)c * lcs + lc], &bits, sizeof bits);
+        }
+        m->lc = lc;
+    }
     // DCT-II rows cos(pi (j + 1/2) i / M) (dct.c:21-30), and the lifter of mel.c:300-302
     std::vector<float> D(n_coeffs * n_mels), L(n_coeffs, 1.0f);
     for (size_t i = 0; i < n_coeffs; ++i)
@@ -1449,6 +1471,8 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
               hipMalloc(&m->cbeg, sizeof(int) * cbeg.size()) == hipSuccess &&
               hipMemcpy(m->cbeg, cbeg.data(), sizeof(int) * cbeg.size(), hipMemcpyHostToDevice) == hipSuccess &&
               hipMalloc(&m->W, sizeof(float) * (w.size() + 1)) == hipSuccess &&
+              hipMalloc(&m->Wf, sizeof(float) * (wf.size() + 1)) == hipSuccess &&
+              (wf.empty() || hipMemcpy(m->Wf, wf.data(), sizeof(float) * wf.size(), hipMemcpyHostToDevice) == hipSuccess) &&
               (w.empty() || hipMemcpy(m->W, w.data(), sizeof(float) * w.size(), hipMemcpyHostToDevice) == hipSuccess) &&
               hipMalloc(&m->D, sizeof(float) * (D.size() + 1)) == hipSuccess &&
               (D.empty() || hipMemcpy(m->D, D.data(), sizeof(float) * D.size(), hipMemcpyHostToDevice) == hipSuccess) &&
@@ -1502,6 +1526,8 @@ int vvhip_stft_mel_device(vvhip_stft* h, vvhip_mel* m, const float* d_signal, si
         MelArgs a;
         a.W = m->W;
         a.chunks = m->chunks;
+        a.Ww = m->lc > 0 ? m->Wf : nullptr;   // the chunk windows (launch_stft_mel's choice)
+        a.lcw = m->lc;
         a.cbeg = m->cbeg;
         a.D = m->D;
         a.lift = m->lift;

@@ -144,6 +144,15 @@ struct MelArgs {
     const float* D = nullptr;      // DCT-II rows [C][M]
     const float* lift = nullptr;   // lifter factors [C]
     int nnz = 0, nc = 0, M = 0, C = 0;
+    // The layout the kernel reads: cw = 3 -- W packed with the chunk table above;
+    // cw = 0 -- each chunk's window of lc bins as a row of lcs = lc + 1 floats in W,
+    // [c lcs + j] the weight of bin lo_c + j (zero outside the chunk), [c lcs + lc]
+    // lo_c's bits, the window inside the row (lo_c + lc <= n/2 + 1), lc % 4 == 0, no
+    // chunk table.  The plan passes the packed layout plus the windows (Ww, lcw);
+    // launch_stft_mel gives log-mel the windows and MFCC the packed layout.
+    int lc = 0, lcs = 0, cw = 3;
+    const float* Ww = nullptr;
+    int lcw = 0;
     float eps = 0.0f;
 };
 // Log-mel (kind 0) or MFCC (kind 1) rows [ch][frame][M or C] straight from the
