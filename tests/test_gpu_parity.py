@@ -609,7 +609,7 @@ def test_golden_dct(amd, golden):
         np.testing.assert_allclose(xi, g["x"], rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 8, 40, 63, 64, 257, 400, 1000, 1024, 4800, 8192, 16384])
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 40, 63, 64, 256, 257, 400, 1000, 1024, 4800, 8192, 16384])
 def test_dct_types_vs_formula(amd, n):
     import scipy.fft
     rng = np.random.default_rng(n)
@@ -842,16 +842,17 @@ def test_dct2_batched_device(vdev, n):
 def test_dct_nan_policy_matches_reference(amd, ref, policy):
     """NaN/Inf handling of vv_dsp_dct_execute (dct.c:98,130, nan_policy.c):
     same status as the reference, same non-finite pattern, finite values within
-    tolerance -- for the single-pass (1024) and the multi-pass (1000) paths."""
+    tolerance -- for the single-pass (1024; 256 with its mirror bins through LDS)
+    and the multi-pass (1000) paths."""
     import ctypes as C
-    for n in (1024, 1000):
+    for n in (1024, 256, 1000):
         rng = np.random.default_rng(n + policy)
         x = rng.standard_normal(n).astype(np.float32)
         x[[3, 77]] = np.nan
         if policy != 3:
             # clamp maps +-Inf to +-FLT_MAX, whose FFT-based transform overflows where the
             # reference's O(n^2) f32 sums do not: only NaN is compared under clamp
-            x[500] = np.inf
+            x[n // 2 - 12] = np.inf
         outs = []
         for lib in (amd, ref):
             lib.lib.vv_dsp_set_nan_policy.argtypes = [C.c_int]

@@ -133,12 +133,16 @@ k_dct2_pair(const float* __restrict__ x, float* __restrict__ X, long long batch,
     const TwTab<N> tw{ltab};
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
-    // W_4N^k for this thread's output bins (loop invariant)
+    // W_4N^k for this thread's output bins (loop invariant).  PAIRV: bins k =
+    // out_pos(t, q) of the mirror-paired last pass; otherwise (N = 256: one last-pass
+    // butterfly per thread) bins k = t + T r, whose mirrors N - k are read back
+    // through LDS
+    constexpr bool PAIRV = G::CAN_PAIR;
     float2 wk[G::P];
     int kq[G::P];
 #pragma unroll
     for (int q = 0; q < G::P; ++q) {
-        kq[q] = out_pos<N, true>(t, q);
+        kq[q] = PAIRV ? out_pos<N, true>(t, q) : t + G::T * q;
         wk[q] = tw4n[kq[q]];
     }
     const long long pairs = (batch + 1) / 2;
@@ -173,9 +177,30 @@ k_dct2_pair(const float* __restrict__ x, float* __restrict__ X, long long batch,
             }
             xsync<G::T>();   // the FFT's first exchange overwrites `my`
         }
-        fft_regs<N, true, true>(v, t, my, tw);
         float* oa = X + ra * dist;
         float* ob = oa + dist;
+        if constexpr (!PAIRV) {
+            // natural last-pass layout, then (Z[k], Z[N - k]) from LDS for k = t + T r:
+            // lane-contiguous bins, stored straight out
+            fft_regs<N, true, false>(v, t, my, tw);
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<N>(t, q))] = v[q];
+            xsync<G::T>();
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const int k = kq[r];
+                const float2 Z = my[G::pad(k)], Zm = my[G::pad((N - k) & (N - 1))];
+                const float2 Va = make_float2(0.5f * (Z.x + Zm.x), 0.5f * (Z.y - Zm.y));
+                const float2 Vb = make_float2(0.5f * (Z.y + Zm.y), -0.5f * (Z.x - Zm.x));
+                const float2 W = wk[r];
+                __builtin_nontemporal_store(nan_fix<POL>(W.x * Va.x - W.y * Va.y), oa + k);
+                if (hb) __builtin_nontemporal_store(nan_fix<POL>(W.x * Vb.x - W.y * Vb.y), ob + k);
+            }
+            xsync<G::T>();   // the next row pair's permutation overwrites `my`
+            continue;
+        } else {
+            fft_regs<N, true, true>(v, t, my, tw);
+        }
         float2 o[G::P];   // (Xa[k], Xb[k]) at k = kq[q]
 #pragma unroll
         for (int q = 0; q < G::P; ++q) {
@@ -209,8 +234,8 @@ k_dct2_pair(const float* __restrict__ x, float* __restrict__ X, long long batch,
 }
 
 bool dct2_fused_supported(long long n) {
-    // mirror pairing needs >= 2 last-pass butterflies per thread (not 256, 4096)
-    return n >= 2 && n <= 2048 && (n & (n - 1)) == 0 && n != 256;
+    // 256 (one last-pass butterfly per thread) reads its mirror bins through LDS
+    return n >= 2 && n <= 2048 && (n & (n - 1)) == 0;
 }
 
 hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long batch, int policy, hipStream_t s) {
@@ -238,7 +263,7 @@ hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long ba
         return hipGetLastError();                                                                            \
     }
     switch (n) {
-        VVH_DCT(2) VVH_DCT(4) VVH_DCT(8) VVH_DCT(16) VVH_DCT(32) VVH_DCT(64) VVH_DCT(128) VVH_DCT(512)
+        VVH_DCT(2) VVH_DCT(4) VVH_DCT(8) VVH_DCT(16) VVH_DCT(32) VVH_DCT(64) VVH_DCT(128) VVH_DCT(256) VVH_DCT(512)
         VVH_DCT(1024) VVH_DCT(2048)
         default: return hipErrorInvalidValue;
     }
