@@ -234,8 +234,9 @@ k_dct2_pair(const float* __restrict__ x, float* __restrict__ X, long long batch,
 }
 
 bool dct2_fused_supported(long long n) {
-    // 256 (one last-pass butterfly per thread) reads its mirror bins through LDS
-    return n >= 2 && n <= 2048 && (n & (n - 1)) == 0;
+    // 256, 4096, 8192 (one last-pass butterfly per thread) read their mirror bins
+    // through LDS; 4096 / 8192 run one transform per workgroup (T = 256 / 512)
+    return n >= 2 && n <= 8192 && (n & (n - 1)) == 0;
 }
 
 hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long batch, int policy, hipStream_t s) {
@@ -264,7 +265,7 @@ hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long ba
     }
     switch (n) {
         VVH_DCT(2) VVH_DCT(4) VVH_DCT(8) VVH_DCT(16) VVH_DCT(32) VVH_DCT(64) VVH_DCT(128) VVH_DCT(256) VVH_DCT(512)
-        VVH_DCT(1024) VVH_DCT(2048)
+        VVH_DCT(1024) VVH_DCT(2048) VVH_DCT(4096) VVH_DCT(8192)
         default: return hipErrorInvalidValue;
     }
 #undef VVH_DCT
