@@ -809,7 +809,7 @@ def test_golden_mel(amd, golden):
 
 
 # ---------------------------------------------------------------- batched single-pass Hilbert / DCT-II
-@pytest.mark.parametrize("n", [2, 8, 16, 128, 256, 1024, 2048, 4096])
+@pytest.mark.parametrize("n", [2, 8, 16, 128, 256, 1024, 2048, 4096, 8192])
 def test_hilbert_batched_device(vdev, n):
     """vv_dsp_hilbert_analytic over a batch of rows (two rows per complex FFT,
     odd batch -> last row alone) vs scipy.signal.hilbert in f64."""
@@ -824,7 +824,7 @@ def test_hilbert_batched_device(vdev, n):
         np.testing.assert_allclose(z.real, x, rtol=0, atol=0)   # the real part is the input itself
 
 
-@pytest.mark.parametrize("n", [2, 4, 16, 32, 40, 128, 256, 400, 512, 1000, 1024, 2048, 4096])
+@pytest.mark.parametrize("n", [2, 4, 16, 32, 40, 128, 256, 400, 512, 1000, 1024, 2048, 4096, 8192])
 def test_dct2_batched_device(vdev, n):
     """DCT-II over a batch of rows (two rows per complex FFT where the FFT can
     be mirror-paired) vs scipy.fft.dct(type 2)/2 in f64 (dct.c:21-30)."""

@@ -84,7 +84,7 @@ k_hilbert_pair(const float* __restrict__ x, float2* __restrict__ z, long long ba
     }
 }
 
-bool hilbert_fused_supported(long long n) { return n >= 2 && n <= 4096 && (n & (n - 1)) == 0; }
+bool hilbert_fused_supported(long long n) { return n >= 2 && n <= 8192 && (n & (n - 1)) == 0; }
 
 hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long long batch, hipStream_t s) {
     if (batch <= 0) return hipSuccess;
@@ -105,7 +105,7 @@ hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long lon
     }
     switch (n) {
         VVH_HIL(2) VVH_HIL(4) VVH_HIL(8) VVH_HIL(16) VVH_HIL(32) VVH_HIL(64) VVH_HIL(128) VVH_HIL(256)
-        VVH_HIL(512) VVH_HIL(1024) VVH_HIL(2048) VVH_HIL(4096)
+        VVH_HIL(512) VVH_HIL(1024) VVH_HIL(2048) VVH_HIL(4096) VVH_HIL(8192)
         default: return hipErrorInvalidValue;
     }
 #undef VVH_HIL
