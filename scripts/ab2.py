@@ -210,7 +210,7 @@ CASES = {
     "logmel8": lambda L, s: case_mel(L, s, False, nch=8),
     "mfcc": lambda L, s: case_mel(L, s, True),
     "c2c1024": case_c2c,
-    **{f"c2c{n}": (lambda L, s, n=n: case_c2c(L, s, n, (1 << 26) // n)) for n in (64, 256, 2048, 4096, 8192)},
+    **{f"c2c{n}": (lambda L, s, n=n: case_c2c(L, s, n, (1 << 26) // n)) for n in (16, 32, 64, 128, 256, 512, 2048, 4096, 8192)},
     **{f"r2c{n}": (lambda L, s, n=n: case_real(L, s, n, (1 << 27) // n, 1)) for n in (256, 400, 480, 960, 1024, 2048, 4096, 8192, 16384)},
     **{f"c2r{n}": (lambda L, s, n=n: case_real(L, s, n, (1 << 27) // n, 2)) for n in (256, 1024, 2048, 4096, 8192, 16384)},
     **{f"hilbert{n}": (lambda L, s, n=n: case_hilbert(L, s, n, (1 << 26) // n)) for n in (64, 256, 1024, 2048, 4096, 8192)},

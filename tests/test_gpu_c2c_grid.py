@@ -20,14 +20,17 @@ def _x(n, batch, seed):
                          torch.rand(batch, n, device="cuda", generator=g) - 0.5)
 
 
-@pytest.mark.parametrize("n", [256, 1024, 2048, 4096])
+@pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 1024, 2048, 4096])
 @pytest.mark.parametrize("fwd", [True, False])
 def test_c2c_grid_shapes_bit_identical(n, fwd):
+    """(16..128 points: the default stages each wave's 1024-point block through
+    LDS; knob C2C_SMALL = 0 the persistent strided kernel.)  Batch 1031: the last
+    wave's block is partial."""
     batch = 1031
     x = _x(n, batch, n + fwd)
     p = vv.FftPlan(n, vv.C2C, vv.FWD if fwd else vv.BWD, batch=batch)
     ref = p(x).clone()
-    for kn in ({"C2C_ONE": 0}, {"C2C_TPW": 0}, {"C2C_TPW": 3}, {"C2C_TPW": 1, "C2C_ONE": 0}):
+    for kn in ({"C2C_ONE": 0}, {"C2C_TPW": 0}, {"C2C_TPW": 3}, {"C2C_TPW": 1, "C2C_ONE": 0}, {"C2C_SMALL": 0}):
         with vv.knobs(**kn):
             got = p(x).clone()
         assert torch.equal(got.view(torch.int64), ref.view(torch.int64)), kn

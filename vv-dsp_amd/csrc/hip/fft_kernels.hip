@@ -35,21 +35,76 @@ namespace vvh {
 // (pass_exchange_ri): 26 KB of LDS per workgroup instead of 43 KB, so four
 // workgroups (16 waves) fit per CU and keep more transforms' loads in flight.
 template <int N, bool FWD, bool ONE = false>
-__global__ void __launch_bounds__(Wg<N>::value, N == 1024 ? 4 : 1)
+__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 || (ONE && N >= 16 && N <= 128)) ? 4 : 1)
 k_c2c(const float2* in, float2* out, long long batch, long long in_dist, long long out_dist,
       const float2* gpass, const float2* gtab, float scale) {
     using G = Geo<N>;
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     constexpr bool RI = N == 1024;
     constexpr int XF = RI ? ri_floats<N>() / 2 : G::LDS;   // float2 per transform
-    constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
+    // ONE with 16..128 points: each wave's 1024-point block staged through LDS
+    constexpr bool SMALL = ONE && G::T < 16 && G::P == 16;
+    constexpr int LDSX = G::NPASS > 1 ? F * XF : 1, LDSN = SMALL && F * G::LDS > LDSX ? F * G::LDS : LDSX;
     __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
     const TwTab<N> tw{ltab};
     const long long fend = batch;
-    if constexpr (ONE) {
+    if constexpr (SMALL) {
+        // small N (16..128): a wave's 64 / T transforms are 1024 consecutive points
+        // (8 KB).  Lane-strided loads would touch 16..64 lines per instruction, so
+        // the block moves as 16 B per lane, coalesced, and is re-laid through the
+        // wave's LDS area (its slots' exchange buffers, padded 1 per 16) in both
+        // directions.  The host takes this only for dense rows (dist == N).
+        constexpr int WS = 64 / G::T;   // transforms per wave
+        const int wv = lt >> 6, lane = lt & 63, sl = slot - wv * WS;
+        const long long fw = (long long)blockIdx.x * F + (long long)wv * WS;   // the wave's first transform
+        const long long nvl = fend - fw < WS ? fend - fw : WS;                   // its transforms in the batch
+        const int nval = nvl > 0 ? (int)nvl * N : 0;                            // valid points of the block
+        float2* wa = lds + wv * WS * G::LDS;                                    // the wave's LDS area
+        stage_twiddles<N, WG>(ltab, gpass, gtab);
+        __syncthreads();
+        if (nval == 0) return;
+        {
+            vf4_t blk[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = i * 128 + 2 * lane;
+                blk[i] = e < nval ? __builtin_nontemporal_load(reinterpret_cast<const vf4_t*>(in + fw * N + e))
+                                  : vf4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = i * 128 + 2 * lane;
+                wa[G::pad(e)] = make_float2(blk[i][0], blk[i][1]);
+                wa[G::pad(e + 1)] = make_float2(blk[i][2], blk[i][3]);
+            }
+        }
+        xsync<64>();
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = wa[G::pad(sl * N + t + r * G::T)];
+        xsync<64>();   // the FFT's exchanges reuse the area
+        fft_regs<N, FWD, false, RI, TwTab<N>, false, false, 1>(v, t, my, tw);
+        xsync<64>();
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            float2 o = v[q];
+            if (!FWD) o = cscale(o, scale);
+            wa[G::pad(sl * N + out_pos<N>(t, q))] = o;
+        }
+        xsync<64>();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = i * 128 + 2 * lane;
+            if (e < nval) {
+                const float2 a = wa[G::pad(e)], b = wa[G::pad(e + 1)];
+                __builtin_nontemporal_store(vf4_t{a.x, a.y, b.x, b.y}, reinterpret_cast<vf4_t*>(out + fw * N + e));
+            }
+        }
+        return;
+    } else if constexpr (ONE) {
         // one transform per slot, no loop and no prefetch registers.  One-wave
         // transforms (N <= 1024) issue their loads before the block stages its
         // twiddles, so the load latency overlaps the staging: 1024 points 0.1815 ->
@@ -125,7 +180,13 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     // points -3.6 / -4.5 %, 4096 -0.5 %; 64 points +10 % and 8192 +32 % keep the
     // persistent grid (profiles/r05_ab2_c2c_grid.jsonl).  Knob C2C_TPW = t > 0:
     // t transforms per wave slot; 0: the persistent grid (A/B)
-    const long long tpw = knob(KNOB_C2C_TPW, N >= 256 && N <= 4096 ? 1 : -1);
+    // 16..128 points with dense rows: the same one-transform grid, each wave's
+    // 1024-point block moved as 16 B per lane and re-laid through LDS (k_c2c ONE,
+    // G::T < 16): 32 / 64 / 128 points 0.650 / 0.332 / 0.230 -> 0.177 ms for 2^26
+    // points (0.21 / 0.40 / 0.58 -> 0.76; profiles/r05_ab2_c2c_small.jsonl), bit-identical;
+    // knob C2C_SMALL = 0 keeps the persistent grid (A/B)
+    const bool small = N >= 16 && N <= 128 && in_dist == N && out_dist == N && knob(KNOB_C2C_SMALL, 1) == 1;
+    const long long tpw = knob(KNOB_C2C_TPW, (N >= 256 && N <= 4096) || small ? 1 : -1);
     long long need = (batch + F - 1) / F, cap = grid_cap;
     if (tpw > 0) {
         need = (batch + F * tpw - 1) / (F * tpw);
@@ -139,7 +200,7 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     // keeps the looping kernel (A/B)
     // (two consecutive transforms per slot on this kernel measured +0.4 / +11 / +22 %
     // at 1024 / 2048 / 4096 points)
-    if (tpw == 1 && need <= cap && knob(KNOB_C2C_ONE, 1) == 1) {   // (every slot's one transform in the grid)
+    if (tpw == 1 && need <= cap && knob(KNOB_C2C_ONE, 1) == 1 && (N >= 256 || small)) {   // (every slot's one transform in the grid)
         hipLaunchKernelGGL((k_c2c<N, FWD, true>), dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pas,
                            tab, scale);
         return hipGetLastError();
