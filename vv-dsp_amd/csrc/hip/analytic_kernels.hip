@@ -233,6 +233,106 @@ k_dct2_pair(const float* __restrict__ x, float* __restrict__ X, long long batch,
     }
 }
 
+// Small N (16..128, several row pairs per wave) with dense rows: the same
+// transform as k_dct2_pair, but a wave's 2 * 64 / T rows (2048 consecutive
+// floats) are loaded as 16 B per lane and re-laid through LDS (padded 1 per 16
+// floats), and its outputs leave the same way -- lane-strided 4 B accesses
+// touched 16 lines per instruction (0.10 of the roofline at 64 points).  The
+// loop is wave-uniform; slots past the batch compute on zeros and store nothing.
+template <int N, int POL>
+__global__ void __launch_bounds__(256, N >= 32 ? 3 : 4)
+k_dct2_small(const float* __restrict__ x, float* __restrict__ X, long long batch, const float2* gpass,
+             const float2* gtab, const float2* __restrict__ tw4n) {
+    using G = Geo<N>;
+    static_assert(G::P == 16 && G::T <= 8 && G::CAN_PAIR, "16..128 points");
+    constexpr int F = 256 / G::T, WS = 64 / G::T, WF = 2048 + 128;   // floats per wave area
+    constexpr int LDSN = (F * G::LDS > 4 * WF / 2) ? F * G::LDS : 4 * WF / 2;
+    __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    __shared__ float2 lw4[N];   // W_4N^k, k < N (read per output bin: no registers held)
+    stage_twiddles<N, 256>(ltab, gpass, gtab);
+    for (int i = threadIdx.x; i < N; i += 256) lw4[i] = tw4n[i];
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T, wv = lt >> 6, lane = lt & 63, sl = slot - wv * WS;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    float* wa = reinterpret_cast<float*>(lds) + wv * WF;   // the wave's staging area (its slots' buffers)
+    auto padf = [](int e) { return e + (e >> 4); };
+    const long long pairs = (batch + 1) / 2;
+    for (long long pw = (long long)blockIdx.x * F + (long long)wv * WS; pw < pairs; pw += (long long)gridDim.x * F) {
+        const long long r0 = 2 * pw;                       // the wave's first row
+        const long long nr = batch - r0 < 2 * WS ? batch - r0 : 2 * WS;
+        const int nval = (int)nr * N;                      // valid floats of the block
+        {
+            vf4_t blk[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = i * 256 + 4 * lane;
+                blk[i] = e < nval ? __builtin_nontemporal_load(reinterpret_cast<const vf4_t*>(x + r0 * N + e))
+                                  : vf4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = i * 256 + 4 * lane;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wa[padf(e + k)] = blk[i][k];
+            }
+        }
+        xsync<64>();
+        float a[G::P], b[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            a[r] = wa[padf(2 * sl * N + t + r * G::T)];
+            b[r] = wa[padf((2 * sl + 1) * N + t + r * G::T)];
+        }
+        xsync<64>();   // the permutation below and the FFT reuse the area
+        float2 v[G::P];
+        if constexpr (G::T == 1) {
+#pragma unroll
+            for (int j = 0; j < G::P; ++j) {
+                const int src = j < N / 2 ? 2 * j : 2 * N - 2 * j - 1;
+                v[j] = make_float2(nan_fix<POL>(a[src]), nan_fix<POL>(b[src]));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) my[G::pad(t + r * G::T)] = make_float2(nan_fix<POL>(a[r]), nan_fix<POL>(b[r]));
+            xsync<64>();
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const int j = t + r * G::T;
+                v[r] = my[G::pad(j < N / 2 ? 2 * j : 2 * N - 2 * j - 1)];
+            }
+            xsync<64>();
+        }
+        fft_regs<N, true, true>(v, t, my, tw);
+        // (the wave's LDS accesses run in program order: its FFT's last reads
+        // precede these writes into the same area)
+        xsync<64>();
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const float2 Z = v[q], Zm = mirror_of<N, true>(v, t, q);
+            const float2 Va = make_float2(0.5f * (Z.x + Zm.x), 0.5f * (Z.y - Zm.y));
+            const float2 Vb = make_float2(0.5f * (Z.y + Zm.y), -0.5f * (Z.x - Zm.x));
+            const int k = out_pos<N, true>(t, q);
+            const float2 W = lw4[k];
+            wa[padf(2 * sl * N + k)] = nan_fix<POL>(W.x * Va.x - W.y * Va.y);
+            wa[padf((2 * sl + 1) * N + k)] = nan_fix<POL>(W.x * Vb.x - W.y * Vb.y);
+        }
+        xsync<64>();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = i * 256 + 4 * lane;
+            if (e < nval) {
+                vf4_t w4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w4[k] = wa[padf(e + k)];
+                __builtin_nontemporal_store(w4, reinterpret_cast<vf4_t*>(X + r0 * N + e));
+            }
+        }
+        xsync<64>();   // the next block's loads overwrite the area
+    }
+}
+
 bool dct2_fused_supported(long long n) {
     // 256, 4096, 8192 (one last-pass butterfly per thread) read their mirror bins
     // through LDS; 4096 / 8192 run one transform per workgroup (T = 256 / 512)
@@ -243,6 +343,31 @@ hipError_t launch_dct2_fused(long long n, const float* x, float* X, long long ba
     if (batch <= 0) return hipSuccess;
     const float2* tw4n = twiddle_table((int)(4 * n));
     if (!tw4n) return hipErrorOutOfMemory;
+    // 16..128 points: the staged kernel, one wave block per 2 x 64 / T rows (not
+    // persistent); knob DCT_SMALL = 0 keeps k_dct2_pair (A/B)
+    if (n >= 16 && n <= 128 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)X & 15) == 0 && knob(KNOB_DCT_SMALL, 1) == 1) {
+#define VVH_DCTS(NN)                                                                                          \
+        case NN: {                                                                                            \
+            const float2* tab = twiddle_table(NN);                                                            \
+            const float2* pas = pass_twiddles(NN);                                                            \
+            if (!tab || !pas) return hipErrorOutOfMemory;                                                     \
+            constexpr int F = 256 / Geo<NN>::T;                                                               \
+            const long long need = ((batch + 1) / 2 + F - 1) / F;                                             \
+            const int grid = (int)(need < (1LL << 30) ? need : (1LL << 30));                                  \
+            if (policy == 1)                                                                                  \
+                hipLaunchKernelGGL((k_dct2_small<NN, 1>), dim3(grid), dim3(256), 0, s, x, X, batch, pas, tab, tw4n); \
+            else if (policy == 3)                                                                             \
+                hipLaunchKernelGGL((k_dct2_small<NN, 3>), dim3(grid), dim3(256), 0, s, x, X, batch, pas, tab, tw4n); \
+            else                                                                                              \
+                hipLaunchKernelGGL((k_dct2_small<NN, 0>), dim3(grid), dim3(256), 0, s, x, X, batch, pas, tab, tw4n); \
+            return hipGetLastError();                                                                         \
+        }
+        switch (n) {
+            VVH_DCTS(16) VVH_DCTS(32) VVH_DCTS(64) VVH_DCTS(128)
+            default: break;
+        }
+#undef VVH_DCTS
+    }
 #define VVH_DCT(NN)                                                                                          \
     case NN: {                                                                                               \
         const float2* tab = twiddle_table(NN);                                                               \
