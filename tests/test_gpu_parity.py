@@ -809,14 +809,14 @@ def test_golden_mel(amd, golden):
 
 
 # ---------------------------------------------------------------- batched single-pass Hilbert / DCT-II
-@pytest.mark.parametrize("n", [2, 8, 16, 128, 256, 1024, 2048, 4096, 8192])
+@pytest.mark.parametrize("n", [2, 8, 16, 32, 64, 128, 256, 1024, 2048, 4096, 8192])
 def test_hilbert_batched_device(vdev, n):
     """vv_dsp_hilbert_analytic over a batch of rows (two rows per complex FFT,
     odd batch -> last row alone) vs scipy.signal.hilbert in f64."""
     import scipy.signal
     import torch
     rng = np.random.default_rng(100 + n)
-    for batch in (1, 5, 64):
+    for batch in (1, 5, 64, 1029):
         x = rng.standard_normal((batch, n)).astype(np.float32)
         z = vdev.hilbert(torch.from_numpy(x).cuda()).cpu().numpy()
         ref = scipy.signal.hilbert(x.astype(np.float64), axis=1)

@@ -84,10 +84,125 @@ k_hilbert_pair(const float* __restrict__ x, float2* __restrict__ z, long long ba
     }
 }
 
+// Small N (16..128) with dense rows: k_hilbert_pair's arithmetic with each wave's
+// 2 x 64 / T input rows (2048 floats) loaded as 16 B per lane and re-laid through
+// LDS, and its complex outputs staged the same way (even rows, then odd rows) --
+// lane-strided 4 / 8 B accesses touched 16..64 lines per instruction; a
+// wave-uniform loop.
+template <int N>
+__global__ void __launch_bounds__(256, N >= 32 ? 3 : 4)
+k_hilbert_small(const float* __restrict__ x, float2* __restrict__ z, long long batch, const float2* gpass,
+                const float2* gtab) {
+    using G = Geo<N>;
+    static_assert(G::P == 16 && G::T <= 8, "16..128 points");
+    constexpr int F = 256 / G::T, WS = 64 / G::T, WF = 2048 + 128;   // floats per wave area
+    constexpr int LDSN = (F * G::LDS > 4 * WF / 2) ? F * G::LDS : 4 * WF / 2;
+    __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, 256>(ltab, gpass, gtab);
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T, wv = lt >> 6, lane = lt & 63, sl = slot - wv * WS;
+    float2* my = lds + (G::NPASS > 1 ? slot * G::LDS : 0);
+    float* wa = reinterpret_cast<float*>(lds) + wv * WF;
+    auto padf = [](int e) { return e + (e >> 4); };
+    const long long pairs = (batch + 1) / 2;
+    const float inv = 1.0f / (float)N;
+    for (long long pw = (long long)blockIdx.x * F + (long long)wv * WS; pw < pairs; pw += (long long)gridDim.x * F) {
+        const long long r0 = 2 * pw;
+        const long long nr = batch - r0 < 2 * WS ? batch - r0 : 2 * WS;
+        const int nval = (int)nr * N;
+        {
+            vf4_t blk[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = i * 256 + 4 * lane;
+                blk[i] = e < nval ? __builtin_nontemporal_load(reinterpret_cast<const vf4_t*>(x + r0 * N + e))
+                                  : vf4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = i * 256 + 4 * lane;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wa[padf(e + k)] = blk[i][k];
+            }
+        }
+        xsync<64>();
+        float a[G::P], b[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            a[r] = wa[padf(2 * sl * N + t + r * G::T)];
+            b[r] = wa[padf((2 * sl + 1) * N + t + r * G::T)];
+        }
+        xsync<64>();
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(a[r], b[r]);
+        fft_regs<N, true>(v, t, my, tw);
+        float2 u[G::P];
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) {
+            const int m = q / G::RL + G::NPT * (q % G::RL);   // out_pos<N>(t, q) = t + T*m
+            const int k = t + G::T * m;
+            const float sc = (k == 0 || 2 * k == N) ? 1.0f : (2 * k < N ? 2.0f : 0.0f);
+            u[m] = cscale(v[q], sc);
+        }
+        fft_regs<N, false>(u, t, my, tw);
+        // outputs as k_hilbert_pair (row 2 sl: (a, w.y - b), row 2 sl + 1: (b, a - w.x)),
+        // staged in two passes -- the wave's even rows, then its odd rows (WS rows x N
+        // complex, padded 1 per 16 in the area) -- and stored as 16 B per lane, row
+        // segments of N complex
+        float2* wc = reinterpret_cast<float2*>(wa);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            xsync<64>();
+#pragma unroll
+            for (int q = 0; q < G::P; ++q) {
+                const int m = q / G::RL + G::NPT * (q % G::RL);
+                const int k = t + G::T * m;
+                const float2 w = cscale(u[q], inv);
+                wc[G::pad(sl * N + k)] = h == 0 ? make_float2(a[m], w.y - b[m]) : make_float2(b[m], a[m] - w.x);
+            }
+            xsync<64>();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int e = i * 128 + 2 * lane;        // complex index among the WS rows
+                const int row = e / N, col = e - row * N;   // N >= 16: e, e + 1 in one row
+                const long long gr = r0 + 2 * row + h;      // its row of the batch
+                if (gr < batch) {
+                    const float2 c0 = wc[G::pad(e)], c1 = wc[G::pad(e + 1)];
+                    __builtin_nontemporal_store(vf4_t{c0.x, c0.y, c1.x, c1.y},
+                                                reinterpret_cast<vf4_t*>(z + gr * N + col));
+                }
+            }
+        }
+        xsync<64>();
+    }
+}
+
 bool hilbert_fused_supported(long long n) { return n >= 2 && n <= 8192 && (n & (n - 1)) == 0; }
 
 hipError_t launch_hilbert_fused(long long n, const float* x, float2* z, long long batch, hipStream_t s) {
     if (batch <= 0) return hipSuccess;
+    // 16..128 points: the staged kernel (knob HIL_SMALL = 0 keeps k_hilbert_pair, A/B)
+    if (n >= 16 && n <= 128 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)z & 15) == 0 && knob(KNOB_HIL_SMALL, 1) == 1) {
+#define VVH_HILS(NN)                                                                                          \
+        case NN: {                                                                                            \
+            const float2* tab = twiddle_table(NN);                                                            \
+            const float2* pas = pass_twiddles(NN);                                                            \
+            if (!tab || !pas) return hipErrorOutOfMemory;                                                     \
+            constexpr int F = 256 / Geo<NN>::T;                                                               \
+            const long long need = ((batch + 1) / 2 + F - 1) / F;                                             \
+            const int grid = (int)(need < (1LL << 30) ? need : (1LL << 30));                                  \
+            hipLaunchKernelGGL((k_hilbert_small<NN>), dim3(grid), dim3(256), 0, s, x, z, batch, pas, tab);    \
+            return hipGetLastError();                                                                         \
+        }
+        switch (n) {
+            VVH_HILS(16) VVH_HILS(32) VVH_HILS(64) VVH_HILS(128)
+            default: break;
+        }
+#undef VVH_HILS
+    }
 #define VVH_HIL(NN)                                                                                         \
     case NN: {                                                                                              \
         const float2* tab = twiddle_table(NN);                                                              \
