@@ -52,7 +52,7 @@ def test_c2c_one_transform_in_place():
     assert torch.equal(y.view(torch.int64), ref.view(torch.int64))
 
 
-@pytest.mark.parametrize("n", [256, 1024, 4096])
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 1024, 4096])
 @pytest.mark.parametrize("kind", ["r2c", "c2r"])
 def test_real_grid_shapes_bit_identical(n, kind):
     """R2C / C2R (fft_kiss.c:120-174 semantics): C2R of n <= 1024 launches one
@@ -68,11 +68,11 @@ def test_real_grid_shapes_bit_identical(n, kind):
                           torch.rand(batch, h, device="cuda", generator=g) - 0.5)
         p = vv.FftPlan(n, vv.C2R, vv.BWD, batch=batch)
     ref = p(x).clone()
-    for v in (0, 1):
-        with vv.knobs(REAL_TPW=v):
+    for kn in ({"REAL_TPW": 0}, {"REAL_TPW": 1}, {"REAL_SMALL": 0}):   # (C2R of 32..128: staged by default)
+        with vv.knobs(**kn):
             got = p(x).clone()
         assert torch.equal(got.view(torch.int32) if got.dtype == torch.float32 else got.view(torch.int64),
-                           ref.view(torch.int32) if ref.dtype == torch.float32 else ref.view(torch.int64)), v
+                           ref.view(torch.int32) if ref.dtype == torch.float32 else ref.view(torch.int64)), kn
     xn = x.cpu().numpy().astype(np.complex128 if kind == "c2r" else np.float64)
     want = np.fft.rfft(xn, axis=1) if kind == "r2c" else np.fft.irfft(xn, n=n, axis=1)
     err = np.abs(ref.cpu().numpy() - want).max() / np.abs(want).max()

@@ -388,6 +388,72 @@ static hipError_t run_r2c(const float* in, float2* out, long long batch, long lo
     return hipGetLastError();
 }
 
+// C2R of 32..128 real points (M = 16..64) with dense rows: k_c2r's arithmetic,
+// each wave's 64 / T rows of M + 1 complex values loaded as 8 B per lane
+// (coalesced) into its LDS area and read from there by the split step, and its
+// real outputs (64 / T rows x 2M floats = 1024 float2) staged back (padded 1 per
+// 16) and stored as 16 B per lane.  A wave-uniform loop.
+template <int M>
+__global__ void __launch_bounds__(256, 4)
+k_c2r_small(const float2* __restrict__ in, float* __restrict__ out, long long batch, const float2* gpass,
+            const float2* gtabM, const float2* gtab2M, float scale) {
+    using G = Geo<M>;
+    static_assert(G::P == 16 && G::T <= 4, "M = 16..64");
+    constexpr int F = 256 / G::T, WS = 64 / G::T, WA = WS * G::LDS;   // float2 per wave area
+    static_assert(WS * (M + 1) <= WA && 1024 + 64 <= WA, "the wave area holds the rows and the outputs");
+    __shared__ __attribute__((aligned(16))) float2 lds[F * G::LDS];
+    __shared__ float2 ltab[TwLayout<M>::ENTRIES];
+    __shared__ float2 lpost[PostLayout<M>::ENTRIES];
+    stage_twiddles<M, 256>(ltab, gpass, gtabM);
+    stage_post<M, 256>(lpost, gtab2M);
+    __syncthreads();
+    const TwTab<M> tw{ltab};
+    const PostTab<M> pw{lpost};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T, wv = lt >> 6, lane = lt & 63, sl = slot - wv * WS;
+    float2* my = lds + slot * G::LDS;
+    float2* wa = lds + wv * WA;
+    for (long long fw = (long long)blockIdx.x * F + (long long)wv * WS; fw < batch; fw += (long long)gridDim.x * F) {
+        const long long nr = batch - fw < WS ? batch - fw : WS;
+        const int nin = (int)nr * (M + 1), nout = (int)nr * M;   // valid input / output float2
+#pragma unroll
+        for (int i = 0; i * 64 < WS * (M + 1); ++i) {
+            const int e = i * 64 + lane;
+            if (e < WS * (M + 1)) wa[e] = e < nin ? in[fw * (M + 1) + e] : make_float2(0.0f, 0.0f);
+        }
+        xsync<64>();
+        const float2* row = wa + sl * (M + 1);
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            const int k = t + r * G::T;
+            float2 A = row[k], B;
+            if (k == 0) {   // imag of DC and Nyquist ignored (the fft_kiss.c:158-171 result)
+                A.y = 0.0f;
+                B = make_float2(row[M].x, 0.0f);
+            } else {
+                B = row[M - k];
+            }
+            v[r] = split_inv(A, B, pw(k));
+        }
+        xsync<64>();   // the FFT's exchanges reuse the area
+        fft_regs<M, false>(v, t, my, tw);
+        xsync<64>();
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) wa[G::pad(sl * M + out_pos<M>(t, q))] = cscale(v[q], scale);
+        xsync<64>();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = i * 128 + 2 * lane;   // float2 index among the wave's outputs
+            if (e < nout) {
+                const float2 c0 = wa[G::pad(e)], c1 = wa[G::pad(e + 1)];
+                __builtin_nontemporal_store(vf4_t{c0.x, c0.y, c1.x, c1.y},
+                                            reinterpret_cast<vf4_t*>(out + 2 * (fw * M + e)));
+            }
+        }
+        xsync<64>();
+    }
+}
+
 template <int M>
 static hipError_t run_c2r(const float2* in, float* out, long long batch, long long in_dist,
                           long long out_dist, hipStream_t s) {
@@ -405,6 +471,16 @@ static hipError_t run_c2r(const float2* in, float* out, long long batch, long lo
     // REAL_TPW = 0 / 1 forces the persistent / one-per-slot grid (A/B)
     if (knob(KNOB_REAL_TPW, M <= 512 ? 1 : 0) == 1) grid = (int)(need < (1LL << 30) ? need : (1LL << 30));
     if (grid < 1) return hipSuccess;
+    if constexpr (M >= 16 && M <= 64) {
+        // 32..128 real points, dense rows: the staged kernel (knob REAL_SMALL = 0 keeps k_c2r, A/B)
+        if (in_dist == M + 1 && out_dist == 2 * M && ((uintptr_t)out & 15) == 0 && knob(KNOB_REAL_SMALL, 1) == 1) {
+            constexpr int FS = 256 / Geo<M>::T;
+            const long long ns = (batch + FS - 1) / FS;
+            hipLaunchKernelGGL(k_c2r_small<M>, dim3((unsigned)(ns < (1LL << 30) ? ns : (1LL << 30))), dim3(256), 0, s,
+                               in, out, batch, pM, tM, t2M, 1.0f / (float)M);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(k_c2r<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pM, tM, t2M,
                        1.0f / (float)M);
     return hipGetLastError();
