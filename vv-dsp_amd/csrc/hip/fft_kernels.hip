@@ -365,6 +365,78 @@ k_c2r(const float2* in, float* out, long long batch, long long in_dist, long lon
     }
 }
 
+// R2C of 32..128 real points (M = 16..64) with dense rows: the mirror of
+// k_c2r_small -- each wave's 64 / T rows (1024 float2) loaded as 16 B per lane
+// through its LDS area (padded 1 per 16), the FFT's bins back through the area
+// for the split step's mirror, and the M + 1 bins per row staged and stored as
+// 8 B per lane, coalesced.  A wave-uniform loop.
+template <int M>
+__global__ void __launch_bounds__(256, 4)
+k_r2c_small(const float* __restrict__ in, float2* __restrict__ out, long long batch, const float2* gpass,
+            const float2* gtabM, const float2* gtab2M) {
+    using G = Geo<M>;
+    static_assert(G::P == 16 && G::T <= 4, "M = 16..64");
+    constexpr int F = 256 / G::T, WS = 64 / G::T, WA = WS * G::LDS;   // float2 per wave area
+    static_assert(WS * (M + 1) <= WA && 1024 + 64 <= WA, "the wave area holds the rows and the bins");
+    __shared__ __attribute__((aligned(16))) float2 lds[F * G::LDS];
+    __shared__ float2 ltab[TwLayout<M>::ENTRIES];
+    __shared__ float2 lpost[PostLayout<M>::ENTRIES];
+    stage_twiddles<M, 256>(ltab, gpass, gtabM);
+    stage_post<M, 256>(lpost, gtab2M);
+    __syncthreads();
+    const TwTab<M> tw{ltab};
+    const PostTab<M> pw{lpost};
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T, wv = lt >> 6, lane = lt & 63, sl = slot - wv * WS;
+    float2* my = lds + slot * G::LDS;
+    float2* wa = lds + wv * WA;
+    for (long long fw = (long long)blockIdx.x * F + (long long)wv * WS; fw < batch; fw += (long long)gridDim.x * F) {
+        const long long nr = batch - fw < WS ? batch - fw : WS;
+        const int nin = (int)nr * M, nout = (int)nr * (M + 1);   // valid input / output float2
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int e = i * 128 + 2 * lane;
+            const vf4_t q = e < nin ? __builtin_nontemporal_load(reinterpret_cast<const vf4_t*>(in + 2 * (fw * M + e)))
+                                    : vf4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            wa[G::pad(e)] = make_float2(q[0], q[1]);
+            wa[G::pad(e + 1)] = make_float2(q[2], q[3]);
+        }
+        xsync<64>();
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = wa[G::pad(sl * M + t + r * G::T)];
+        xsync<64>();   // the FFT's exchanges reuse the area
+        fft_regs<M, true>(v, t, my, tw);
+        xsync<64>();
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) wa[G::pad(sl * M + out_pos<M>(t, q))] = v[q];
+        xsync<64>();
+        float2 o[G::P];
+        float2 onyq = make_float2(0.0f, 0.0f);
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) {
+            const int k = t + r * G::T;
+            const float2 A = wa[G::pad(sl * M + k)];
+            if (k == 0) {
+                o[r] = make_float2(A.x + A.y, 0.0f);
+                onyq = make_float2(A.x - A.y, 0.0f);
+            } else {
+                o[r] = split_fwd(A, cconj(wa[G::pad(sl * M + M - k)]), pw(k));
+            }
+        }
+        xsync<64>();
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) wa[sl * (M + 1) + t + r * G::T] = o[r];
+        if (t == 0) wa[sl * (M + 1) + M] = onyq;
+        xsync<64>();
+#pragma unroll
+        for (int i = 0; i * 64 < WS * (M + 1); ++i) {
+            const int e = i * 64 + lane;
+            if (e < nout) st_nt(wa[e], out + fw * (M + 1) + e);
+        }
+        xsync<64>();
+    }
+}
+
 template <int M>
 static hipError_t run_r2c(const float* in, float2* out, long long batch, long long in_dist,
                           long long out_dist, hipStream_t s) {
@@ -384,6 +456,16 @@ static hipError_t run_r2c(const float* in, float2* out, long long batch, long lo
     // at 256 points, 9.8 % at 4096, equal at 1024: profiles/r05_ab2_real_grid.jsonl)
     if (knob(KNOB_REAL_TPW, 0) == 1) grid = (int)(need < (1LL << 30) ? need : (1LL << 30));
     if (grid < 1) return hipSuccess;
+    if constexpr (M >= 16 && M <= 64) {
+        // 32..128 real points, dense rows: the staged kernel on knob R2C_SMALL = 1 (A/B)
+        if (in_dist == 2 * M && out_dist == M + 1 && ((uintptr_t)in & 15) == 0 && knob(KNOB_R2C_SMALL, 0) == 1) {
+            constexpr int FS = 256 / Geo<M>::T;
+            const long long ns = (batch + FS - 1) / FS;
+            hipLaunchKernelGGL(k_r2c_small<M>, dim3((unsigned)(ns < (1LL << 30) ? ns : (1LL << 30))), dim3(256), 0, s,
+                               in, out, batch, pM, tM, t2M);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL(k_r2c<M>, dim3(grid), dim3(WG), 0, s, in, out, batch, in_dist, out_dist, pM, tM, t2M);
     return hipGetLastError();
 }
