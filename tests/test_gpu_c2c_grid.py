@@ -68,8 +68,8 @@ def test_real_grid_shapes_bit_identical(n, kind):
                           torch.rand(batch, h, device="cuda", generator=g) - 0.5)
         p = vv.FftPlan(n, vv.C2R, vv.BWD, batch=batch)
     ref = p(x).clone()
-    # (C2R of 32..128: staged by default; R2C_SMALL = 1: the staged R2C kernel)
-    for kn in ({"REAL_TPW": 0}, {"REAL_TPW": 1}, {"REAL_SMALL": 0}, {"R2C_SMALL": 1}):
+    # (R2C / C2R of 32..128: staged by default; knobs R2C_SMALL / REAL_SMALL = 0 the strided kernels)
+    for kn in ({"REAL_TPW": 0}, {"REAL_TPW": 1}, {"REAL_SMALL": 0}, {"R2C_SMALL": 0}):
         with vv.knobs(**kn):
             got = p(x).clone()
         assert torch.equal(got.view(torch.int32) if got.dtype == torch.float32 else got.view(torch.int64),

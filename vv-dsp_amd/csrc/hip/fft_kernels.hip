@@ -457,8 +457,10 @@ static hipError_t run_r2c(const float* in, float2* out, long long batch, long lo
     if (knob(KNOB_REAL_TPW, 0) == 1) grid = (int)(need < (1LL << 30) ? need : (1LL << 30));
     if (grid < 1) return hipSuccess;
     if constexpr (M >= 16 && M <= 64) {
-        // 32..128 real points, dense rows: the staged kernel on knob R2C_SMALL = 1 (A/B)
-        if (in_dist == 2 * M && out_dist == M + 1 && ((uintptr_t)in & 15) == 0 && knob(KNOB_R2C_SMALL, 0) == 1) {
+        // 32..128 real points, dense rows: the staged kernel -- 0.404 / 0.479 / 0.285 ->
+        // 0.198 / 0.215 / 0.221 ms for 2^27 points, bit-identical
+        // (profiles/r05_ab2_r2c_small.jsonl); knob R2C_SMALL = 0 keeps k_r2c (A/B)
+        if (in_dist == 2 * M && out_dist == M + 1 && ((uintptr_t)in & 15) == 0 && knob(KNOB_R2C_SMALL, 1) == 1) {
             constexpr int FS = 256 / Geo<M>::T;
             const long long ns = (batch + FS - 1) / FS;
             hipLaunchKernelGGL(k_r2c_small<M>, dim3((unsigned)(ns < (1LL << 30) ? ns : (1LL << 30))), dim3(256), 0, s,
