@@ -185,7 +185,8 @@ static hipError_t run_c2c(const float2* in, float2* out, long long batch, long l
     // G::T < 16): 32 / 64 / 128 points 0.650 / 0.332 / 0.230 -> 0.177 ms for 2^26
     // points (0.21 / 0.40 / 0.58 -> 0.76; profiles/r05_ab2_c2c_small.jsonl), bit-identical;
     // knob C2C_SMALL = 0 keeps the persistent grid (A/B)
-    const bool small = N >= 16 && N <= 128 && in_dist == N && out_dist == N && knob(KNOB_C2C_SMALL, 1) == 1;
+    const bool small = N >= 16 && N <= 128 && in_dist == N && out_dist == N && ((uintptr_t)in & 15) == 0 &&
+                       ((uintptr_t)out & 15) == 0 && knob(KNOB_C2C_SMALL, 1) == 1;
     const long long tpw = knob(KNOB_C2C_TPW, (N >= 256 && N <= 4096) || small ? 1 : -1);
     long long need = (batch + F - 1) / F, cap = grid_cap;
     if (tpw > 0) {
