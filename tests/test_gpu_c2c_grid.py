@@ -104,3 +104,16 @@ def test_mixed_register_grid_bit_identical(n, kind):
     want = np.fft.fft(xn, axis=1) if kind == "c2c" else np.fft.rfft(xn, axis=1)
     err = np.abs(ref.cpu().numpy() - want).max() / np.abs(want).max()
     assert err < 2e-5, err
+
+
+@pytest.mark.parametrize("n", [16, 64, 128])
+def test_c2c_small_rows_unaligned_buffer(n):
+    """A batch starting 8 B past a 16 B boundary takes the strided kernel (the
+    staged one needs 16 B aligned buffers): the same values."""
+    batch = 333
+    flat = _x(1, batch * n + 2, n).view(-1)
+    x = flat[1:1 + batch * n].view(batch, n)      # 8 B aligned, not 16
+    p = vv.FftPlan(n, vv.C2C, vv.FWD, batch=batch)
+    got = p(x).clone()
+    ref = p(x.clone()).clone()                     # a fresh (aligned) copy
+    assert torch.equal(got.view(torch.int64), ref.view(torch.int64))
