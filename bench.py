@@ -767,6 +767,8 @@ def dist_gather_leg(d, slots, root_slot, full, total_ch, nfr, compute_s, frames_
         if full is not None and len(slots) > 1:   # one process holds every rank's rows: check them
             same = True
             for x in slots:
+                if not x["cnt"]:      # fewer channels than ranks: this rank holds no rows
+                    continue
                 for c in sorted({0, x["cnt"] // 2, x["cnt"] - 1}):
                     for f in (0, 12345, nfr - 1):
                         a = full[x["lo"] + c, f].cpu()

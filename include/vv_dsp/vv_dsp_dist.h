@@ -84,8 +84,12 @@ VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_stft(vv_dsp_dist* d, vv_dsp_stft* h, 
  * rank sends bins 0..fft_size/2 only and the root expands them
  * (vv_dsp_spectrogram_pack/unpack_half_device): the same rows for half the
  * xGMI bytes.  Stream-ordered: returns once everything is enqueued; the
- * sources must be complete in stream order on streams[s].  Loopback contexts
- * run every copy on streams[root], after a device-side wait for each
+ * sources must be complete in stream order on streams[s].  half != 0 with an
+ * odd row_floats is INVALID_SIZE.  Loopback contexts run every copy on
+ * streams[root], after a device-side wait for each streams[s]; afterwards each
+ * streams[s] waits (device side) for streams[root], so work the caller enqueues
+ * on streams[s] after the call (e.g. the next step's rows into d_local[s]) runs
+ * after the gather has read d_local[s] -- as on the RCCL path, whose sends run on
  * streams[s]. */
 VV_DSP_NODISCARD vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* d_local,
                                                        size_t total_items, size_t rows_per_item, size_t row_floats,

@@ -216,7 +216,7 @@ CASES = {
     **{f"hilbert{n}": (lambda L, s, n=n: case_hilbert(L, s, n, (1 << 26) // n)) for n in (16, 32, 64, 128, 256, 1024, 2048, 4096, 8192)},
     **{f"dct{n}": (lambda L, s, n=n: case_dct(L, s, n, (1 << 27) // n)) for n in (16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192)},
     **{f"c2c{n}": (lambda L, s, n=n: case_c2c(L, s, n, (1 << 26) // n)) for n in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960, 1000, 2000, 3000, 4000)},
-    **{f"stft{n}": (lambda L, s, n=n: case_stft_nfft(L, s, n, n // 4)) for n in (64, 128, 256, 400, 480, 512, 960, 2048, 4096)},
+    **{f"stft{n}": (lambda L, s, n=n: case_stft_nfft(L, s, n, n // 4)) for n in (64, 128, 256, 400, 480, 512, 960, 1024, 2048, 4096)},
 }
 
 

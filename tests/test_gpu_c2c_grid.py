@@ -6,6 +6,8 @@ C2C_TPW = t > 0 t transforms per slot.  The transform arithmetic is the same in
 every shape, so outputs must be bit-identical (fft_kiss.c:27-74 semantics,
 pinned to f64 by test_gpu_parity.py).  Batches not a multiple of the 4 slots per
 workgroup, forward and backward (1/n), out-of-place and in-place."""
+import ctypes as C
+
 import numpy as np
 import pytest
 import torch
@@ -117,3 +119,61 @@ def test_c2c_small_rows_unaligned_buffer(n):
     got = p(x).clone()
     ref = p(x.clone()).clone()                     # a fresh (aligned) copy
     assert torch.equal(got.view(torch.int64), ref.view(torch.int64))
+
+
+def _off(shape, dtype, seed, floats=2):
+    """a random (batch, m) tensor whose data starts `floats` floats (8 B) past a
+    16 B boundary: a view into a larger allocation"""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    per = 2 if dtype == torch.complex64 else 1
+    numel = shape[0] * shape[1]
+    flat = torch.rand(numel * per + 8, device="cuda", generator=g) - 0.5
+    v = flat[floats:floats + numel * per]
+    return v.view(torch.complex64).view(shape) if per == 2 else v.view(shape)
+
+
+@pytest.mark.parametrize("n", [32, 64, 128])
+@pytest.mark.parametrize("kind", ["r2c", "c2r", "hilbert", "dct"])
+def test_small_real_rows_unaligned_buffers(n, kind):
+    """the staged 16..128-point kernels gate on 16 B alignment -- R2C
+    on its input, C2R on its output, Hilbert and DCT-II on both buffers.  Views
+    8 B past a 16 B boundary (input and output) take the other kernels: the same
+    values (bit for bit for R2C / C2R / Hilbert; DCT-II's staged kernel contracts
+    differently, so it is held to f64 and to the aligned result at 1e-6)."""
+    batch, h = 333, n // 2 + 1
+    assert _off((batch, n), torch.float32, 1).data_ptr() % 16 == 8
+    L = vv.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    if kind in ("r2c", "c2r"):
+        p = vv.FftPlan(n, vv.R2C if kind == "r2c" else vv.C2R, vv.FWD if kind == "r2c" else vv.BWD, batch=batch)
+        x = _off((batch, n), torch.float32, n) if kind == "r2c" else _off((batch, h), torch.complex64, n)
+        y = _off((batch, h), torch.complex64, 0) if kind == "r2c" else _off((batch, n), torch.float32, 0)
+        p(x, out=y)
+        ref = p(x.clone())
+    elif kind == "hilbert":
+        x = _off((batch, n), torch.float32, n)
+        y = _off((batch, n), torch.complex64, 0)
+        assert L.vv_dsp_hilbert_analytic_device(C.c_void_p(x.data_ptr()), n, batch, C.c_void_p(y.data_ptr()),
+                                                C.c_void_p(s)) == 0
+        ref = vv.hilbert(x.clone())
+    else:
+        x = _off((batch, n), torch.float32, n)
+        y = _off((batch, n), torch.float32, 0)
+        pl = C.c_void_p()
+        assert L.vv_dsp_dct_make_plan(n, 2, 1, C.byref(pl)) == 0
+        assert L.vv_dsp_dct_execute_device(pl, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), batch,
+                                           C.c_void_p(s)) == 0
+        L.vv_dsp_dct_destroy(pl)
+        ref = vv.dct(x.clone())
+    torch.cuda.synchronize()
+    if kind == "dct":
+        import scipy.fft
+        want = scipy.fft.dct(x.double().cpu().numpy(), type=2, axis=1) / 2
+        got = y.cpu().numpy()
+        assert np.abs(got - want).max() <= 5e-5 + 5e-5 * np.abs(want).max()
+        assert np.allclose(got, ref.cpu().numpy(), rtol=1e-6, atol=1e-6)
+    else:
+        a, b = y.contiguous(), ref
+        if a.dtype == torch.complex64:
+            a, b = a.view(torch.float32), b.view(torch.float32)
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))

@@ -153,6 +153,40 @@ def test_loopback_distinct_streams(job):
         assert torch.equal(out, ref)
 
 
+def test_loopback_slot_overwrite_after_gather(job):
+    """right after the gather returns, each slot overwrites its rows
+    on its OWN stream with no host synchronisation (the next step's rows); the
+    gather's reads on the root's stream must come first -- each slot stream
+    waits (device side) for the root's stream before the call returns."""
+    import torch
+    sig, st, ref = job
+    world, root = 3, 1
+    d = vv.Dist.loopback(world)
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    sl = _shards(NCH, world)
+    fr = st.frames(N)
+    for half in (False, True):
+        rows = [torch.full((c, fr, 1024), -3.0, device="cuda") for (_, c) in sl]
+        out = torch.full_like(ref, -1.0)
+        torch.cuda.synchronize()
+        d.stft(st, [sig[f] for f, _ in sl], N, NCH, N, rows, streams=streams)
+        d.gather_rows(rows, NCH, fr, 1024, out, root=root, half=half, streams=streams)
+        for s in range(world):
+            if s != root:
+                with torch.cuda.stream(streams[s]):
+                    rows[s].fill_(-7.0)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        assert all(bool((rows[s] == -7.0).all()) for s in range(world) if s != root)
+
+
+def test_half_rows_need_even_width(job):
+    d = vv.Dist.loopback(2)
+    sig, _, ref = job
+    with pytest.raises(vv.VvError):
+        d.gather_rows([ref, ref], 2, 1, 513, ref, root=0, half=True)
+
+
 def test_half_rows_need_two_bins(job):
     d = vv.Dist.loopback(2)
     sig, _, ref = job

@@ -42,8 +42,10 @@ def test_power_pitch_below_row_refused():
         st.power(_sig(1, 4096, 1), pitch=512)
 
 
-@pytest.mark.parametrize("pitch", [544, 520])
+@pytest.mark.parametrize("pitch", [544, 520, 1024, 70000])
 def test_mel_on_pitched_rows(pitch):
+    """520 / 544: the kernel reads the pitched rows; 1024 / 70000 (a pad past
+    64 floats; 70000 floats would not fit a CU's LDS): packed by a 2-D copy first"""
     import torch
     st = vv.Stft(1024, 256)
     mf = vv.Mfcc(1024, 40, 13, 48000.0, 20.0, 20000.0, lifter=22.0)

@@ -1496,11 +1496,23 @@ int vvhip_mel_pitched_device(vvhip_mel* m, const float* d_in, size_t frames, siz
     if (kind < 0 || kind > 2) return fail(ST_RANGE, "mel output kind");
     if ((kind != 2 && m->nbins == 0) || (kind != 0 && m->n_coeffs == 0)) return fail(ST_RANGE, "mel plan lacks tables");
     if (kind == 2) row_pitch = 0;
-    if (row_pitch != 0 && (row_pitch < (size_t)m->nbins || row_pitch > (1u << 20)))
-        return fail(ST_SIZE, "mel input row pitch below the row length");
+    if (row_pitch != 0 && row_pitch < (size_t)m->nbins) return fail(ST_SIZE, "mel input row pitch below the row length");
     if (frames == 0) return ST_OK;
+    const hipStream_t s = (hipStream_t)stream;
+    // the kernel stages whole pitched rows (pad included) through LDS; a pad
+    // past 64 floats would cost reads (and, far out, more LDS than a CU has):
+    // such rows are packed first by one 2-D copy, then run as packed rows
+    Scratch packed(s);
+    if (row_pitch > (size_t)m->nbins + 64) {
+        const size_t rb = sizeof(float) * (size_t)m->nbins;
+        HIPCHK(packed.alloc(rb * frames), ST_INTERNAL);
+        HIPCHK(hipMemcpy2DAsync(packed.p, rb, d_in, sizeof(float) * row_pitch, rb, frames, hipMemcpyDeviceToDevice, s),
+               ST_INTERNAL);
+        d_in = (const float*)packed.p;
+        row_pitch = 0;
+    }
     HIPCHK(launch_mel_grp(kind, d_in, (long long)frames, m->nbins, m->n_mels, m->n_coeffs, m->W, m->nnz, m->chunks,
-                          m->nc, m->cbeg, m->D, m->lift, m->eps, d_out, (hipStream_t)stream, (int)row_pitch),
+                          m->nc, m->cbeg, m->D, m->lift, m->eps, d_out, s, (int)row_pitch),
            ST_INTERNAL);
     return ST_OK;
 }

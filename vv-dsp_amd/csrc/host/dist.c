@@ -28,7 +28,9 @@
 #include <string.h>
 
 #define DIST_MAX_SLOTS 64
+#ifndef DIST_SLAB_BYTES /* a test-only build (tests/distsim) compiles a small slab in */
 #define DIST_SLAB_BYTES ((size_t)256 << 20)
+#endif
 
 /* ---- RCCL entry points, resolved at run time ---- */
 static struct {
@@ -243,6 +245,30 @@ vv_dsp_status vv_dsp_dist_comm_count(const vv_dsp_dist* d, int slot, int* count)
     return e == ncclSuccess ? VV_DSP_OK : nccl_fail("ncclCommCount", e);
 }
 
+/* ---- layout helpers (vv_dsp_amd.h) ---- */
+vv_dsp_status vv_dsp_shard_range(size_t total, size_t world, size_t rank, size_t* first, size_t* count) {
+    if (!first || !count) return VV_DSP_ERROR_NULL_POINTER;
+    if (world == 0 || rank >= world) return VV_DSP_ERROR_OUT_OF_RANGE;
+    const size_t base = total / world, rem = total % world;
+    *first = rank * base + (rank < rem ? rank : rem);
+    *count = base + (rank < rem ? 1 : 0);
+    return VV_DSP_OK;
+}
+
+vv_dsp_status vv_dsp_spectrogram_pack_half_device(const vv_dsp_real* d_rows, size_t rows, size_t fft_size,
+                                                  vv_dsp_real* d_half, void* stream) {
+    if (!d_rows || !d_half) return VV_DSP_ERROR_NULL_POINTER;
+    if (fft_size == 0) return VV_DSP_ERROR_INVALID_SIZE;
+    return (vv_dsp_status)vvhip_rows_half_device(d_rows, d_half, rows, fft_size, 0, stream);
+}
+
+vv_dsp_status vv_dsp_spectrogram_unpack_half_device(const vv_dsp_real* d_half, size_t rows, size_t fft_size,
+                                                    vv_dsp_real* d_rows, void* stream) {
+    if (!d_half || !d_rows) return VV_DSP_ERROR_NULL_POINTER;
+    if (fft_size == 0) return VV_DSP_ERROR_INVALID_SIZE;
+    return (vv_dsp_status)vvhip_rows_half_device(d_half, d_rows, rows, fft_size, 1, stream);
+}
+
 /* ---- helpers ---- */
 static size_t shard_first(size_t total, int world, int r) {
     size_t first = 0, count = 0;
@@ -371,7 +397,12 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
                                       int root, void* const* streams) {
     if (!d || !d_local || !streams) return VV_DSP_ERROR_NULL_POINTER;
     if (row_floats == 0 || rows_per_item == 0) return VV_DSP_ERROR_INVALID_SIZE;
-    if (half && row_floats < 2) return VV_DSP_ERROR_INVALID_SIZE;
+    /* half rows: bins 0..row_floats/2 of an even-length mirror-symmetric row
+     * (an odd width is a power row or some other non-mirror row: refused) */
+    if (half && (row_floats < 2 || row_floats % 2 != 0)) {
+        vvhip_set_error("dist gather: half rows need an even row_floats (mirror-symmetric fft_size-bin rows)");
+        return VV_DSP_ERROR_INVALID_SIZE;
+    }
     if (root < 0 || root >= d->world) return VV_DSP_ERROR_OUT_OF_RANGE;
     if (!d->loopback && !rccl_ready()) return VV_DSP_ERROR_UNSUPPORTED;
     vv_dsp_status st = check_streams(d, streams);
@@ -515,6 +546,12 @@ vv_dsp_status vv_dsp_dist_gather_rows(vv_dsp_dist* d, const vv_dsp_real* const* 
                 st = dev_leave(&g, st);
             }
     }
+    /* loopback: every read of d_local[s] ran on the root's stream, so each slot
+     * stream now waits for it -- the caller may overwrite d_local[s] on
+     * streams[s] right away, as on the RCCL path where the send runs on streams[s] */
+    if (d->loopback && st == VV_DSP_OK)
+        for (int s = 0; s < d->nslots && st == VV_DSP_OK; ++s)
+            if (s != rs && vvhip_stream_wait(streams[s], rstream) != 0) st = VV_DSP_ERROR_INTERNAL;
     /* stream-ordered frees: after the last use on each stream */
     for (int s = 0; s < d->nslots; ++s)
         if (pack[s]) {

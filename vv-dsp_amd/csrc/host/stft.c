@@ -174,15 +174,6 @@ vv_dsp_status vv_dsp_stft_get_sizes(const vv_dsp_stft* h, size_t* fft_size, size
     return VV_DSP_OK;
 }
 
-vv_dsp_status vv_dsp_shard_range(size_t total, size_t world, size_t rank, size_t* first, size_t* count) {
-    if (!first || !count) return VV_DSP_ERROR_NULL_POINTER;
-    if (world == 0 || rank >= world) return VV_DSP_ERROR_OUT_OF_RANGE;
-    const size_t base = total / world, rem = total % world;
-    *first = rank * base + (rank < rem ? rank : rem);
-    *count = base + (rank < rem ? 1 : 0);
-    return VV_DSP_OK;
-}
-
 vv_dsp_status vv_dsp_stft_channel_shard_device(vv_dsp_stft* h, int device, const vv_dsp_real* d_signal, size_t n,
                                                size_t count, size_t ch_stride, int out_kind, void* d_out,
                                                size_t out_ch_stride, void* stream, size_t* out_frames) {
@@ -198,18 +189,4 @@ vv_dsp_status vv_dsp_stft_channel_shard_device(vv_dsp_stft* h, int device, const
                                                       out_kind, stream);
     vv_dsp_status st2 = (vv_dsp_status)vvhip_set_device(prev);
     return st != VV_DSP_OK ? st : st2;
-}
-
-vv_dsp_status vv_dsp_spectrogram_pack_half_device(const vv_dsp_real* d_rows, size_t rows, size_t fft_size,
-                                                  vv_dsp_real* d_half, void* stream) {
-    if (!d_rows || !d_half) return VV_DSP_ERROR_NULL_POINTER;
-    if (fft_size == 0) return VV_DSP_ERROR_INVALID_SIZE;
-    return (vv_dsp_status)vvhip_rows_half_device(d_rows, d_half, rows, fft_size, 0, stream);
-}
-
-vv_dsp_status vv_dsp_spectrogram_unpack_half_device(const vv_dsp_real* d_half, size_t rows, size_t fft_size,
-                                                    vv_dsp_real* d_rows, void* stream) {
-    if (!d_half || !d_rows) return VV_DSP_ERROR_NULL_POINTER;
-    if (fft_size == 0) return VV_DSP_ERROR_INVALID_SIZE;
-    return (vv_dsp_status)vvhip_rows_half_device(d_half, d_rows, rows, fft_size, 1, stream);
 }
