@@ -149,6 +149,20 @@ def stft_config3(reps=50, burst=100):
     per = a.elapsed_time(b) / burst
     byts = n * 4 + NFFT * 4 + fr * NFFT * 4
     del sig, out
+    ceil = copy_ceiling(fr)
+    extra = {}
+    if ceil is not None:
+        cbyts = fr * HOP * 4 + fr * NFFT * 4
+        extra = {"copy_ceiling": {
+            "what": "the same job's bytes (1 KB in -> 4 KB out per frame) moved by a streaming copy with no FFT "
+                    "(scripts/membench.hip k_rwc, best of u in {1,2} x {703, 2812} workgroups), timed in this run "
+                    "exactly as the product: the box's ceiling for a 57.6 MB single launch",
+            "ms_avg": round(ceil["ms_avg"], 4), "ms_back_to_back": round(ceil["ms_back_to_back"], 4),
+            "frac": round(cbyts / (ceil["ms_avg"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_back_to_back": round(cbyts / (ceil["ms_back_to_back"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "shape": {"u": ceil["u"], "blocks": ceil["blocks"]}},
+            "frac_of_ceiling": round(ceil["ms_avg"] / avg, 4),
+            "frac_of_ceiling_back_to_back": round(ceil["ms_back_to_back"] / per, 4)}
     return {"workload": "config3: STFT 60 s mono @ 48 kHz, 1024 Hann, hop 256 (11,248 frames)",
             "bytes_per_call": byts, "ms_avg": round(avg, 4), "ms_min": round(best, 4),
             "timing": "ms_avg: an event pair around each single call (isolated); back_to_back: one event pair "
@@ -156,7 +170,50 @@ def stft_config3(reps=50, burst=100):
             "frames_per_s": round(fr / (avg * 1e-3), 1),
             "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             f"back_to_back_{burst}": {"ms_per_call": round(per, 4), "frames_per_s": round(fr / (per * 1e-3), 1),
-                                      "frac": round(byts / (per * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+                                      "frac": round(byts / (per * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            **extra}
+
+
+def _membench():
+    """scripts/libmembench.so (built by __graft_entry__.build(): `make -C vv-dsp_amd membench`): streaming
+    kernels with no FFT, the box's own ceiling for a job's bytes (measurement only, not the product)"""
+    path = os.path.join(ROOT, "scripts", "libmembench.so")
+    if not os.path.exists(path):
+        return None
+    mb = C.CDLL(path)
+    mb.membench_rwc.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong] + [C.c_int] * 5 + [C.c_void_p]
+    return mb
+
+
+def copy_ceiling(frames, reps=50, burst=100):
+    """Config 3's bytes (1 KB of new samples in, one 4 KB row out per frame) moved
+    by a pure streaming kernel with no FFT (membench k_rwc: one 1 KB -> 4 KB item
+    per wave step, u items in flight per wave), timed exactly as stft_config3 times
+    the product: the best of four launch shapes, single call and back to back."""
+    mb = _membench()
+    if mb is None:
+        return None
+    a = torch.rand(frames * HOP, device="cuda")
+    b = torch.empty(frames * NFFT, device="cuda")
+    s = torch.cuda.current_stream()
+    best = None
+    for u in (1, 2):
+        for blocks in (703, 2812):
+            fn = (lambda u=u, blocks=blocks: mb.membench_rwc(a.data_ptr(), b.data_ptr(), frames, 4, u, 1, 1, blocks,
+                                                             s.cuda_stream))
+            assert fn() == 0
+            _, mn, avg = timed_launches(fn, reps)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(burst):
+                fn()
+            e1.record(s)
+            torch.cuda.synchronize()
+            b2b = e0.elapsed_time(e1) / burst
+            if best is None or avg < best["ms_avg"]:
+                best = {"ms_avg": avg, "ms_back_to_back": b2b, "u": u, "blocks": blocks}
+    del a, b
+    return best
 
 
 def fir_roofline(reps=50):
@@ -311,6 +368,27 @@ def cpu_baseline(threads=None, seconds=5.0, reps=3):
                       f"65536 x 1024 uniform[-0.5,0.5) batch, {reps} samples of 3 s: {cnt} transforms in {dt2:.2f} s"}
         del x, ys
 
+    # the reference's other STFT sizes (bench/bench_stft.c:165), 60 s mono per call, hop nfft/4
+    sigs = [np.random.default_rng(3 + i).uniform(-1, 1, n).astype(np.float32) for i in range(threads)]
+    sizes = {}
+    for nfft in STFT_SIZES:
+        hop = nfft // 4
+        per = 1 if n < nfft else 1 + (n - nfft + hop) // hop
+
+        def size_work(i, t_end, nfft=nfft, hop=hop, per=per):
+            done = 0
+            while time.perf_counter() < t_end:
+                ref.spectrogram(sigs[i], nfft, hop)
+                done += per
+            return done
+
+        r, cnt, dts = _repeats(threads, 2.0, size_work, 1)
+        sizes[str(nfft)] = {"value": round(r[0], 1), "unit": "frames/s", "hop": hop,
+                            "sample": f"{threads} threads x vv_dsp_stft_spectrogram(60 s mono, nfft {nfft}, hop {hop}) "
+                                      f"back to back for 2 s: {cnt} frames in {dts:.2f} s"}
+    res["stft_sizes"] = sizes
+    del sigs
+
     h = np.zeros(257, np.float32)          # config 4
     ref.lib.vv_dsp_fir_design_lowpass(h.ctypes.data_as(C.POINTER(C.c_float)), 257, 0.25, 2)
     ns = 1 << 22
@@ -403,10 +481,46 @@ def shard_leg(ch=CH_SHARD, steps=20, warm=10):
             "check_row_vs_numpy_f64": bool(ok)}
 
 
-def hann64():
+def hann64(nfft=NFFT):
     """The reference's symmetric Hann (window.c:25-36, float arithmetic) in f64."""
-    return np.array([0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(NFFT - 1) * np.float32(i))
-                     for i in range(NFFT)], np.float64)
+    return np.array([0.5 - 0.5 * np.cos(np.float32(2 * np.pi) / np.float32(nfft - 1) * np.float32(i))
+                     for i in range(nfft)], np.float64)
+
+
+STFT_SIZES = (256, 512, 2048, 4096)   # the reference's own STFT sizes besides 1024 (bench/bench_stft.c:165)
+
+
+def stft_sizes_leg(ch=CH_SHARD, reps=20, sizes=STFT_SIZES):
+    """The reference's benchmarked STFT sizes (bench/bench_stft.c:163-227, docs/profiles/stft_profile.json:17-46:
+    nfft 256 / 512 / 2048 / 4096 at hop nfft/4) on config 5's per-GPU shard (32 ch x 10 min @ 48 kHz),
+    magnitude rows [ch][frame][nfft]: frames/s, HBM fraction and one row per size against NumPy f64."""
+    try:
+        sig = torch.empty(ch, SAMPLES, device="cuda")
+        for c in range(ch):
+            g = torch.Generator(device="cuda").manual_seed(c)
+            sig[c].uniform_(-1.0, 1.0, generator=g)
+    except torch.OutOfMemoryError as e:
+        return {"error": repr(e)[:200]}
+    res = {"workload": f"{ch} ch x 10 min @ 48 kHz per size, Hann, hop nfft/4, magnitude rows (stft.c:112-144)"}
+    for nfft in sizes:
+        hop = nfft // 4
+        nfr = 1 if SAMPLES < nfft else 1 + (SAMPLES - nfft + hop) // hop
+        out = torch.empty(ch, nfr, nfft, device="cuda")
+        st = vv.Stft(nfft, hop, vv.WIN_HANN)
+        avg, best, iso = timed_launches(lambda: st.spectrogram(sig, out=out), reps, warm=10)
+        byts = ch * SAMPLES * 4 + ch * nfr * nfft * 4 + nfft * 4
+        fr = nfr // 3
+        x0 = sig[ch - 1, fr * hop: fr * hop + nfft].double().cpu().numpy()
+        ok = np.allclose(out[ch - 1, fr].cpu().numpy(), np.abs(np.fft.fft(x0 * hann64(nfft))), rtol=5e-5, atol=5e-5)
+        res[str(nfft)] = {"hop": hop, "frames": ch * nfr, "ms_avg": round(avg, 4), "ms_min": round(best, 4),
+                          "frames_per_s": round(ch * nfr / (avg * 1e-3), 1), "bytes_per_launch": byts,
+                          "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "check_row_vs_numpy_f64": bool(ok)}
+        del out, st
+        torch.cuda.empty_cache()
+    del sig
+    torch.cuda.empty_cache()
+    return res
 
 
 def parse_args():
@@ -421,9 +535,10 @@ def parse_args():
                     help="channels of the whole job (config 5: 256), split over the ranks (strong scaling)")
     ap.add_argument("--no-extras", action="store_true", help="skip config 2/3/4, shard and CPU baseline legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
-    ap.add_argument("--legs", default="c2c,fir,config3,shard",
+    ap.add_argument("--legs", default="c2c,fir,config3,shard,sizes",
                     help="extra GPU legs: c2c (config 2), fir (config 4), config3, shard (config 5's 32-channel "
-                         "per-GPU shard of the N = 8 run); profiling runs leave config3 and shard out so the "
+                         "per-GPU shard of the N = 8 run), sizes (the reference's STFT sizes 256/512/2048/4096 on "
+                         "that shard); profiling runs leave config3, shard and sizes out so the "
                          "headline kernel's PMC average covers the headline launches only")
     ap.add_argument("--gather-bins", choices=["half", "full"], default="half",
                     help="gather bins 0..512 and expand on rank 0 (half, default) or all 1024 bins (full)")
@@ -574,6 +689,9 @@ def main_plain(args):
             torch.cuda.empty_cache()
         if "config3" in legs:
             res["stft_config3"] = stft_config3()
+            torch.cuda.empty_cache()
+        if "sizes" in legs:
+            res["stft_sizes"] = stft_sizes_leg()
             torch.cuda.empty_cache()
     if not args.no_extras and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline()

@@ -107,6 +107,22 @@ def case_stft_nfft(L, s, nfft, hop, nch=32, seconds=600, sr=48000):
         nch * n * 4 + nch * fr * nfft * 4, (lambda: out.clone())
 
 
+def case_stft_cpx(L, s, nfft, hop, nch=8, seconds=120, sr=48000):
+    """complex rows [ch][frame][nfft] (vv_dsp_stft_spectrum_device)"""
+    n = seconds * sr
+    fr = frames_of(n, nfft, hop)
+    sig, out = buf(("stftc", nfft, hop, nch, n), lambda: (torch.rand(nch, n, device="cuda") * 2 - 1,
+                                                          torch.empty(nch, fr, nfft, dtype=torch.complex64,
+                                                                      device="cuda")))
+    h = vp()
+    ok(L, L.vv_dsp_stft_create(C.byref(StftParams(nfft, hop, 1)), C.byref(h)), "stft create")
+    nf = sz()
+    f = L.vv_dsp_stft_spectrum_device
+    f.argtypes = [vp, vp, sz, sz, sz, vp, sz, vp, C.POINTER(sz)]
+    return (lambda: ok(L, f(h, sig.data_ptr(), n, nch, n, out.data_ptr(), fr * nfft, s, C.byref(nf)), "stftc")), \
+        nch * n * 4 + nch * fr * nfft * 8, (lambda: out.clone())
+
+
 def case_stft_rows(L, s, kind, nch, seconds):
     """kind mag / pow (packed 513-float rows) / pow544 (rows 544 floats apart;
     bytes counted as the 513 floats written)"""
@@ -217,6 +233,7 @@ CASES = {
     **{f"dct{n}": (lambda L, s, n=n: case_dct(L, s, n, (1 << 27) // n)) for n in (16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192)},
     **{f"c2c{n}": (lambda L, s, n=n: case_c2c(L, s, n, (1 << 26) // n)) for n in (320, 400, 441, 480, 600, 640, 720, 800, 900, 960, 1000, 2000, 3000, 4000)},
     **{f"stft{n}": (lambda L, s, n=n: case_stft_nfft(L, s, n, n // 4)) for n in (64, 128, 256, 400, 480, 512, 960, 1024, 2048, 4096)},
+    **{f"stftc{n}": (lambda L, s, n=n: case_stft_cpx(L, s, n, n // 4)) for n in (256, 512, 1024, 2048, 4096)},
 }
 
 

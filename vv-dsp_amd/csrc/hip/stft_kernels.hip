@@ -931,8 +931,10 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
 // each thread reads Z[k], Z[N-k] for bins k = t + T j -- so both rows leave
 // as lane-contiguous, full-line stores.  Persistent XCD walk with the next
 // pair's samples loaded into registers while this pair is transformed.
+// N = 256: three waves per SIMD (168 VGPRs, no spills; two at the 172 it
+// takes unbounded)
 template <int N, int MODE>
-__global__ void __launch_bounds__(Wg<N>::value)
+__global__ void __launch_bounds__(Wg<N>::value, N == 256 ? 3 : 1)
 k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
                 long long hop, const float* win, void* out, long long out_ch_stride, long long row_pitch,
                 const float2* gpass, const float2* gtab) {
@@ -992,18 +994,36 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
         const long long rp = MODE == 2 ? row_pitch : ROW;   // power rows: row_pitch floats apart
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * rp) * ES;
         char* rowb = rowa + rp * ES;
+        // bins k = t + T j <= N/2 only: bin N - k of a real frame is the
+        // conjugate of bin k, bit for bit (pair_post with Z[k], Z[N-k] swapped
+        // gives conj(A), conj(B) exactly: the sums commute and negation is exact),
+        // so each post serves both bins -- half the posts and LDS reads
 #pragma unroll
-        for (int j = 0; j < G::P; ++j) {
+        for (int j = 0; j <= G::P / 2; ++j) {
             const int k = t + G::T * j;
-            if (MODE == 2 && k > N / 2) continue;
+            if (j == G::P / 2 && t != 0) continue;   // bin N/2 (its own mirror): thread 0
             float2 A, B;
             pair_post<MODE>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
+            const bool mir = MODE != 2 && k != 0 && k != N / 2;   // bin N - k is another bin
+            // bases at bins t and N - t: bin k = t + T j and N - k at -T j
             if constexpr (MODE == 1) {
-                st_nt(A, reinterpret_cast<float2*>(rowa) + k);
-                if (hb) st_nt(B, reinterpret_cast<float2*>(rowb) + k);
+                float2* ra = reinterpret_cast<float2*>(rowa) + t;
+                float2* rm = reinterpret_cast<float2*>(rowa) + (N - t);
+                st_nt(A, ra + G::T * j);
+                if (mir) st_nt(cconj(A), rm - G::T * j);
+                if (hb) {
+                    st_nt(B, ra + (rowb - rowa) / 8 + G::T * j);
+                    if (mir) st_nt(cconj(B), rm + (rowb - rowa) / 8 - G::T * j);
+                }
             } else {
-                __builtin_nontemporal_store(A.x, reinterpret_cast<float*>(rowa) + k);
-                if (hb) __builtin_nontemporal_store(B.x, reinterpret_cast<float*>(rowb) + k);
+                float* ra = reinterpret_cast<float*>(rowa) + t;
+                float* rm = reinterpret_cast<float*>(rowa) + (N - t);
+                __builtin_nontemporal_store(A.x, ra + G::T * j);
+                if (mir) __builtin_nontemporal_store(A.x, rm - G::T * j);
+                if (hb) {
+                    __builtin_nontemporal_store(B.x, ra + rp + G::T * j);
+                    if (mir) __builtin_nontemporal_store(B.x, rm + rp - G::T * j);
+                }
             }
         }
         xsync<G::T>();   // the next pair's FFT exchange reuses `my`
