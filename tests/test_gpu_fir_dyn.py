@@ -122,25 +122,3 @@ def test_fir_r32_strided_and_prefix(vdev, amd, orc):
     assert torch.equal(y[:, :n], ref)
     assert bool((y[:, n:] == -9.0).all())
 
-
-@pytest.mark.parametrize("nch,n", [(8, 1 << 24), (3, 5_000_001), (5, 1537), (7, 100_003), (2, 3000), (1, 700),
-                                   (4, 768 * 2 * 5 + 1), (9, 2_345_678), (1, 1 << 20)])
-@pytest.mark.parametrize("run", [1, 2, 3, 8])
-def test_fir_r32run_equals_r32(vdev, orc, nch, n, run):
-    """k_fir_r32run (each half-wave walks its own run of pairs, the block history
-    carried in registers; knob FIR_RUN = run: 1 one run per half-wave, L >= 2 runs
-    of L pairs) against
-    k_fir_r32 (the couple walk): the same transform arithmetic on the same
-    samples, so bit-identical -- runs crossing channels, edge pairs inside runs,
-    halves with no run, n below one block."""
-    import torch
-    h = orc.fir_design_lowpass(257, 0.25, 2)
-    plan = vdev.FirPlan(torch.from_numpy(h))
-    g = torch.Generator(device="cuda").manual_seed(nch * 131 + n % 977 + run)
-    x = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
-    with vv.knobs(FIR_RUN=0):   # the couple walk
-        ref = plan(x).clone()
-    with vv.knobs(FIR_RUN=run):
-        got = plan(x)
-    torch.cuda.synchronize()
-    assert torch.equal(got, ref)

@@ -342,6 +342,46 @@ struct TwLastReg {
     }
 };
 
+// The same for a MIRROR-PAIRED last pass with two butterflies per thread
+// (NPT = 2, e.g. N = 2048: T = 128, last radix 8): a thread's last-pass
+// butterflies are j0 = t (< NS/2) and j1 = NS - t (NS / 2 for t = 0, so in
+// [NS/2, NS)), the same for every transform.  Butterfly j0's RL - 1 twiddles
+// are loaded once into registers; butterfly j1's are read per transform from
+// the upper half of the last pass' table staged in LDS (`hi`: [r-1][j - NS/2]).
+// Either way the table's own values -- bit-identical to TwTab -- with half the
+// last pass' entries in LDS and RL - 1 twiddles in VGPRs.
+template <int N>
+struct TwLastRegP {
+    using G = Geo<N>;
+    static constexpr int LAST = G::NPASS - 1, RL = G::RL, NS = G::ns(LAST);
+    static constexpr int HI_ENTRIES = (RL - 1) * (NS / 2);
+    static_assert(G::NPT == 2 && G::NB == NS && G::T == NS / 2, "two mirror-paired last-pass butterflies per thread");
+    const float2* tab;   // LDS: pass-major entries of passes < LAST
+    const float2* hi;    // LDS: [r-1][j - NS/2], the last pass for j in [NS/2, NS)
+    float2 w[RL - 1];    // W^{t r} of the last pass, r = 1..RL-1
+    template <int p>
+    __device__ __forceinline__ float2 at(int j, int r, int i) const {
+        if constexpr (p == LAST) return (i & 1) ? hi[(r - 1) * (NS / 2) + (j - NS / 2)] : w[r - 1];
+        else return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
+    }
+    __device__ __forceinline__ void load(const float2* gpass, int t) {
+#pragma unroll
+        for (int r = 1; r < RL; ++r) w[r - 1] = gpass[G::tw_off(LAST) + (r - 1) * NS + t];
+        opaque();
+    }
+    // stage the table entries of the passes < LAST and the last pass' upper half
+    template <int NTHREADS>
+    __device__ __forceinline__ static void stage(float2* lds_tab, float2* lds_hi, const float2* gpass) {
+        for (int i = threadIdx.x; i < G::tw_off(LAST); i += NTHREADS) lds_tab[i] = gpass[i];
+        for (int i = threadIdx.x; i < HI_ENTRIES; i += NTHREADS)
+            lds_hi[i] = gpass[G::tw_off(LAST) + (i / (NS / 2)) * NS + NS / 2 + i % (NS / 2)];
+    }
+    __device__ __forceinline__ void opaque() {
+#pragma unroll
+        for (int r = 0; r < RL - 1; ++r) asm volatile("" : "+v"(w[r].x), "+v"(w[r].y));
+    }
+};
+
 // Stage the global table into LDS (all NTHREADS threads of the block).
 //   gpass : pass-major table for N (host: pass_twiddles(N)), used when !SPLIT
 //   gtab  : W_N^k, k < N (host: twiddle_table(N)), used when SPLIT

@@ -614,221 +614,6 @@ k_fir_r32(const float2* Hg, const float* x, float* y, long long nch, long long x
     }
 }
 
-// ------------------------------------------------------------------------
-// k_fir_r32run: k_fir_r32<true> (the 8 B pair layout) with each HALF-wave
-// walking its own run of consecutive pairs of the XCD group's share, so the
-// 256-sample history of a pair's block a (its rows 0..7) is the previous
-// pair's block b rows 24..31 -- still in this half's registers.  They are
-// carried across the iteration (8 VGPRs, raw 8 B pair layout) and only a run's
-// first pair (or the pair after a channel start or an edge pair) loads them.
-// k_fir_r32 re-reads every block's history: within a couple the two halves
-// fetch the same lines at once, across couples neighbouring waves do, and
-// whichever request misses L2 second fetches them from HBM again (read traffic
-// 1.068-1.073x the input, profiles/r05_final_pmc_summary.txt).  Here the input
-// is read once per run boundary (about 8.3 % / run extra) and each pair issues
-// 24 loads instead of 28.  Half h of wave w takes runs 2 (w + k nw) + h of its
-// group (nw waves per group); both halves step in lockstep, a half past the end
-// of its group's share computes a repeat of a valid pair and stores nothing.
-// run_len <= 0: one run per half-wave, the group's share split evenly (no
-// straggler round; the default), else runs of run_len pairs.
-// Edge pairs (span before sample 0 or past n) load through the prefix / zero
-// rule as in k_fir_r32 (the whole wave takes that branch when either half needs it).
-// ------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 2)
-k_fir_r32run(const float2* Hg, const float* x, float* y, long long nch, long long x_stride, long long y_stride,
-             long long ppc, const float2* tw1024, long long n, const float* prefix, long long lm1, long long qf,
-             long long ql, long long run_len) {
-    constexpr int N = 1024, LE = 256, LOUT = N - LE, F = 4;
-    __shared__ __attribute__((aligned(16))) float2 xch[F * 2 * R32_BUF];
-    __shared__ float2 lH[N / 2 + 1];
-    __shared__ float2 ltw[32 * 32];   // [r][m] = W_1024^(m r) (row 0 unused)
-    for (int i = threadIdx.x; i <= N / 2; i += 256) lH[i] = Hg[i];
-    for (int i = threadIdx.x; i < 32 * 32; i += 256) ltw[i] = tw1024[((i & 31) * (i >> 5)) & (N - 1)];
-    const int lt = threadIdx.x, slot = lt >> 6, lane = lt & 63, half = lane >> 5, m = lane & 31;
-    float2* buf = xch + (2 * slot + half) * R32_BUF;
-    const int mr = 2 * (m & 15) + (m >> 4);   // the lane's residue (8 B pair layout, r32_pairswap)
-    const float2* atwf = ltw + mr;
-    const float2* atw = ltw + m;
-    const float2* ahl = lH + m;
-    const float2* ahh = lH + 32 - m;
-    __syncthreads();
-    const long long pairs = nch * ppc;
-    // this XCD group's share of the pairs, cut into runs
-    const long long nb = gridDim.x, b = blockIdx.x, ng = nb < 8 ? nb : 8, grp = b % ng;
-    const long long nbg = (nb - grp + ng - 1) / ng;
-    long long lo, hi;
-    chunk_of(pairs, grp, ng, &lo, &hi);
-    lo = uni<64>(lo);
-    hi = uni<64>(hi);
-    const long long nw = nbg * F;                       // waves of the group
-    const long long RUN = uni<64>(run_len > 0 ? run_len : (hi - lo + 2 * nw - 1) / (2 * nw));
-    const long long nrun = RUN > 0 ? (hi - lo + RUN - 1) / RUN : 0;
-    long long rw = uni<64>((b / ng) * F + slot);        // this wave's run pair: runs 2 rw, 2 rw + 1
-    if (2 * rw >= nrun) return;                         // nothing for this wave (uniform; no barrier follows)
-    // per half: the current pair p (channel c, pair q of it), its run's end pe
-    long long p, pe, c, q;
-    auto start_run = [&](long long rwv) {
-        long long r = 2 * rwv + half;
-        if (r >= nrun) r = 2 * rwv;                     // no run for half 1: repeat half 0's, store nothing
-        p = lo + r * RUN;
-        pe = 2 * rwv + half < nrun ? (p + RUN < hi ? p + RUN : hi) : p;   // pe == p: nothing valid
-        c = p / ppc;
-        q = p - c * ppc;
-    };
-    start_run(rw);
-    long long i = 0;                                    // step within the run (uniform)
-    float xa[32], xb[32], cy[8];
-    auto is_edge = [&](long long qq) { return qq < qf || qq >= ql; };
-    auto load_bulk = [&](long long cc, long long qq, bool carry) {
-        const float2* a = reinterpret_cast<const float2*>(x + cc * x_stride + 2 * qq * LOUT - LE) + m;
-        const float2* bb = a + LOUT / 2;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {   // block a rows 0..7: the previous pair's block b rows 24..31
-            if (carry) {
-                xa[2 * k] = cy[2 * k];
-                xa[2 * k + 1] = cy[2 * k + 1];
-            } else {
-                const float2 u = ld_nt(a + 32 * k);
-                xa[2 * k] = u.x;
-                xa[2 * k + 1] = u.y;
-            }
-        }
-#pragma unroll
-        for (int k = 4; k < 16; ++k) {
-            const float2 u = ld_nt(a + 32 * k);
-            xa[2 * k] = u.x;
-            xa[2 * k + 1] = u.y;
-        }
-#pragma unroll
-        for (int k = 4; k < 16; ++k) {   // rows 0..7 of block b = rows 24..31 of block a
-            const float2 u = ld_nt(bb + 32 * k);
-            xb[2 * k] = u.x;
-            xb[2 * k + 1] = u.y;
-        }
-    };
-    auto load_edge = [&](long long cc, long long qq) {
-        const float* xs = x + cc * x_stride;
-        const float* pre = prefix ? prefix + cc * lm1 : nullptr;
-        float* sf = reinterpret_cast<float*>(buf);
-        const long long s0 = 2 * qq * LOUT - LE;
-#pragma unroll 1
-        for (int k = m; k < 2 * N; k += 32) {
-            const long long ii = s0 + (k < N ? k : k - N + LOUT);
-            float v = 0.0f;
-            if (ii < 0) {
-                if (pre && ii >= -lm1) v = pre[lm1 + ii];
-            } else if (ii < n) {
-                v = xs[ii];
-            }
-            sf[k] = v;
-        }
-        xsync<64>();
-#pragma unroll
-        for (int r = 0; r < 32; ++r) xa[r] = sf[mr + 32 * r];
-#pragma unroll
-        for (int r = 0; r < 32; ++r) xb[r] = sf[N + mr + 32 * r];
-        xsync<64>();
-    };
-    bool edge = __ballot(is_edge(q)) != 0;   // either half: the staged path
-    bool valid = p < pe;
-    if (!edge) load_bulk(c, q, false);
-    while (true) {
-        if (edge) {
-            load_edge(c, q);
-        } else {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) cy[r] = xb[24 + r];   // raw rows 24..31: the next pair's rows 0..7
-#pragma unroll
-            for (int k = 0; k < 16; ++k) r32_pairswap(xa[2 * k], xa[2 * k + 1]);
-#pragma unroll
-            for (int k = 4; k < 16; ++k) r32_pairswap(xb[2 * k], xb[2 * k + 1]);
-        }
-        float2 v[32];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const vf2_t A = {xa[2 * k], xa[2 * k + 1]};
-            const vf2_t B = k < 4 ? vf2_t{xa[24 + 2 * k], xa[25 + 2 * k]} : vf2_t{xb[2 * k], xb[2 * k + 1]};
-            v[2 * k] = upk(pk_pair<0>(A, B));
-            v[2 * k + 1] = upk(pk_pair<1>(A, B));
-        }
-        // the next step: the same run's next pair, or the next run pair of this wave
-        const long long cc0 = c, q0 = q;
-        const bool valid0 = valid, edge0 = edge;
-        bool more;
-        bool carry = false;
-        if (i + 1 < RUN && __ballot(p + 1 < pe) != 0) {   // either half continues its run
-            ++i;
-            ++p;
-            ++q;
-            if (q == ppc) {
-                q = 0;
-                ++c;
-            }
-            carry = !edge0 && q != 0;                      // same channel, the previous pair loaded in bulk
-            more = true;
-        } else {
-            i = 0;
-            rw += nw;
-            more = 2 * rw < nrun;
-            if (more) start_run(rw);
-        }
-        if (more) {
-            valid = p < pe;
-            edge = __ballot(is_edge(q)) != 0;
-            if (!edge) load_bulk(c, q, carry && !is_edge(q));
-        }
-        {
-            dft32<true>(v);
-            r32_twiddle<true>(v, atwf);
-            r32_transpose(v, buf, mr, m);
-            dft32<true>(v);
-            {
-                float2 h[16];
-                lds_rd64x16<0, 256>(ahl, h);
-#pragma unroll
-                for (int k2 = 0; k2 < 16; ++k2) v[k2] = cmul(v[k2], h[k2]);
-                lds_rd64x16<15 * 256, -256>(ahh, h);
-#pragma unroll
-                for (int k = 0; k < 16; ++k) v[16 + k] = cmulc(v[16 + k], h[k]);
-            }
-            dft32<false>(v);
-            r32_twiddle<false>(v, atw);
-            r32_transpose(v, buf, m, mr);
-            dft32<false>(v);
-        }
-        {
-            const long long j = 2 * q0;
-            if (!edge0) {
-                float2 oa[12], ob[12];
-#pragma unroll
-                for (int k = 0; k < 12; ++k) {
-                    oa[k] = upk(pk_pair<0>(pk(v[8 + 2 * k]), pk(v[9 + 2 * k])));
-                    ob[k] = upk(pk_pair<1>(pk(v[8 + 2 * k]), pk(v[9 + 2 * k])));
-                    r32_pairswap(oa[k].x, oa[k].y);
-                    r32_pairswap(ob[k].x, ob[k].y);
-                }
-                float2* yp = reinterpret_cast<float2*>(y + cc0 * y_stride + j * LOUT - LE) + (m & 15) + 16 * (m >> 4);
-                if (valid0) {
-#pragma unroll
-                    for (int k = 0; k < 12; ++k) st_nt(oa[k], yp + 16 * (8 + 2 * k));
-#pragma unroll
-                    for (int k = 0; k < 12; ++k) st_nt(ob[k], yp + LOUT / 2 + 16 * (8 + 2 * k));
-                }
-            } else if (valid0) {   // outputs past n are not stored
-                float* ya = y + cc0 * y_stride + j * LOUT - LE + mr;
-                const long long rem = n - (j * LOUT - LE + mr);
-                const int rm = (int)(rem < (1 << 30) ? rem : (1 << 30));
-#pragma unroll
-                for (int bb = 8; bb < 32; ++bb) {
-                    if (32 * bb < rm) ya[32 * bb] = v[bb].x;
-                    if (32 * bb + LOUT < rm) ya[LOUT + 32 * bb] = v[bb].y;
-                }
-            }
-        }
-        if (!more) break;
-    }
-}
-
 // Effective history of the block geometry (see the header comment).
 long long fir_effective_history(long long nfft, long long taps) {
     long long le = taps - 1;
@@ -894,18 +679,6 @@ static hipError_t run_fir(long long taps, const float2* H, const float* x, float
             if (!t1024) return hipErrorOutOfMemory;
             if (grid < 1) return hipSuccess;
             stat_inc(STAT_FIR_R32);
-            // knob FIR_RUN (A/B): 0 the couple walk (k_fir_r32); 1 per-half runs with the
-            // history carried in registers, one run per half-wave (k_fir_r32run);
-            // L >= 2 runs of L pairs
-            const long long run = paired ? knob(KNOB_FIR_RUN, 0) : 0;
-            if (run >= 1) {
-                const long long rl = run == 1 ? 0 : run;   // the kernel's run_len: 0 = even split
-                const long long halves = rl > 0 ? (nch * ppc + rl - 1) / rl : nch * ppc, needr = (halves + 7) / 8;
-                const int gr = (int)(needr < cap ? needr : cap);
-                hipLaunchKernelGGL(k_fir_r32run, dim3(gr), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride, ppc,
-                                   t1024, n, prefix, lm1, qf, ql, rl);
-                return hipGetLastError();
-            }
             if (paired)
                 hipLaunchKernelGGL((k_fir_r32<true>), dim3(grid), dim3(256), 0, s, H, x, y, nch, x_stride, y_stride,
                                    ppc, t1024, n, prefix, lm1, qf, ql);

@@ -475,7 +475,10 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
 //   VAR 2: tail -- the last few pairs, zero-padded past the end / odd last frame
 // N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
 template <int N, int MODE, int VAR>
-__global__ void __launch_bounds__(Wg<N>::value, (N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ? 3 : 1)
+__global__ void __launch_bounds__(Wg<N>::value, ((N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ||
+                                                 (N == 2048 && MODE == 0 && VAR == 0))
+                                                    ? 3
+                                                    : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
             long long hop, long long pair0, long long ppc, const float* win, void* out,
             long long out_ch_stride, long long row_pitch, const float2* gpass, const float2* gtab, long long chunk,
@@ -518,15 +521,32 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // stores per pair (both rows): power rows keep half the blocks + bin N/2
     constexpr int NST = MEL ? (MODE == 3 ? 4 : 2) : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
+    // N = 2048 magnitude rows (two waves per transform, LDS-DMA spans, rows
+    // staged for 16 B stores): the same half-size exchange, the last pass'
+    // twiddles of each thread's first butterfly held in registers (TwLastRegP:
+    // 1136 table entries in LDS instead of 2032) and the two rows staged one
+    // after the other through the half-size buffer -- 51 KB of LDS per
+    // workgroup instead of 75.6 KB, so 3 workgroups (3 waves per SIMD) fit per
+    // CU instead of 2
+    constexpr bool R2048 = N == 2048 && STAGE && GLDS;
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
-    constexpr bool RI = DIRECT;
+    constexpr bool RI = DIRECT || R2048;
     constexpr int XF = RI ? (ri_floats<N>() + 3) / 4 * 2 : G::LDS;   // float2 per transform (16 B multiple)
     constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
     __shared__ __attribute__((aligned(16))) float2 lds[LDSN];   // 16 B: pass_exchange_ri's b128 writes
-    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    constexpr int TWE = R2048 ? G::tw_off(G::NPASS - 1) + (G::RL - 1) * (G::ns(G::NPASS - 1) / 2)   // TwLastRegP's
+                              : TwLayout<N>::ENTRIES;
+    __shared__ float2 ltab[TWE];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
     const TwTab<N> tw{ltab};
+    using TwL = std::conditional_t<R2048, TwLastRegP<N>, TwTab<N>>;
+    TwL twl{};
+    if constexpr (R2048) {
+        twl.tab = ltab;
+        twl.hi = ltab + Geo<N>::tw_off(Geo<N>::NPASS - 1);
+        twl.load(gpass, (int)threadIdx.x % Geo<N>::T);
+    }
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + (G::NPASS > 1 ? slot * XF : 0);
     // window values 0.5 w[t + r T], packed two per VGPR pair (pk_mul_bcast)
@@ -727,7 +747,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (any && pn < pairs) grab();   // -> the pair after pn
         }
     }
-    stage_twiddles<N, WG>(ltab, gpass, gtab);
+    if constexpr (R2048) {   // the passes before the last, and the last pass' upper half
+        TwLastRegP<N>::template stage<WG>(ltab, ltab + Geo<N>::tw_off(Geo<N>::NPASS - 1), gpass);
+    } else {
+        stage_twiddles<N, WG>(ltab, gpass, gtab);
+    }
     if constexpr (MEL) {
         int* const mi = reinterpret_cast<int*>(mel_lds);
         for (int i = threadIdx.x; i < mel.nnz; i += WG) mel_lds[i] = mel.W[i];
@@ -849,7 +873,12 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
-        fft_regs<N, true, true, RI, TwTab<N>, false, false, 1>(v, t, my, tw);
+        if constexpr (R2048) {
+            twl.opaque();
+            fft_regs<N, true, true, RI, TwL, false, false, 1>(v, t, my, twl);
+        } else {
+            fft_regs<N, true, true, RI, TwTab<N>, false, false, 1>(v, t, my, tw);
+        }
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * ROWR) * ES;
         char* rowb = rowa + ROWR * ES;
         const bool has_b = (TAIL || GLDS) ? fa + 1 < frames : true;
@@ -860,6 +889,57 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                               mel_lds + mel_dpos, mel_lds + mel_dpos + mel.C * mel.M, mel);
         } else if constexpr (DIRECT) {
             direct_rows<N, MODE>(v, t, rowa, rowb, has_b, sink);
+        } else if constexpr (R2048) {
+            // row a, then row b, through the (now idle) half-size exchange buffer
+            // (N floats each), each as full-line 16 B/lane streaming stores
+            float* sf = reinterpret_cast<float*>(my);
+            float bq[G::P];   // row b's magnitudes, staged after row a's stores
+#pragma unroll
+            for (int i = 0; i < G::NPT; i += 2) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int q = i * R + r, qm = Mi::normal(q);
+                    float2 A, B;
+                    pair_post<0>(v[q], mirror_of<N, true>(v, t, q), &A, &B);
+                    float am = A.x, bm = B.x;
+                    if (i == 0) {
+                        float2 A2, B2;
+                        pair_post<0>(v[qm], v[Mi::special(qm)], &A2, &B2);
+                        am = t == 0 ? A2.x : am;
+                        bm = t == 0 ? B2.x : bm;
+                    }
+                    const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
+                    sf[k] = A.x;
+                    sf[km] = am;
+                    bq[2 * (i / 2 * R + r)] = B.x;
+                    bq[2 * (i / 2 * R + r) + 1] = bm;
+                }
+            }
+            char* rb = has_b ? rowb : reinterpret_cast<char*>(sink);
+            xsync<G::T>();
+#pragma unroll
+            for (int j = 0; j < G::P / 4; ++j) {   // N / (4 T) = P / 4 stores per row
+                const int e = 4 * (t + G::T * j);
+                st16_nt_counted(reinterpret_cast<vf4_t*>(rowa) + (t + G::T * j),
+                                *reinterpret_cast<const vf4_t*>(sf + e));
+            }
+            xsync<G::T>();
+#pragma unroll
+            for (int i = 0; i < G::NPT; i += 2) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int k = kb[i] + r * G::NB, km = kb[i + 1] + (R - 1 - r) * G::NB;
+                    sf[k] = bq[2 * (i / 2 * R + r)];
+                    sf[km] = bq[2 * (i / 2 * R + r) + 1];
+                }
+            }
+            xsync<G::T>();
+#pragma unroll
+            for (int j = 0; j < G::P / 4; ++j) {
+                const int e = 4 * (t + G::T * j);
+                st16_nt_counted(reinterpret_cast<vf4_t*>(rb) + (t + G::T * j), *reinterpret_cast<const vf4_t*>(sf + e));
+            }
+            xsync<G::T>();   // the next transform's first exchange reuses `my`
         } else if constexpr (STAGE) {
             // both magnitude rows through the (now idle) exchange buffer, then
             // full-line 16 B/lane streaming stores: 2N/(4T) instead of 2P per lane
@@ -994,39 +1074,217 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
         const long long rp = MODE == 2 ? row_pitch : ROW;   // power rows: row_pitch floats apart
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * rp) * ES;
         char* rowb = rowa + rp * ES;
-        // bins k = t + T j <= N/2 only: bin N - k of a real frame is the
-        // conjugate of bin k, bit for bit (pair_post with Z[k], Z[N-k] swapped
-        // gives conj(A), conj(B) exactly: the sums commute and negation is exact),
-        // so each post serves both bins -- half the posts and LDS reads
+        if constexpr (N == 4096 && MODE == 0) {
+            // bins k = t + T j <= N/2 only: bin N - k of a real frame is the
+            // conjugate of bin k, bit for bit (pair_post with Z[k], Z[N-k] swapped
+            // gives conj(A), conj(B) exactly: the sums commute and negation is
+            // exact), so each post serves both bins -- half the posts and LDS
+            // reads: 5.48 -> 5.17 ms for 32 ch x 10 min.  (At N = 256 the mirror
+            // halves are 16-lane, one-float-misaligned 64 B segments whose
+            // streaming stores leave partial lines: 2x slower there, and complex
+            // rows at 4096 +16 %: not used; profiles/r06_ab_fir_run_stft_sizes.jsonl.)
 #pragma unroll
-        for (int j = 0; j <= G::P / 2; ++j) {
-            const int k = t + G::T * j;
-            if (j == G::P / 2 && t != 0) continue;   // bin N/2 (its own mirror): thread 0
-            float2 A, B;
-            pair_post<MODE>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
-            const bool mir = MODE != 2 && k != 0 && k != N / 2;   // bin N - k is another bin
-            // bases at bins t and N - t: bin k = t + T j and N - k at -T j
-            if constexpr (MODE == 1) {
-                float2* ra = reinterpret_cast<float2*>(rowa) + t;
-                float2* rm = reinterpret_cast<float2*>(rowa) + (N - t);
-                st_nt(A, ra + G::T * j);
-                if (mir) st_nt(cconj(A), rm - G::T * j);
-                if (hb) {
-                    st_nt(B, ra + (rowb - rowa) / 8 + G::T * j);
-                    if (mir) st_nt(cconj(B), rm + (rowb - rowa) / 8 - G::T * j);
+            for (int j = 0; j <= G::P / 2; ++j) {
+                const int k = t + G::T * j;
+                if (j == G::P / 2 && t != 0) continue;   // bin N/2 (its own mirror): thread 0
+                float2 A, B;
+                pair_post<MODE>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
+                const bool mir = MODE != 2 && k != 0 && k != N / 2;   // bin N - k is another bin
+                // bases at bins t and N - t: bin k = t + T j and N - k at -T j
+                if constexpr (MODE == 1) {
+                    float2* ra = reinterpret_cast<float2*>(rowa) + t;
+                    float2* rm = reinterpret_cast<float2*>(rowa) + (N - t);
+                    st_nt(A, ra + G::T * j);
+                    if (mir) st_nt(cconj(A), rm - G::T * j);
+                    if (hb) {
+                        st_nt(B, ra + (rowb - rowa) / 8 + G::T * j);
+                        if (mir) st_nt(cconj(B), rm + (rowb - rowa) / 8 - G::T * j);
+                    }
+                } else {
+                    float* ra = reinterpret_cast<float*>(rowa) + t;
+                    float* rm = reinterpret_cast<float*>(rowa) + (N - t);
+                    __builtin_nontemporal_store(A.x, ra + G::T * j);
+                    if (mir) __builtin_nontemporal_store(A.x, rm - G::T * j);
+                    if (hb) {
+                        __builtin_nontemporal_store(B.x, ra + rp + G::T * j);
+                        if (mir) __builtin_nontemporal_store(B.x, rm + rp - G::T * j);
+                    }
                 }
-            } else {
-                float* ra = reinterpret_cast<float*>(rowa) + t;
-                float* rm = reinterpret_cast<float*>(rowa) + (N - t);
-                __builtin_nontemporal_store(A.x, ra + G::T * j);
-                if (mir) __builtin_nontemporal_store(A.x, rm - G::T * j);
-                if (hb) {
-                    __builtin_nontemporal_store(B.x, ra + rp + G::T * j);
-                    if (mir) __builtin_nontemporal_store(B.x, rm + rp - G::T * j);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < G::P; ++j) {
+                const int k = t + G::T * j;
+                if (MODE == 2 && k > N / 2) continue;
+                float2 A, B;
+                pair_post<MODE>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
+                if constexpr (MODE == 1) {
+                    st_nt(A, reinterpret_cast<float2*>(rowa) + k);
+                    if (hb) st_nt(B, reinterpret_cast<float2*>(rowb) + k);
+                } else {
+                    __builtin_nontemporal_store(A.x, reinterpret_cast<float*>(rowa) + k);
+                    if (hb) __builtin_nontemporal_store(B.x, reinterpret_cast<float*>(rowb) + k);
                 }
             }
         }
         xsync<G::T>();   // the next pair's FFT exchange reuses `my`
+    }
+}
+
+// ------------------------------------------------------------------------
+// k_stft_stage<N>: magnitude rows for N = 256 (T = 16 threads per transform,
+// four transforms per wave) with every global access a coalesced 16 B per
+// lane.  k_stft_pair_lds reads each frame as 16 dword loads of 64 B per slot
+// (four frames of four pairs per instruction) and writes each row the same
+// way.  Here the four slots of a wave take four consecutive frame pairs of one
+// channel (xcd_walk gives a wave's slots consecutive pairs), so the wave's
+// eight frames are ONE span of 7 hop + N samples: it comes in as <= 3
+// dwordx4 per lane (issued one step ahead, 12 VGPRs instead of 32), is laid
+// into the wave's idle exchange buffers, and each slot reads its two frames
+// from there.  After the transforms and the mirror-bin posts (bins k <= N/2,
+// bin N - k its mirror) the wave's eight rows -- 2048 contiguous floats --
+// go back through the same buffers and leave as eight dwordx4 streaming
+// stores per lane.  Steps whose four pairs cross a channel, reach past the
+// end of the signal (zero padding) or would need an unaligned span take the
+// per-slot path with the padding rule, in the same loop (a wave-uniform
+// branch).  Bit-identical to k_stft_pair_lds<N, 0> (same transform, same posts).
+// ------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(256, 3)
+k_stft_stage(const float* sig, long long n, long long nch, long long ch_stride, long long frames, long long hop,
+             const float* win, float* out, long long out_ch_stride, const float2* gpass, const float2* gtab) {
+    using G = Geo<N>;
+    constexpr int T = G::T, NT = 64 / T, F = 256 / T;
+    constexpr int WF = NT * G::LDS * 2;        // floats of one wave's exchange buffers
+    constexpr int ROWS = 2 * NT * N;           // floats of the wave's eight rows
+    constexpr int U = 3;                       // span pieces of 256 floats: 7 hop + N <= 768
+    static_assert(T == 16 && ROWS <= WF && U * 256 <= WF, "N = 256: four transforms per wave");
+    __shared__ __attribute__((aligned(16))) float2 lds[F * G::LDS];
+    __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    stage_twiddles<N, 256>(ltab, gpass, gtab);
+    const int lt = threadIdx.x, slot = lt / T, t = lt % T, lane = lt & 63, ws = slot % NT;
+    float2* my = lds + slot * G::LDS;
+    float* wb = reinterpret_cast<float*>(lds + (slot - ws) * G::LDS);   // the wave's buffers (16 B aligned)
+    float w[G::P];   // 0.5 w (pair_post)
+#pragma unroll
+    for (int r = 0; r < G::P; ++r) w[r] = 0.5f * win[t + r * T];
+    __syncthreads();
+    const TwTab<N> tw{ltab};
+    const long long ppc = (frames + 1) / 2, pairs = nch * ppc;
+    long long p, p_end, p_step;
+    xcd_walk(pairs, F, slot, &p, &p_end, &p_step);
+    long long p0 = uni<64>(p - ws);   // the wave's first pair (its slots hold p0 .. p0 + NT - 1)
+    p_end = uni<64>(p_end);
+    p_step = uni<64>(p_step);
+    const int span = (int)(2 * NT - 1) * (int)hop + N;   // the launcher keeps it <= U * 256
+    // wave-uniform: the NT pairs from q0 lie in one channel, all 2 NT frames
+    // inside the signal, and their span starts 16 B aligned
+    auto staged_ok = [&](long long q0) -> bool {
+        if (q0 + NT > p_end) return false;
+        const long long c = q0 / ppc, q = q0 - c * ppc;
+        if (q + NT > ppc) return false;
+        const long long f0 = 2 * q;
+        if (f0 + 2 * NT > frames || (f0 + 2 * NT - 1) * hop + N > n) return false;
+        return ((c * ch_stride + f0 * hop) & 3) == 0;
+    };
+    vf4_t pre[U];
+    auto issue = [&](long long q0) {
+        const long long c = q0 / ppc, f0 = 2 * (q0 - c * ppc);
+        const vf4_t* s = reinterpret_cast<const vf4_t*>(sig + c * ch_stride + f0 * hop);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = 4 * lane + 256 * u;
+            pre[u] = e < span ? __builtin_nontemporal_load(s + (e >> 2)) : vf4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+    bool stg = p0 < p_end && staged_ok(p0);
+    if (stg) issue(p0);
+    for (; p0 < p_end; p0 += p_step) {
+        const long long qq = p0 + ws, q = qq < p_end ? qq : p_end - 1;   // invalid slots redo a valid pair
+        const bool qv = qq < p_end;
+        const long long c = q / ppc, fa = 2 * (q - c * ppc);
+        const bool hb = fa + 1 < frames;
+        float xa[G::P], xb[G::P];
+        const bool stg0 = stg;
+        if (stg0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (4 * lane + 256 * u < span) *reinterpret_cast<vf4_t*>(wb + 4 * lane + 256 * u) = pre[u];
+            xsync<64>();
+            const float* fsa = wb + 2 * ws * hop + t;
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = fsa[T * r];
+                xb[r] = fsa[hop + T * r];
+            }
+            xsync<64>();
+        } else {
+            const float* sg = sig + c * ch_stride;
+            const long long sa = fa * hop, sb = sa + hop;
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const long long i = t + r * T;
+                xa[r] = sa + i < n ? sg[sa + i] : 0.0f;
+                xb[r] = hb && sb + i < n ? sg[sb + i] : 0.0f;
+            }
+        }
+        // the next step's span, in flight across this step's transforms and stores
+        stg = p0 + p_step < p_end && staged_ok(p0 + p_step);
+        if (stg) issue(p0 + p_step);
+        float2 v[G::P];
+#pragma unroll
+        for (int r = 0; r < G::P; ++r) v[r] = make_float2(xa[r] * w[r], xb[r] * w[r]);
+        fft_regs<N, true>(v, t, my, tw);
+#pragma unroll
+        for (int k = 0; k < G::P; ++k) my[G::pad(out_pos<N>(t, k))] = v[k];
+        xsync<T>();
+        float A[G::P / 2 + 1], B[G::P / 2 + 1];
+#pragma unroll
+        for (int j = 0; j <= G::P / 2; ++j) {
+            const int k = t + T * j;
+            float2 a, b;
+            pair_post<0>(my[G::pad(k & (N - 1))], my[G::pad((N - k) & (N - 1))], &a, &b);
+            A[j] = a.x;
+            B[j] = b.x;
+        }
+        xsync<64>();   // every slot of the wave has read its spectrum: the buffers take the rows
+        if (stg0) {
+            float* ra = wb + 2 * ws * N;
+#pragma unroll
+            for (int j = 0; j <= G::P / 2; ++j) {
+                const int k = t + T * j;
+                if (j == G::P / 2 && t != 0) continue;   // bin N/2: thread 0
+                ra[k] = A[j];
+                ra[N + k] = B[j];
+                if (k != 0 && k != N / 2) {
+                    ra[N - k] = A[j];
+                    ra[2 * N - k] = B[j];
+                }
+            }
+            xsync<64>();
+            const long long cw = p0 / ppc, f0 = 2 * (p0 - cw * ppc);
+            vf4_t* dst = reinterpret_cast<vf4_t*>(out + cw * out_ch_stride + f0 * N);
+#pragma unroll
+            for (int u = 0; u < ROWS / 256; ++u)
+                __builtin_nontemporal_store(*reinterpret_cast<const vf4_t*>(wb + 4 * lane + 256 * u), dst + lane + 64 * u);
+        } else if (qv) {
+            float* rowa = out + c * out_ch_stride + fa * N;
+            float* r0 = rowa + t;
+            float* rm = rowa + (N - t);
+#pragma unroll
+            for (int j = 0; j <= G::P / 2; ++j) {
+                const int k = t + T * j;
+                if (j == G::P / 2 && t != 0) continue;
+                const bool mir = k != 0 && k != N / 2;
+                __builtin_nontemporal_store(A[j], r0 + T * j);
+                if (mir) __builtin_nontemporal_store(A[j], rm - T * j);
+                if (hb) {
+                    __builtin_nontemporal_store(B[j], r0 + N + T * j);
+                    if (mir) __builtin_nontemporal_store(B[j], rm + N - T * j);
+                }
+            }
+        }
+        xsync<64>();   // the next step's span / exchange reuses the buffers
     }
 }
 
@@ -1487,6 +1745,21 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         const float2* pN = pass_twiddles(N);
         if (!tN || !pN) return hipErrorOutOfMemory;
         constexpr int WG = Wg<N>::value, F = Wg<N>::F;
+        if constexpr (N == 256 && MODE == 0) {
+            // magnitude rows with every global access 16 B per lane (k_stft_stage);
+            // knob STFT_STAGE = 0 keeps k_stft_pair_lds (A/B)
+            if (7 * hop + N <= 768 && hop % 4 == 0 && ((uintptr_t)sig & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                (out_ch_stride & 3) == 0 && knob(KNOB_STFT_STAGE, 1) != 0) {
+                static std::atomic<int> caps;
+                const int cap = cached_grid(caps, (const void*)k_stft_stage<N>, 256, 0, 1LL << 40);
+                const long long need = (nch * ((frames + 1) / 2) + F - 1) / F;
+                const int grid = (int)(need < cap ? need : cap);
+                if (grid < 1) return hipSuccess;
+                hipLaunchKernelGGL((k_stft_stage<N>), dim3(grid), dim3(256), 0, s, sig, n, nch, ch_stride, frames, hop,
+                                   win, (float*)out, out_ch_stride, pN, tN);
+                return hipGetLastError();
+            }
+        }
         static std::atomic<int> capl;
         const int cap = cached_grid(capl, (const void*)k_stft_pair_lds<N, MODE>, WG, 0, 1LL << 40);
         const long long need = (nch * ((frames + 1) / 2) + F - 1) / F;
