@@ -54,7 +54,8 @@ PUBLISHED_CPU_FPS = 24903.0   # BASELINE.md §1 STFT_size_1024 (CPU, 1 thread) -
 # the newest round's committed PMC summary of this command (profiles/rNN_bench_pmc.json,
 # or that round's rNN_final_pmc.json of its final tree, which sorts after it)
 TRAFFIC_JSON = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_pmc.json")) +
-                       glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_final_pmc.json"))) or
+                       glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_final_pmc.json")),
+                       key=lambda f: (os.path.basename(f)[:3], "_final_" in f)) or
                 [os.path.join(ROOT, "profiles", "r01_bench_pmc.json")])[-1]
 METRIC = "STFT frames/sec (1024-pt, hop 256) at 1/2/4/8 GPU; achieved HBM GB/s vs peak"
 TIMING_NOTE = ("ms_avg: HIP events around the timed launches back to back / launches (the launch stream); "

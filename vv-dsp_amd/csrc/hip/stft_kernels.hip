@@ -1011,10 +1011,11 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
 // each thread reads Z[k], Z[N-k] for bins k = t + T j -- so both rows leave
 // as lane-contiguous, full-line stores.  Persistent XCD walk with the next
 // pair's samples loaded into registers while this pair is transformed.
-// N = 256: three waves per SIMD (168 VGPRs, no spills; two at the 172 it
-// takes unbounded)
+// (Bounded to three waves per SIMD at N = 256 -- 168 VGPRs, no spills -- its
+// magnitude rows ran 4 % slower: profiles/r06_ab_stft_sizes_stage.jsonl; they
+// now run in k_stft_stage.)
 template <int N, int MODE>
-__global__ void __launch_bounds__(Wg<N>::value, N == 256 ? 3 : 1)
+__global__ void __launch_bounds__(Wg<N>::value)
 k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
                 long long hop, const float* win, void* out, long long out_ch_stride, long long row_pitch,
                 const float2* gpass, const float2* gtab) {
