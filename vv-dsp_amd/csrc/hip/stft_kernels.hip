@@ -476,7 +476,7 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
 // N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
 template <int N, int MODE, int VAR>
 __global__ void __launch_bounds__(Wg<N>::value, ((N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ||
-                                                 (N == 2048 && MODE == 0 && VAR == 0))
+                                                 (N == 2048 && MODE == 0 && (VAR == 0 || VAR == 6)))
                                                     ? 3
                                                     : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
@@ -489,7 +489,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // (launch_stft_mel; the tables of the MFCC plan in dynamic LDS)
     constexpr bool MEL = MODE == 3 || MODE == 4;
     constexpr bool TAIL = VAR == 2;
-    constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5;
+    // VAR 6 (N = 2048 magnitude rows): VAR 0 with the rows stored straight from
+    // registers (R2048D below) instead of staged through LDS
+    constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5 || VAR == 6;
     // VAR 3: VAR 0 with each wave walking a contiguous run of pairs and its
     // span kept as a ring of 256-float chunks (hop % 256 == 0): a pair DMAs only
     // its 2*hop new samples instead of the whole N + hop span
@@ -519,7 +521,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr bool DIRECT = GLDS && G::T == 64;
     static_assert(!RING || DIRECT, "ring spans: one wave per transform on the LDS-DMA path");
     // stores per pair (both rows): power rows keep half the blocks + bin N/2
-    constexpr int NST = MEL ? (MODE == 3 ? 4 : 2) : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P) : 2 * (G::P / 4);
+    constexpr int NST = MEL ? (MODE == 3 ? 4 : 2)
+                            : (DIRECT || (N == 2048 && VAR == 6)) ? (MODE == 2 ? G::P + 2 : 2 * G::P)
+                                                                  : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     // N = 2048 magnitude rows (two waves per transform, LDS-DMA spans, rows
     // staged for 16 B stores): the same half-size exchange, the last pass'
@@ -529,6 +533,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // workgroup instead of 75.6 KB, so 3 workgroups (3 waves per SIMD) fit per
     // CU instead of 2
     constexpr bool R2048 = N == 2048 && STAGE && GLDS;
+    constexpr bool R2048D = R2048 && VAR == 6;
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
     constexpr bool RI = DIRECT || R2048;
@@ -539,6 +544,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                               : TwLayout<N>::ENTRIES;
     __shared__ float2 ltab[TWE];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
+    __shared__ float xswap[R2048D ? F * 4 * G::RL : 1];   // R2048D: lane 0 trades between the transform's waves
     const TwTab<N> tw{ltab};
     using TwL = std::conditional_t<R2048, TwLastRegP<N>, TwTab<N>>;
     TwL twl{};
@@ -889,6 +895,72 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                               mel_lds + mel_dpos, mel_lds + mel_dpos + mel.C * mel.M, mel);
         } else if constexpr (DIRECT) {
             direct_rows<N, MODE>(v, t, rowa, rowb, has_b, sink);
+        } else if constexpr (R2048D) {
+            // Straight from registers, every store one aligned 256 B block (two
+            // full lines).  Lane t holds E_r = |X(t + 256 r)| (its even butterfly),
+            // which is also |X(N - t - 256 r)| (real frames: bit-identical mirror),
+            // and lane 0 its special butterfly S_r = |X(128 + 256 (7 - r))|.  Wave
+            // 0 (t < 64) stores blocks [256 r, +64) and [256 (7 - r) + 192, +64),
+            // wave 1 blocks [256 r + 64, +64) and [256 (7 - r) + 128, +64); the
+            // mirror blocks line up once lane 0 of wave 0 and lane 0 of wave 1
+            // (t = 64) trade their values through LDS: wave 0's lane 0 stores
+            // t = 64's E_r at 256 (7 - r) + 192, wave 1's lane 0 the special S_r
+            // at 256 (7 - r) + 128.
+            static_assert(G::T == 128 && R == 8 && G::NB == 256, "N = 2048: T 128, last radix 8");
+            float ea[R], eb[R], sa[R], sb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int qm = Mi::normal(r);
+                float2 A, B, A2, B2;
+                pair_post<0>(v[r], mirror_of<N, true>(v, t, r), &A, &B);
+                pair_post<0>(v[qm], v[Mi::special(qm)], &A2, &B2);
+                ea[r] = A.x;
+                eb[r] = B.x;
+                sa[r] = A2.x;
+                sb[r] = B2.x;
+            }
+            float* xs = xswap + slot * (4 * R);   // [0, R): S (row a), [R, 2R): S (row b), then t = 64's E
+            if (t == 0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    xs[r] = sa[r];
+                    xs[R + r] = sb[r];
+                }
+            } else if (t == 64) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    xs[2 * R + r] = ea[r];
+                    xs[3 * R + r] = eb[r];
+                }
+            }
+            xsync<G::T>();
+            float ma[R], mb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                ma[r] = t == 0 ? xs[2 * R + r] : t == 64 ? xs[r] : ea[r];
+                mb[r] = t == 0 ? xs[3 * R + r] : t == 64 ? xs[R + r] : eb[r];
+            }
+            const unsigned ve = 4u * (unsigned)t;
+            const unsigned vo = 4u * (unsigned)(t == 0 ? 192 : t == 64 ? 128 : 256 - t);
+            const char* ra = rowa;
+            const char* rbb = has_b ? rowb : reinterpret_cast<const char*>(sink);   // counted stores all issue
+            const char* ra2 = ra + 4096;
+            const char* rb2 = rbb + 4096;
+            auto st = [&](auto imm, unsigned off, float val, const char* b1, const char* b2) {
+                constexpr int I = decltype(imm)::value;
+                if constexpr (I < 4096) st4_pol_sbase<I, 2>(off, val, b1);
+                else st4_pol_sbase<I - 4096, 2>(off, val, b2);
+            };
+            static_for<0, R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                st(std::integral_constant<int, 4 * 256 * r>{}, ve, ea[r], ra, ra2);
+                st(std::integral_constant<int, 4 * 256 * (R - 1 - r)>{}, vo, ma[r], ra, ra2);
+            });
+            static_for<0, R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                st(std::integral_constant<int, 4 * 256 * r>{}, ve, eb[r], rbb, rb2);
+                st(std::integral_constant<int, 4 * 256 * (R - 1 - r)>{}, vo, mb[r], rbb, rb2);
+            });
         } else if constexpr (R2048) {
             // row a, then row b, through the (now idle) half-size exchange buffer
             // (N floats each), each as full-line 16 B/lane streaming stores
@@ -1601,7 +1673,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         long long mpc = (nfull < frames ? nfull : frames) / 2;
         if (mpc > ppc) mpc = ppc;
         const long long tpc = ppc - mpc;
-        static std::atomic<int> capc[6];   // zero-initialised (static storage)
+        static std::atomic<int> capc[7];   // zero-initialised (static storage)
         // The bulk launch is NOT persistent: one workgroup per `cps` pairs per
         // transform slot, so the hardware dispatcher balances the CUs and the
         // launch has no straggler tail (measured 8-13 % faster than the
@@ -1625,7 +1697,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             const long long need = (nch * cnt + F - 1) / F;
             long long grid = need < capv ? need : capv;
             long long chunk = 0;
-            if (var == 0 || var == 3) {
+            if (var == 0 || var == 3 || var == 6) {
                 chunk = cps * F;
                 grid = (nch * cnt + chunk - 1) / chunk;
             }
@@ -1731,6 +1803,14 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         } else if (aligned && FUSE_TAIL && ring) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 3>, 3, 0LL, ppc);
         } else if (aligned && FUSE_TAIL) {
+            // N = 2048 magnitude rows straight from registers (VAR 6); knob
+            // STFT_2048D = 0 stages them through LDS (VAR 0; A/B)
+            if constexpr (N == 2048 && MODE == 0) {
+                if (knob(KNOB_STFT_2048D, 1) != 0) {
+                    launch(k_stft_pair<N, MODE, 6>, 6, 0LL, ppc);
+                    return hipGetLastError();
+                }
+            }
             launch(k_stft_pair<N, MODE, 0>, 0, 0LL, ppc);
         } else {
             if (mpc > 0) {
