@@ -1804,9 +1804,9 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 3>, 3, 0LL, ppc);
         } else if (aligned && FUSE_TAIL) {
             // N = 2048 magnitude rows straight from registers (VAR 6); knob
-            // STFT_2048D = 0 stages them through LDS (VAR 0; A/B)
+            // STFT_2048D = 1 (A/B; VAR 0 stages them through LDS)
             if constexpr (N == 2048 && MODE == 0) {
-                if (knob(KNOB_STFT_2048D, 1) != 0) {
+                if (knob(KNOB_STFT_2048D, 0) != 0) {
                     launch(k_stft_pair<N, MODE, 6>, 6, 0LL, ppc);
                     return hipGetLastError();
                 }
