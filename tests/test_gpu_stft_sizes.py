@@ -89,3 +89,22 @@ def test_stft_mirror_post_complex_rows(nfft):
             x[:len(seg)] = seg
             want = np.fft.fft(x * w)
             assert np.abs(z[c, f] - want).max() <= 5e-5 + 5e-5 * np.abs(want).max() * 4
+
+
+@pytest.mark.parametrize("nch,n", [(8, 20 * 48000 + 77), (3, 2048 * 9 + 1), (1, 48000 * 30), (5, 4096 + 512 * 3)])
+def test_stft2048_direct_rows_equal_staged(nch, n):
+    """nfft 2048 magnitude rows straight from registers (k_stft_pair VAR 6, knob
+    STFT_2048D = 1: aligned 256 B blocks after a lane-0 trade between the
+    transform's two waves) against the rows staged through LDS (VAR 0): the same
+    transform and posts, so bit-identical; and against f64."""
+    import torch
+    hop = 512
+    g = torch.Generator(device="cuda").manual_seed(nch * 3 + n % 89)
+    sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
+    st = vv.Stft(2048, hop)
+    ref = st.spectrogram(sig).clone()
+    with vv.knobs(STFT_2048D=1):
+        got = st.spectrogram(sig)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    _check_rows(sig, got, 2048, hop)

@@ -1095,6 +1095,7 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     __shared__ float2 lds[F * G::LDS];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
+    __shared__ float lz[2][4][N == 4096 ? G::P / 2 + 1 : 1];   // N = 4096 rows: the waves' lane-0 values
     stage_twiddles<N, WG>(ltab, gpass, gtab);
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
@@ -1148,40 +1149,56 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * rp) * ES;
         char* rowb = rowa + rp * ES;
         if constexpr (N == 4096 && MODE == 0) {
-            // bins k = t + T j <= N/2 only: bin N - k of a real frame is the
-            // conjugate of bin k, bit for bit (pair_post with Z[k], Z[N-k] swapped
-            // gives conj(A), conj(B) exactly: the sums commute and negation is
-            // exact), so each post serves both bins -- half the posts and LDS
-            // reads: 5.48 -> 5.17 ms for 32 ch x 10 min.  (At N = 256 the mirror
-            // halves are 16-lane, one-float-misaligned 64 B segments whose
-            // streaming stores leave partial lines: 2x slower there, and complex
-            // rows at 4096 +16 %: not used; profiles/r06_ab_fir_run_stft_sizes.jsonl.)
+            // Bins k = t + T j < N/2 only: bin N - k of a real frame has the same
+            // magnitude bit for bit (pair_post with Z[k], Z[N-k] swapped gives
+            // conj(A), conj(B) exactly: the sums commute, negation is exact), so
+            // each post serves both bins -- half the posts and LDS reads
+            // (5.48 -> 5.17 ms for 32 ch x 10 min).  The mirror bins N - t - T j of
+            // a wave are one 256 B block shifted by one float; lane 0 of each wave
+            // instead stores bin N - T j - 64 (w + 1), the block's missing bin,
+            // whose value is lane 0 of the next wave's forward bin (wave 3: lane 0
+            // of wave 0 at j + 1, j = 8 being bin N/2) -- traded through LDS, so
+            // every store is one aligned 256 B block.  (At N = 256 the unshifted
+            // mirror halves are 64 B segments: 2x slower; complex rows at 4096
+            // +16 %: neither uses it; profiles/r06_ab_fir_run_stft_sizes.jsonl.)
+            constexpr int JH = G::P / 2;   // 8: bins t + T j, j < JH, cover [0, N/2)
+            float fa[JH], fb[JH];
 #pragma unroll
-            for (int j = 0; j <= G::P / 2; ++j) {
+            for (int j = 0; j < JH; ++j) {
                 const int k = t + G::T * j;
-                if (j == G::P / 2 && t != 0) continue;   // bin N/2 (its own mirror): thread 0
                 float2 A, B;
-                pair_post<MODE>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
-                const bool mir = MODE != 2 && k != 0 && k != N / 2;   // bin N - k is another bin
-                // bases at bins t and N - t: bin k = t + T j and N - k at -T j
-                if constexpr (MODE == 1) {
-                    float2* ra = reinterpret_cast<float2*>(rowa) + t;
-                    float2* rm = reinterpret_cast<float2*>(rowa) + (N - t);
-                    st_nt(A, ra + G::T * j);
-                    if (mir) st_nt(cconj(A), rm - G::T * j);
-                    if (hb) {
-                        st_nt(B, ra + (rowb - rowa) / 8 + G::T * j);
-                        if (mir) st_nt(cconj(B), rm + (rowb - rowa) / 8 - G::T * j);
-                    }
-                } else {
-                    float* ra = reinterpret_cast<float*>(rowa) + t;
-                    float* rm = reinterpret_cast<float*>(rowa) + (N - t);
-                    __builtin_nontemporal_store(A.x, ra + G::T * j);
-                    if (mir) __builtin_nontemporal_store(A.x, rm - G::T * j);
-                    if (hb) {
-                        __builtin_nontemporal_store(B.x, ra + rp + G::T * j);
-                        if (mir) __builtin_nontemporal_store(B.x, rm + rp - G::T * j);
-                    }
+                pair_post<0>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
+                fa[j] = A.x;
+                fb[j] = B.x;
+            }
+            const int wv = t >> 6, ln = t & 63;
+            if (ln == 0) {
+#pragma unroll
+                for (int j = 0; j < JH; ++j) {
+                    lz[0][wv][j] = fa[j];
+                    lz[1][wv][j] = fb[j];
+                }
+                if (wv == 0) {   // bin N/2, its own mirror
+                    float2 A, B;
+                    pair_post<0>(my[G::pad(N / 2)], my[G::pad(N / 2)], &A, &B);
+                    lz[0][0][JH] = A.x;
+                    lz[1][0][JH] = B.x;
+                }
+            }
+            xsync<G::T>();
+            const int sw = wv == 3 ? 0 : wv + 1, sj = wv == 3 ? 1 : 0;   // lane 0's source wave and j offset
+            float* ra = reinterpret_cast<float*>(rowa);
+            float* rb = reinterpret_cast<float*>(rowb);
+            const int mo = ln == 0 ? N - 64 * (wv + 1) : N - t;   // mirror bin at j = 0
+#pragma unroll
+            for (int j = 0; j < JH; ++j) {
+                const float ma = ln == 0 ? lz[0][sw][j + sj] : fa[j];
+                const float mb = ln == 0 ? lz[1][sw][j + sj] : fb[j];
+                __builtin_nontemporal_store(fa[j], ra + t + G::T * j);
+                __builtin_nontemporal_store(ma, ra + mo - G::T * j);
+                if (hb) {
+                    __builtin_nontemporal_store(fb[j], rb + t + G::T * j);
+                    __builtin_nontemporal_store(mb, rb + mo - G::T * j);
                 }
             }
         } else {
