@@ -6,7 +6,8 @@ nfft/4; stft.c:112-144 semantics) through the round-6 kernels:
     STFT_STAGE = 0), which is pinned to f64 by test_gpu_parity.py;
   * nfft 2048: k_stft_pair VAR 0 with the half-size exchange and register
     last-pass twiddles (three waves per SIMD);
-  * nfft 256 / 4096: mirror-bin posts (bin N - k from bin k's post).
+  * nfft 256 / 4096: mirror-bin posts (bin N - k from bin k's post);
+  * nfft 4096: k_stft_one (one frame pair per transform slot, no loop).
 Every case checks sampled rows of every channel against NumPy f64 at the
 harness rule (VV_PY_RTOL/ATOL, python/test_fft.py:37-38), channels with odd
 pair counts and zero-padded tails included."""
@@ -91,20 +92,25 @@ def test_stft_mirror_post_complex_rows(nfft):
             assert np.abs(z[c, f] - want).max() <= 5e-5 + 5e-5 * np.abs(want).max() * 4
 
 
-@pytest.mark.parametrize("nch,n", [(8, 20 * 48000 + 77), (3, 2048 * 9 + 1), (1, 48000 * 30), (5, 4096 + 512 * 3)])
-def test_stft2048_direct_rows_equal_staged(nch, n):
-    """nfft 2048 magnitude rows straight from registers (k_stft_pair VAR 6, knob
-    STFT_2048D = 1: aligned 256 B blocks after a lane-0 trade between the
-    transform's two waves) against the rows staged through LDS (VAR 0): the same
-    transform and posts, so bit-identical; and against f64."""
+@pytest.mark.parametrize("nch,n", [(8, 20 * 48000 + 77), (3, 4096 * 9 + 1), (1, 48000 * 30), (5, 4096 + 1024 * 3),
+                                   (2, 5000)])
+def test_stft4096_one_pair_per_slot(nch, n):
+    """nfft 4096 magnitude rows on k_stft_one (one frame pair per transform slot,
+    no loop; last-pass twiddles as powers in registers) against k_stft_pair_lds
+    (knob STFT_ONE = 0): the same transform and mirror-bin posts, up to f32
+    rounding (other roundings of the twiddles, and the compiler may contract the
+    window product into the first butterflies differently) -- within 2e-5 of the
+    largest bin; and against f64 at the harness rule (zero-padded tails, odd
+    pair counts, fewer pairs than the grid's eight XCD ranges)."""
     import torch
-    hop = 512
-    g = torch.Generator(device="cuda").manual_seed(nch * 3 + n % 89)
+    nfft = 4096
+    hop = nfft // 4
+    g = torch.Generator(device="cuda").manual_seed(nch * 5 + n % 97 + nfft)
     sig = torch.rand(nch, n, device="cuda", generator=g) * 2 - 1
-    st = vv.Stft(2048, hop)
-    ref = st.spectrogram(sig).clone()
-    with vv.knobs(STFT_2048D=1):
-        got = st.spectrogram(sig)
+    st = vv.Stft(nfft, hop)
+    got = st.spectrogram(sig).clone()
+    with vv.knobs(STFT_ONE=0):
+        ref = st.spectrogram(sig)
     torch.cuda.synchronize()
-    assert torch.equal(got, ref)
-    _check_rows(sig, got, 2048, hop)
+    assert (got - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
+    _check_rows(sig, got, nfft, hop)

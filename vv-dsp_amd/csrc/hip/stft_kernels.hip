@@ -476,7 +476,7 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
 // N = 1024 bulk: 3 waves per SIMD (<= 168 VGPRs) -- the LDS budget allows 3 workgroups per CU
 template <int N, int MODE, int VAR>
 __global__ void __launch_bounds__(Wg<N>::value, ((N == 1024 && (VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5)) ||
-                                                 (N == 2048 && MODE == 0 && (VAR == 0 || VAR == 6)))
+                                                 (N == 2048 && MODE == 0 && VAR == 0))
                                                     ? 3
                                                     : 1)
 k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, long long frames,
@@ -489,9 +489,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // (launch_stft_mel; the tables of the MFCC plan in dynamic LDS)
     constexpr bool MEL = MODE == 3 || MODE == 4;
     constexpr bool TAIL = VAR == 2;
-    // VAR 6 (N = 2048 magnitude rows): VAR 0 with the rows stored straight from
-    // registers (R2048D below) instead of staged through LDS
-    constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5 || VAR == 6;
+    constexpr bool BULK = VAR == 0 || VAR == 3 || VAR == 4 || VAR == 5;
     // VAR 3: VAR 0 with each wave walking a contiguous run of pairs and its
     // span kept as a ring of 256-float chunks (hop % 256 == 0): a pair DMAs only
     // its 2*hop new samples instead of the whole N + hop span
@@ -522,7 +520,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     static_assert(!RING || DIRECT, "ring spans: one wave per transform on the LDS-DMA path");
     // stores per pair (both rows): power rows keep half the blocks + bin N/2
     constexpr int NST = MEL ? (MODE == 3 ? 4 : 2)
-                            : (DIRECT || (N == 2048 && VAR == 6)) ? (MODE == 2 ? G::P + 2 : 2 * G::P)
+                            : DIRECT ? (MODE == 2 ? G::P + 2 : 2 * G::P)
                                                                   : 2 * (G::P / 4);
     constexpr int WG = Wg<N>::value, F = Wg<N>::F, R = G::RL;
     // N = 2048 magnitude rows (two waves per transform, LDS-DMA spans, rows
@@ -533,7 +531,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // workgroup instead of 75.6 KB, so 3 workgroups (3 waves per SIMD) fit per
     // CU instead of 2
     constexpr bool R2048 = N == 2048 && STAGE && GLDS;
-    constexpr bool R2048D = R2048 && VAR == 6;
     // DIRECT needs no staging buffer: the exchange goes through a half-size
     // (real, then imaginary) buffer, so 3 workgroups fit per CU instead of 2
     constexpr bool RI = DIRECT || R2048;
@@ -544,7 +541,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                               : TwLayout<N>::ENTRIES;
     __shared__ float2 ltab[TWE];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
-    __shared__ float xswap[R2048D ? F * 4 * G::RL : 1];   // R2048D: lane 0 trades between the transform's waves
     const TwTab<N> tw{ltab};
     using TwL = std::conditional_t<R2048, TwLastRegP<N>, TwTab<N>>;
     TwL twl{};
@@ -895,72 +891,6 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
                               mel_lds + mel_dpos, mel_lds + mel_dpos + mel.C * mel.M, mel);
         } else if constexpr (DIRECT) {
             direct_rows<N, MODE>(v, t, rowa, rowb, has_b, sink);
-        } else if constexpr (R2048D) {
-            // Straight from registers, every store one aligned 256 B block (two
-            // full lines).  Lane t holds E_r = |X(t + 256 r)| (its even butterfly),
-            // which is also |X(N - t - 256 r)| (real frames: bit-identical mirror),
-            // and lane 0 its special butterfly S_r = |X(128 + 256 (7 - r))|.  Wave
-            // 0 (t < 64) stores blocks [256 r, +64) and [256 (7 - r) + 192, +64),
-            // wave 1 blocks [256 r + 64, +64) and [256 (7 - r) + 128, +64); the
-            // mirror blocks line up once lane 0 of wave 0 and lane 0 of wave 1
-            // (t = 64) trade their values through LDS: wave 0's lane 0 stores
-            // t = 64's E_r at 256 (7 - r) + 192, wave 1's lane 0 the special S_r
-            // at 256 (7 - r) + 128.
-            static_assert(G::T == 128 && R == 8 && G::NB == 256, "N = 2048: T 128, last radix 8");
-            float ea[R], eb[R], sa[R], sb[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int qm = Mi::normal(r);
-                float2 A, B, A2, B2;
-                pair_post<0>(v[r], mirror_of<N, true>(v, t, r), &A, &B);
-                pair_post<0>(v[qm], v[Mi::special(qm)], &A2, &B2);
-                ea[r] = A.x;
-                eb[r] = B.x;
-                sa[r] = A2.x;
-                sb[r] = B2.x;
-            }
-            float* xs = xswap + slot * (4 * R);   // [0, R): S (row a), [R, 2R): S (row b), then t = 64's E
-            if (t == 0) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    xs[r] = sa[r];
-                    xs[R + r] = sb[r];
-                }
-            } else if (t == 64) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    xs[2 * R + r] = ea[r];
-                    xs[3 * R + r] = eb[r];
-                }
-            }
-            xsync<G::T>();
-            float ma[R], mb[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                ma[r] = t == 0 ? xs[2 * R + r] : t == 64 ? xs[r] : ea[r];
-                mb[r] = t == 0 ? xs[3 * R + r] : t == 64 ? xs[R + r] : eb[r];
-            }
-            const unsigned ve = 4u * (unsigned)t;
-            const unsigned vo = 4u * (unsigned)(t == 0 ? 192 : t == 64 ? 128 : 256 - t);
-            const char* ra = rowa;
-            const char* rbb = has_b ? rowb : reinterpret_cast<const char*>(sink);   // counted stores all issue
-            const char* ra2 = ra + 4096;
-            const char* rb2 = rbb + 4096;
-            auto st = [&](auto imm, unsigned off, float val, const char* b1, const char* b2) {
-                constexpr int I = decltype(imm)::value;
-                if constexpr (I < 4096) st4_pol_sbase<I, 2>(off, val, b1);
-                else st4_pol_sbase<I - 4096, 2>(off, val, b2);
-            };
-            static_for<0, R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                st(std::integral_constant<int, 4 * 256 * r>{}, ve, ea[r], ra, ra2);
-                st(std::integral_constant<int, 4 * 256 * (R - 1 - r)>{}, vo, ma[r], ra, ra2);
-            });
-            static_for<0, R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                st(std::integral_constant<int, 4 * 256 * r>{}, ve, eb[r], rbb, rb2);
-                st(std::integral_constant<int, 4 * 256 * (R - 1 - r)>{}, vo, mb[r], rbb, rb2);
-            });
         } else if constexpr (R2048) {
             // row a, then row b, through the (now idle) half-size exchange buffer
             // (N floats each), each as full-line 16 B/lane streaming stores
@@ -1095,7 +1025,6 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
     constexpr int WG = Wg<N>::value, F = Wg<N>::F;
     __shared__ float2 lds[F * G::LDS];
     __shared__ float2 ltab[TwLayout<N>::ENTRIES];
-    __shared__ float lz[2][4][N == 4096 ? G::P / 2 + 1 : 1];   // N = 4096 rows: the waves' lane-0 values
     stage_twiddles<N, WG>(ltab, gpass, gtab);
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
     float2* my = lds + slot * G::LDS;
@@ -1149,56 +1078,40 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
         char* rowa = reinterpret_cast<char*>(out) + (c * out_ch_stride + fa * rp) * ES;
         char* rowb = rowa + rp * ES;
         if constexpr (N == 4096 && MODE == 0) {
-            // Bins k = t + T j < N/2 only: bin N - k of a real frame has the same
-            // magnitude bit for bit (pair_post with Z[k], Z[N-k] swapped gives
-            // conj(A), conj(B) exactly: the sums commute, negation is exact), so
-            // each post serves both bins -- half the posts and LDS reads
-            // (5.48 -> 5.17 ms for 32 ch x 10 min).  The mirror bins N - t - T j of
-            // a wave are one 256 B block shifted by one float; lane 0 of each wave
-            // instead stores bin N - T j - 64 (w + 1), the block's missing bin,
-            // whose value is lane 0 of the next wave's forward bin (wave 3: lane 0
-            // of wave 0 at j + 1, j = 8 being bin N/2) -- traded through LDS, so
-            // every store is one aligned 256 B block.  (At N = 256 the unshifted
-            // mirror halves are 64 B segments: 2x slower; complex rows at 4096
-            // +16 %: neither uses it; profiles/r06_ab_fir_run_stft_sizes.jsonl.)
-            constexpr int JH = G::P / 2;   // 8: bins t + T j, j < JH, cover [0, N/2)
-            float fa[JH], fb[JH];
+            // bins k = t + T j <= N/2 only: bin N - k of a real frame is the
+            // conjugate of bin k, bit for bit (pair_post with Z[k], Z[N-k] swapped
+            // gives conj(A), conj(B) exactly: the sums commute and negation is
+            // exact), so each post serves both bins -- half the posts and LDS
+            // reads: 5.48 -> 5.17 ms for 32 ch x 10 min.  (At N = 256 the mirror
+            // halves are 16-lane, one-float-misaligned 64 B segments whose
+            // streaming stores leave partial lines: 2x slower there, and complex
+            // rows at 4096 +16 %: not used; profiles/r06_ab_fir_run_stft_sizes.jsonl.)
 #pragma unroll
-            for (int j = 0; j < JH; ++j) {
+            for (int j = 0; j <= G::P / 2; ++j) {
                 const int k = t + G::T * j;
+                if (j == G::P / 2 && t != 0) continue;   // bin N/2 (its own mirror): thread 0
                 float2 A, B;
-                pair_post<0>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
-                fa[j] = A.x;
-                fb[j] = B.x;
-            }
-            const int wv = t >> 6, ln = t & 63;
-            if (ln == 0) {
-#pragma unroll
-                for (int j = 0; j < JH; ++j) {
-                    lz[0][wv][j] = fa[j];
-                    lz[1][wv][j] = fb[j];
-                }
-                if (wv == 0) {   // bin N/2, its own mirror
-                    float2 A, B;
-                    pair_post<0>(my[G::pad(N / 2)], my[G::pad(N / 2)], &A, &B);
-                    lz[0][0][JH] = A.x;
-                    lz[1][0][JH] = B.x;
-                }
-            }
-            xsync<G::T>();
-            const int sw = wv == 3 ? 0 : wv + 1, sj = wv == 3 ? 1 : 0;   // lane 0's source wave and j offset
-            float* ra = reinterpret_cast<float*>(rowa);
-            float* rb = reinterpret_cast<float*>(rowb);
-            const int mo = ln == 0 ? N - 64 * (wv + 1) : N - t;   // mirror bin at j = 0
-#pragma unroll
-            for (int j = 0; j < JH; ++j) {
-                const float ma = ln == 0 ? lz[0][sw][j + sj] : fa[j];
-                const float mb = ln == 0 ? lz[1][sw][j + sj] : fb[j];
-                __builtin_nontemporal_store(fa[j], ra + t + G::T * j);
-                __builtin_nontemporal_store(ma, ra + mo - G::T * j);
-                if (hb) {
-                    __builtin_nontemporal_store(fb[j], rb + t + G::T * j);
-                    __builtin_nontemporal_store(mb, rb + mo - G::T * j);
+                pair_post<MODE>(my[G::pad(k)], my[G::pad((N - k) & (N - 1))], &A, &B);
+                const bool mir = MODE != 2 && k != 0 && k != N / 2;   // bin N - k is another bin
+                // bases at bins t and N - t: bin k = t + T j and N - k at -T j
+                if constexpr (MODE == 1) {
+                    float2* ra = reinterpret_cast<float2*>(rowa) + t;
+                    float2* rm = reinterpret_cast<float2*>(rowa) + (N - t);
+                    st_nt(A, ra + G::T * j);
+                    if (mir) st_nt(cconj(A), rm - G::T * j);
+                    if (hb) {
+                        st_nt(B, ra + (rowb - rowa) / 8 + G::T * j);
+                        if (mir) st_nt(cconj(B), rm + (rowb - rowa) / 8 - G::T * j);
+                    }
+                } else {
+                    float* ra = reinterpret_cast<float*>(rowa) + t;
+                    float* rm = reinterpret_cast<float*>(rowa) + (N - t);
+                    __builtin_nontemporal_store(A.x, ra + G::T * j);
+                    if (mir) __builtin_nontemporal_store(A.x, rm - G::T * j);
+                    if (hb) {
+                        __builtin_nontemporal_store(B.x, ra + rp + G::T * j);
+                        if (mir) __builtin_nontemporal_store(B.x, rm + rp - G::T * j);
+                    }
                 }
             }
         } else {
@@ -1219,6 +1132,171 @@ k_stft_pair_lds(const float* sig, long long n, long long nch, long long ch_strid
         }
         xsync<G::T>();   // the next pair's FFT exchange reuses `my`
     }
+}
+
+// ------------------------------------------------------------------------
+// k_stft_one<N>: magnitude rows with ONE frame pair per transform slot and no
+// loop (N = 4096) -- no prefetch registers, no persistent walk: the occupancy
+// hides the latency and the dispatcher balances the CUs (k_c2c ONE's shape,
+// which took c2c 4096 from 0.72 to 0.775).  Slot s of block b takes pair
+// (b % 8) per8 + (b / 8) F + s: each XCD (block b runs on XCD b % 8) walks its
+// own contiguous eighth of the pairs, so the N + hop - 2 hop overlap of
+// neighbouring spans comes from that XCD's L2.  The frames are windowed on load
+// (zero past the end of the signal), two per complex FFT; the spectrum goes to
+// LDS in natural order and each post serves bin k and its mirror N - k (bit for
+// bit the same magnitude), as k_stft_pair_lds<4096>.
+// ------------------------------------------------------------------------
+// Twiddles of a one-transform kernel whose threads own one last-pass butterfly
+// each (T = N/16, e.g. N = 4096): the passes before the last read the LDS
+// pass-major table (its first tw_off(LAST) entries: 240 at 4096); the last
+// pass' W_N^{t r} (j = t) are powers of W = W_N^t -- one L2 load per thread,
+// each power a product of W, W^2, W^4, W^8 (at most four roundings deep) --
+// instead of the two-level table's two LDS reads, index arithmetic and complex
+// multiply per twiddle.
+template <int N>
+struct TwPow {
+    using G = Geo<N>;
+    static constexpr int LAST = G::NPASS - 1, RL = G::RL, NS = G::ns(LAST);
+    static_assert(G::T == NS && G::P == RL, "one last-pass butterfly per thread, j = t");
+    const float2* tab;
+    float2 w[RL - 1];   // w[r - 1] = W^r
+    template <int p>
+    __device__ __forceinline__ float2 at(int j, int r, int /*i*/ = 0) const {
+        if constexpr (p == LAST) return w[r - 1];
+        else return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
+    }
+    __device__ __forceinline__ void init(float2 W) {
+        w[0] = W;
+#pragma unroll
+        for (int r = 2; r < RL; ++r) {
+            const int hp = 1 << (31 - __builtin_clz(r));   // the highest power of two <= r
+            w[r - 1] = r == hp ? cmul(w[hp / 2 - 1], w[hp / 2 - 1]) : cmul(w[hp - 1], w[r - hp - 1]);
+        }
+    }
+};
+
+template <int N, int VAR>
+__global__ void __launch_bounds__(Wg<N>::value)
+k_stft_one(const float* sig, long long n, long long nch, long long ch_stride, long long frames, long long hop,
+           const float* win, float* out, long long out_ch_stride, const float2* gpass, const float2* gtab,
+           long long per8) {
+    // VAR bits: 1 the samples loaded before the twiddles are staged; 2 the
+    // half-size real/imaginary exchange (and spectrum pass), half the LDS per
+    // transform; 4 the last pass' twiddles as powers in registers (TwPow)
+    // instead of the two-level lo * hi table
+    using G = Geo<N>;
+    static_assert(G::T >= 64 && G::T % 64 == 0, "whole waves per transform");
+    constexpr bool EARLY = VAR & 1, RI = VAR & 2, TLR = VAR & 4;
+    constexpr int WG = Wg<N>::value, F = Wg<N>::F, JH = G::P / 2;
+    constexpr int XF = RI ? (ri_floats<N>() + 3) / 4 * 2 : G::LDS;   // float2 per transform
+    __shared__ __attribute__((aligned(16))) float2 lds[F * XF];
+    using TW = std::conditional_t<TLR, TwPow<N>, TwTab<N>>;
+    __shared__ float2 ltab[TLR ? G::tw_off(G::NPASS - 1) : TwLayout<N>::ENTRIES];
+    const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
+    float2* my = lds + slot * XF;
+    const long long b = blockIdx.x;
+    const long long ppc = (frames + 1) / 2, pairs = nch * ppc;
+    const long long p = uni<G::T>((b & 7) * per8 + (b >> 3) * F + slot);
+    const bool act = p < pairs;   // uniform per transform
+    const long long pc = act ? p : 0;   // an idle slot (F > 1) transforms pair 0 and stores nothing
+    // (channel, first frame): 32-bit division (the launcher keeps pairs < 2^31)
+    const unsigned cu = (unsigned)pc / (unsigned)ppc;
+    const long long c = cu, fa = 2 * (pc - (long long)cu * ppc);
+    const float* s = sig + c * ch_stride;
+    const long long sa = fa * hop, sb = sa + hop;
+    const bool hb = fa + 1 < frames;
+    float2 v[G::P];
+    auto load = [&]() {
+        if (sb + N <= n) {   // both frames inside the signal
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const float w = 0.5f * win[t + r * G::T];
+                v[r] = make_float2(s[sa + t + r * G::T] * w, s[sb + t + r * G::T] * w);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                const long long i = t + r * G::T;
+                const float w = 0.5f * win[i];
+                const float xa = sa + i < n ? s[sa + i] : 0.0f;
+                const float xb = hb && sb + i < n ? s[sb + i] : 0.0f;
+                v[r] = make_float2(xa * w, xb * w);
+            }
+        }
+    };
+    if constexpr (EARLY) load();
+    TW tw{ltab};
+    float2 w1 = make_float2(1.0f, 0.0f);
+    if constexpr (TLR) {
+        w1 = gtab[t];   // W_N^t
+        for (int i = threadIdx.x; i < G::tw_off(G::NPASS - 1); i += WG) ltab[i] = gpass[i];
+    } else {
+        stage_twiddles<N, WG>(ltab, gpass, gtab);
+    }
+    __syncthreads();
+    if constexpr (F == 1) {
+        if (!act) return;
+    }
+    if constexpr (!EARLY) load();
+    if constexpr (TLR) tw.init(w1);
+    fft_regs<N, true, false, RI, TW>(v, t, my, tw);
+    float* ra = out + c * out_ch_stride + fa * N;
+    float* rb = ra + N;
+    // each post stores bin k and its mirror N - k at once (k <= N/2; the
+    // mirror blocks one float off the 256 B grid)
+    auto post = [&](const float2* z, const float2* zm) {
+#pragma unroll
+        for (int j = 0; j <= JH; ++j) {
+            const int k = t + G::T * j;
+            if (j == JH && t != 0) continue;   // bin N/2 (its own mirror): thread 0
+            float2 A, B;
+            pair_post<0>(z[j], zm[j], &A, &B);
+            const bool mir = k != 0 && k != N / 2;   // bin N - k is another bin
+            __builtin_nontemporal_store(A.x, ra + k);
+            if (mir) __builtin_nontemporal_store(A.x, ra + N - k);
+            if (hb) {
+                __builtin_nontemporal_store(B.x, rb + k);
+                if (mir) __builtin_nontemporal_store(B.x, rb + N - k);
+            }
+        }
+    };
+    float2 z[JH + 1], zm[JH + 1];
+    if constexpr (RI) {
+        // the spectrum in natural order through the half-size buffer: real
+        // parts, then imaginary parts, of bins k and N - k
+        float* lf = reinterpret_cast<float*>(my);
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) lf[G::pad(out_pos<N>(t, q))] = v[q].x;
+        xsync<G::T>();
+#pragma unroll
+        for (int j = 0; j <= JH; ++j) {
+            const int k = j < JH ? t + G::T * j : N / 2;
+            z[j].x = lf[G::pad(k)];
+            zm[j].x = lf[G::pad((N - k) & (N - 1))];
+        }
+        xsync<G::T>();
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) lf[G::pad(out_pos<N>(t, q))] = v[q].y;
+        xsync<G::T>();
+#pragma unroll
+        for (int j = 0; j <= JH; ++j) {
+            const int k = j < JH ? t + G::T * j : N / 2;
+            z[j].y = lf[G::pad(k)];
+            zm[j].y = lf[G::pad((N - k) & (N - 1))];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < G::P; ++q) my[G::pad(out_pos<N>(t, q))] = v[q];
+        xsync<G::T>();
+#pragma unroll
+        for (int j = 0; j <= JH; ++j) {
+            const int k = j < JH ? t + G::T * j : N / 2;
+            z[j] = my[G::pad(k)];
+            zm[j] = my[G::pad((N - k) & (N - 1))];
+        }
+    }
+    if (!act) return;   // after the last barrier
+    post(z, zm);
 }
 
 // ------------------------------------------------------------------------
@@ -1679,6 +1757,28 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
                            long long frames, long long hop, const float* win, void* out,
                            long long out_ch_stride, hipStream_t s, long long row_pitch) {
     if (MODE != 2 || row_pitch <= 0) row_pitch = MODE == 2 ? N / 2 + 1 : N;   // packed rows
+    if constexpr (MODE == 0 && N == 4096) {
+        // one frame pair per transform slot, no loop (k_stft_one VAR 5: the loads
+        // before the twiddle staging, the last pass' twiddles as powers in
+        // registers): 5.07 -> 4.13 ms for 32 ch x 10 min against k_stft_pair_lds
+        // (0.454 -> 0.558 of HBM; profiles/r06_ab_stft4096_one.jsonl: the
+        // half-size exchange at five workgroups per CU, the lane-0 trade for
+        // aligned mirror blocks and the two-level twiddle table were slower).
+        // Knob STFT_ONE = 0 keeps k_stft_pair_lds (A/B)
+        if (knob(KNOB_STFT_ONE, 1) != 0 && nch * ((frames + 1) / 2) < (1LL << 31)) {
+            const float2* tN = twiddle_table(N);
+            const float2* pN = pass_twiddles(N);
+            if (!tN || !pN) return hipErrorOutOfMemory;
+            constexpr int F = Wg<N>::F;
+            const long long pairs = nch * ((frames + 1) / 2);
+            const long long per8 = ((pairs + 8 * F - 1) / (8 * F)) * F;   // pairs per XCD, whole blocks
+            const long long grid = 8 * (per8 / F);
+            if (pairs < 1) return hipSuccess;
+            hipLaunchKernelGGL((k_stft_one<N, 5>), dim3((unsigned)grid), dim3(Wg<N>::value), 0, s, sig, n, nch,
+                               ch_stride, frames, hop, win, (float*)out, out_ch_stride, pN, tN, per8);
+            return hipGetLastError();
+        }
+    }
     if constexpr (Geo<N>::CAN_PAIR) {
         const float2* tN = twiddle_table(N);
         const float2* pN = pass_twiddles(N);
@@ -1714,7 +1814,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
             const long long need = (nch * cnt + F - 1) / F;
             long long grid = need < capv ? need : capv;
             long long chunk = 0;
-            if (var == 0 || var == 3 || var == 6) {
+            if (var == 0 || var == 3) {
                 chunk = cps * F;
                 grid = (nch * cnt + chunk - 1) / chunk;
             }
@@ -1820,14 +1920,6 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         } else if (aligned && FUSE_TAIL && ring) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 3>, 3, 0LL, ppc);
         } else if (aligned && FUSE_TAIL) {
-            // N = 2048 magnitude rows straight from registers (VAR 6); knob
-            // STFT_2048D = 1 (A/B; VAR 0 stages them through LDS)
-            if constexpr (N == 2048 && MODE == 0) {
-                if (knob(KNOB_STFT_2048D, 0) != 0) {
-                    launch(k_stft_pair<N, MODE, 6>, 6, 0LL, ppc);
-                    return hipGetLastError();
-                }
-            }
             launch(k_stft_pair<N, MODE, 0>, 0, 0LL, ppc);
         } else {
             if (mpc > 0) {
