@@ -28,7 +28,7 @@ constexpr const char* KNOB_NAMES[KNOB_COUNT] = {
     "FS_VAR",        "FS_CHUNK_MB",  "FS_OLD",       "BLUE_UNFUSED", "C2C_MAX",    "STFT_SQ",     "MIX_VAR",
     "MIX_CHUNK_MB",  "MIX_R2C_FULL", "FIR_OLD",      "FIR_DYN",     "FIR_DIRECT_LDS", "FIR_BLOCK",
     "HOST_CHUNK_MB", "NO_MIXED",     "REAL_PROMOTE", "ISTFT_OLD",   "MEL_FUSED",   "CZT_UNFUSED",
-    "CEPS_UNFUSED",  "FIR_R32",      "DIST_SLAB_KB", "POW_R32", "MAG_R32",     "MEL_R32", "C2C_TPW", "C2C_ONE", "REAL_TPW", "ANA_TPW", "MIX_TPW", "C2C_SMALL", "DCT_SMALL", "HIL_SMALL", "REAL_SMALL", "R2C_SMALL", "STFT_STAGE", "STFT_ONE",
+    "CEPS_UNFUSED",  "FIR_R32",      "DIST_SLAB_KB", "POW_R32", "MAG_R32",     "MEL_R32", "C2C_TPW", "C2C_ONE", "REAL_TPW", "ANA_TPW", "MIX_TPW", "C2C_SMALL", "DCT_SMALL", "HIL_SMALL", "REAL_SMALL", "R2C_SMALL", "STFT_STAGE", "STFT_ONE", "MFCC_WIN",
 };
 constexpr const char* STAT_NAMES[STAT_COUNT] = {
     "STAT_STFT_DYN", "STAT_FIR_DYN", "STAT_FIR_STATIC", "STAT_MEL_FUSED", "STAT_MEL_SPLIT", "STAT_FIR_R32", "STAT_POW_R32", "STAT_MAG_R32", "STAT_MEL_R32",

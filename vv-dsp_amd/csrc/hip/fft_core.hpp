@@ -382,6 +382,44 @@ struct TwLastRegP {
     }
 };
 
+// The same for every last-pass butterfly of a thread held in registers (any
+// NPT, e.g. N = 1024 mirror-paired: T = 64, last radix 4, four butterflies
+// t, NB - t, t + 64, NB - 64 - t): NPT (RL - 1) twiddles in VGPRs (24 at 1024),
+// loaded once per workgroup from the global pass-major table -- the table's own
+// values, so bit-identical to TwTab -- and only the passes before the last in
+// LDS (240 of 1008 entries at 1024: 6 KB of LDS and 12 LDS reads per
+// transform saved).
+template <int N, bool PAIRED>
+struct TwLastRegA {
+    using G = Geo<N>;
+    static constexpr int LAST = G::NPASS - 1, RL = G::RL, NS = G::ns(LAST), NPT = G::NPT;
+    static_assert(G::NB == NS, "the last pass' butterfly index is its twiddle index");
+    const float2* tab;            // LDS: pass-major entries of passes < LAST
+    float2 w[NPT * (RL - 1)];     // [i][r - 1]: W^{j_i r} of the thread's last-pass butterfly i
+    template <int p>
+    __device__ __forceinline__ float2 at(int j, int r, int i) const {
+        if constexpr (p == LAST) return w[i * (RL - 1) + r - 1];
+        else return tab[G::tw_off(p) + (r - 1) * G::ns(p) + j];
+    }
+    __device__ __forceinline__ void load(const float2* gpass, int t) {
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int j = bfly<N, LAST, PAIRED>(t, i);
+#pragma unroll
+            for (int r = 1; r < RL; ++r) w[i * (RL - 1) + r - 1] = gpass[G::tw_off(LAST) + (r - 1) * NS + j];
+        }
+        opaque();
+    }
+    template <int NTHREADS>
+    __device__ __forceinline__ static void stage(float2* lds_tab, const float2* gpass) {
+        for (int i = threadIdx.x; i < G::tw_off(LAST); i += NTHREADS) lds_tab[i] = gpass[i];
+    }
+    __device__ __forceinline__ void opaque() {
+#pragma unroll
+        for (int r = 0; r < NPT * (RL - 1); ++r) asm volatile("" : "+v"(w[r].x), "+v"(w[r].y));
+    }
+};
+
 // Stage the global table into LDS (all NTHREADS threads of the block).
 //   gpass : pass-major table for N (host: pass_twiddles(N)), used when !SPLIT
 //   gtab  : W_N^k, k < N (host: twiddle_table(N)), used when SPLIT

@@ -342,15 +342,17 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
     for (int u = 0; u < MEL_MAX_ROUNDS; ++u) {
         pa[u] = pb[u] = 0.0f;
         const int c = t + T * u;
-        if constexpr (MODE == 3) {
+        if (mel.cw == 0) {   // the chunk windows (log-mel; MFCC where the table fits three workgroups per CU)
             if (c >= nc) continue;
             // log-mel: the chunk's window of lc bins, the same lc for every lane (a
             // uniform loop: scalar trip count, immediate offsets); its zero weights
             // add exact zeros to the (row a, row b) partials, so the sums equal the
             // non-zero range's FMAs in bin order (3.053 -> 2.990 ms, 32 ch x 10 min).
             // Rows lcs = lc + 1 floats apart (odd: the lanes' weight reads fall in
-            // distinct banks).  MFCC keeps the packed table: the windows' larger
-            // table costs it a workgroup per CU (+17 %)
+            // distinct banks).  MFCC takes them where the windows' larger table
+            // still leaves three workgroups per CU (with the register last-pass
+            // twiddles, 6 KB less static LDS: the 40-mel / 13-coefficient plan);
+            // otherwise the packed table (a workgroup per CU fewer: +17 %)
             const float* wr = sW + c * lcs;
             const vf2_t* pp = reinterpret_cast<const vf2_t*>(P) + __float_as_int(wr[lc]);
             vf2_t ab = {0.0f, 0.0f};
@@ -363,7 +365,7 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
             }
             pa[u] = ab.x;
             pb[u] = ab.y;
-        } else if (c < nc) {   // MFCC: the packed layout, each chunk's own length
+        } else if (c < nc) {   // the packed layout, each chunk's own length
             const int lo = sCh[3 * c], len = sCh[3 * c + 1], off = sCh[3 * c + 2];
             vf2_t ab = {0.0f, 0.0f};   // (row a, row b) partials: fma per element, bin order
             const vf2_t* pp = reinterpret_cast<const vf2_t*>(P) + lo;
@@ -537,16 +539,27 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr int XF = RI ? (ri_floats<N>() + 3) / 4 * 2 : G::LDS;   // float2 per transform (16 B multiple)
     constexpr int LDSN = G::NPASS > 1 ? F * XF : 1;
     __shared__ __attribute__((aligned(16))) float2 lds[LDSN];   // 16 B: pass_exchange_ri's b128 writes
+    // N = 1024 one-wave transforms (DIRECT): every last-pass twiddle of a
+    // thread in registers (TwLastRegA: 24 VGPRs), only the first two passes'
+    // 240 entries in LDS -- 6 KB less LDS per workgroup, 12 fewer LDS reads per
+    // pair, the table's own values (bit-identical)
+    // (Not for magnitude rows' VAR 0, the launch of small jobs: config 3's single
+    // 60 s call measured +2 % with the per-workgroup twiddle loads.)
+    constexpr bool RA = DIRECT && N == 1024 && !(MODE == 0 && VAR == 0);
     constexpr int TWE = R2048 ? G::tw_off(G::NPASS - 1) + (G::RL - 1) * (G::ns(G::NPASS - 1) / 2)   // TwLastRegP's
+                        : RA  ? G::tw_off(G::NPASS - 1)
                               : TwLayout<N>::ENTRIES;
     __shared__ float2 ltab[TWE];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
     const TwTab<N> tw{ltab};
-    using TwL = std::conditional_t<R2048, TwLastRegP<N>, TwTab<N>>;
+    using TwL = std::conditional_t<R2048, TwLastRegP<N>, std::conditional_t<RA, TwLastRegA<N, true>, TwTab<N>>>;
     TwL twl{};
     if constexpr (R2048) {
         twl.tab = ltab;
         twl.hi = ltab + Geo<N>::tw_off(Geo<N>::NPASS - 1);
+        twl.load(gpass, (int)threadIdx.x % Geo<N>::T);
+    } else if constexpr (RA) {
+        twl.tab = ltab;
         twl.load(gpass, (int)threadIdx.x % Geo<N>::T);
     }
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
@@ -751,6 +764,8 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     }
     if constexpr (R2048) {   // the passes before the last, and the last pass' upper half
         TwLastRegP<N>::template stage<WG>(ltab, ltab + Geo<N>::tw_off(Geo<N>::NPASS - 1), gpass);
+    } else if constexpr (RA) {   // the passes before the last
+        TwLastRegA<N, true>::template stage<WG>(ltab, gpass);
     } else {
         stage_twiddles<N, WG>(ltab, gpass, gtab);
     }
@@ -875,7 +890,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
         } else {
             load_pair(more ? cn : c, more ? fn : fa);   // last step re-reads its own pair
         }
-        if constexpr (R2048) {
+        if constexpr (R2048 || RA) {
             twl.opaque();
             fft_regs<N, true, true, RI, TwL, false, false, 1>(v, t, my, twl);
         } else {
@@ -1985,16 +2000,31 @@ static hipError_t run_stft_mel(const float* sig, long long n, long long nch, lon
         const long long dp = (a.nnz + (long long)a.cw * a.nc + a.M + 1 + 3) & ~3LL;
         return sizeof(float) * (size_t)(dp + (MODE == 4 ? (long long)a.C * a.M + a.C : 0));
     };
-    // log-mel (MODE 3): the chunk windows (cw = 0); MFCC: the packed chunks
+    // log-mel (MODE 3): the chunk windows (cw = 0); MFCC: the windows too when
+    // they keep the packed table's workgroups per CU, else the packed chunks
     MelArgs mel = mel_in;
+    auto windows = [&](MelArgs& a) {
+        a.W = mel_in.Ww;
+        a.chunks = nullptr;
+        a.cw = 0;
+        a.lc = mel_in.lcw;
+        a.lcs = mel_in.lcw + 1;
+        a.nnz = mel_in.nc * a.lcs;
+    };
+    const bool have_w = mel_in.Ww && mel_in.lcw > 0 && mel_in.lcw % 4 == 0;
     if constexpr (MODE == 3) {
-        if (!mel_in.Ww || mel_in.lcw <= 0 || mel_in.lcw % 4 != 0) return hipErrorNotSupported;
-        mel.W = mel_in.Ww;
-        mel.chunks = nullptr;
-        mel.cw = 0;
-        mel.lc = mel_in.lcw;
-        mel.lcs = mel_in.lcw + 1;
-        mel.nnz = mel_in.nc * mel.lcs;
+        if (!have_w) return hipErrorNotSupported;
+        windows(mel);
+    } else if (have_w && knob(KNOB_MFCC_WIN, 1) != 0) {   // knob MFCC_WIN = 0: the packed chunks (A/B)
+        MelArgs mw = mel_in;
+        windows(mw);
+        int pw = 0, pp = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, (const void*)k_stft_pair<N, MODE, 0>, WG, dyn_of(mw)) ==
+                hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&pp, (const void*)k_stft_pair<N, MODE, 0>, WG,
+                                                         dyn_of(mel_in)) == hipSuccess &&
+            pw >= pp)
+            mel = mw;
     }
     const size_t dyn = dyn_of(mel);
     // knob MEL_R32 = 1 (with POW_R32 = 1, so the fused rows stay bit-identical to

@@ -18,7 +18,7 @@ enum Knob : int {
     KNOB_MIX_CHUNK_MB, KNOB_MIX_R2C_FULL, KNOB_FIR_OLD, KNOB_FIR_DYN, KNOB_FIR_DIRECT_LDS, KNOB_FIR_BLOCK,
     KNOB_HOST_CHUNK_MB, KNOB_NO_MIXED, KNOB_REAL_PROMOTE, KNOB_ISTFT_OLD, KNOB_MEL_FUSED, KNOB_CZT_UNFUSED,
     KNOB_CEPS_UNFUSED, KNOB_FIR_R32, KNOB_DIST_SLAB_KB, KNOB_POW_R32, KNOB_MAG_R32, KNOB_MEL_R32,
-    KNOB_C2C_TPW, KNOB_C2C_ONE, KNOB_REAL_TPW, KNOB_ANA_TPW, KNOB_MIX_TPW, KNOB_C2C_SMALL, KNOB_DCT_SMALL, KNOB_HIL_SMALL, KNOB_REAL_SMALL, KNOB_R2C_SMALL, KNOB_STFT_STAGE, KNOB_STFT_ONE, KNOB_COUNT
+    KNOB_C2C_TPW, KNOB_C2C_ONE, KNOB_REAL_TPW, KNOB_ANA_TPW, KNOB_MIX_TPW, KNOB_C2C_SMALL, KNOB_DCT_SMALL, KNOB_HIL_SMALL, KNOB_REAL_SMALL, KNOB_R2C_SMALL, KNOB_STFT_STAGE, KNOB_STFT_ONE, KNOB_MFCC_WIN, KNOB_COUNT
 };
 long long knob(Knob k, long long dflt);
 // launches of the paths the tests must see taken (vvhip_debug_get("STAT_..."))
