@@ -514,7 +514,9 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr bool CPXD = BULK && MODE == 1 && G::T == 64 && G::NPASS > 1;
     constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
     // floats per transform: hop <= N/2 (MEL: hop <= 256)
-    constexpr int SPAN = GLDS ? (MEL ? N + 256 : N + N / 2) : 1;
+    // (MEL and the ring walk, VAR 3: hop <= 256, so N + 256 floats per span -- for
+    // power rows' VAR 3 that makes 40.8 KB of LDS per workgroup: four per CU)
+    constexpr int SPAN = GLDS ? ((MEL || VAR == 3) ? N + 256 : N + N / 2) : 1;
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
     // written as 16 B/lane stores
@@ -1867,7 +1869,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // 1-2 % slower than with VAR 0's interleaved walk, profiles/r02_kbench_ring.jsonl).
         // knob STFT_RING = 0 / 1 forces VAR 0 / VAR 3 (A/B)
         const long long kring = knob(KNOB_STFT_RING, -1);
-        const bool ring = Geo<N>::T == 64 && hop % 256 == 0 && (kring >= 0 ? kring == 1 : MODE == 2);
+        const bool ring = Geo<N>::T == 64 && hop == 256 && (kring >= 0 ? kring == 1 : MODE == 2);
         // Magnitude and complex rows of large jobs: the persistent dynamic walk (VAR 4) --
         // each wave takes its next pair from a per-(XCD group, slot) counter, so
         // the chip sweeps one moving band of pairs with the load balanced on the
