@@ -516,7 +516,7 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // floats per transform: hop <= N/2 (MEL: hop <= 256)
     // (MEL and the ring walk, VAR 3: hop <= 256, so N + 256 floats per span -- for
     // power rows' VAR 3 that makes 40.8 KB of LDS per workgroup: four per CU)
-    constexpr int SPAN = GLDS ? ((MEL || VAR == 3) ? N + 256 : N + N / 2) : 1;
+    constexpr int SPAN = GLDS ? ((MEL || VAR == 3 || VAR == 5) ? N + 256 : N + N / 2) : 1;
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
     // written as 16 B/lane stores
@@ -1930,7 +1930,7 @@ static hipError_t run_stft(const float* sig, long long n, long long nch, long lo
         // knob STFT_DYN = 1 / 2 forces VAR 4 / VAR 5 (A/B)
         const bool dring = kdyn >= 0 ? kdyn == 2 : MODE == 0;
         if (dyn) stat_inc(STAT_STFT_DYN);
-        if (dyn && dring && hop % 256 == 0) {
+        if (dyn && dring && hop == 256) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 5>, 5, 0LL, ppc);
         } else if (dyn) {
             if constexpr (Geo<N>::T == 64) launch(k_stft_pair<N, MODE, 4>, 4, 0LL, ppc);
