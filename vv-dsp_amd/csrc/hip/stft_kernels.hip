@@ -342,7 +342,7 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
     for (int u = 0; u < MEL_MAX_ROUNDS; ++u) {
         pa[u] = pb[u] = 0.0f;
         const int c = t + T * u;
-        if (mel.cw == 0) {   // the chunk windows (log-mel; MFCC where the table fits three workgroups per CU)
+        if (MODE == 3 || mel.cw == 0) {   // the chunk windows (log-mel; MFCC where the table fits three workgroups per CU)
             if (c >= nc) continue;
             // log-mel: the chunk's window of lc bins, the same lc for every lane (a
             // uniform loop: scalar trip count, immediate offsets); its zero weights
