@@ -71,7 +71,8 @@ def test_stft_device_short_signal_writes_every_bin(vdev, orc, nfft, hop, n):
 
 @pytest.mark.parametrize("nfft,hop", [(256, 64), (256, 100), (4096, 1024), (4096, 441)])
 def test_stft_mirror_through_lds_all_row_kinds(vdev, orc, nfft, hop):
-    """nfft 256 / 4096 (k_stft_pair_lds: the mirror bins read back through LDS):
+    """nfft 256 / 4096 (the mirror bins read back through LDS; 4096 magnitude rows
+    on k_stft_one, its complex and power rows on k_stft_pair_lds):
     magnitude, complex and power rows of a multi-channel ragged job against
     NumPy f64 at the harness tolerance; magnitude rows equal |complex rows|
     and the power rows |complex rows|^2 of bins 0..nfft/2."""
@@ -92,5 +93,9 @@ def test_stft_mirror_through_lds_all_row_kinds(vdev, orc, nfft, hop):
         np.testing.assert_allclose(mag[c], np.abs(X), rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))
         np.testing.assert_allclose(cpx[c], X, rtol=5e-5, atol=5e-5 * np.sqrt(nfft / 1024))
         np.testing.assert_allclose(pw[c], np.abs(X[:, :nfft // 2 + 1]) ** 2, rtol=1e-4, atol=1e-4 * nfft)
-    np.testing.assert_allclose(mag, np.abs(cpx), rtol=2e-6, atol=1e-6 * np.sqrt(nfft / 1024))
+    # nfft 4096 magnitude rows come from k_stft_one (its last-pass twiddles are
+    # other f32 roundings of the same values), the complex rows from
+    # k_stft_pair_lds: equal up to f32 transform error, not to the last ulp
+    mtol = (5e-5, 5e-5) if nfft == 4096 else (2e-6, 1e-6 * np.sqrt(nfft / 1024))
+    np.testing.assert_allclose(mag, np.abs(cpx), rtol=mtol[0], atol=mtol[1])
     np.testing.assert_allclose(pw, np.abs(cpx[..., :nfft // 2 + 1]) ** 2, rtol=1e-5, atol=1e-6 * nfft)
