@@ -34,6 +34,14 @@
 #include <cstdint>
 #include <cstdlib>
 
+// N = 2048 magnitude rows (R2048): both last-pass butterflies' twiddles in
+// registers (TwLastRegA, 166 VGPRs, three waves per SIMD as before) instead of
+// TwLastRegP's mirror half read from LDS: -1.5 %, bit-identical
+// (profiles/r06_ab_twregs_mfcc_windows.jsonl); 0 restores TwLastRegP (A/B)
+#ifndef VVH_R2048_RA
+#define VVH_R2048_RA 1
+#endif
+
 namespace vvh {
 
 // samples e = t + r*T of one frame (zero outside [0, n); all zero when !valid).
@@ -547,21 +555,21 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     // pair, the table's own values (bit-identical)
     // (Not for magnitude rows' VAR 0, the launch of small jobs: config 3's single
     // 60 s call measured +2 % with the per-workgroup twiddle loads.)
-    constexpr bool RA = DIRECT && N == 1024 && !(MODE == 0 && VAR == 0);
-    constexpr int TWE = R2048 ? G::tw_off(G::NPASS - 1) + (G::RL - 1) * (G::ns(G::NPASS - 1) / 2)   // TwLastRegP's
-                        : RA  ? G::tw_off(G::NPASS - 1)
-                              : TwLayout<N>::ENTRIES;
+    constexpr bool RA = (DIRECT && N == 1024 && !(MODE == 0 && VAR == 0)) || (R2048 && VVH_R2048_RA);
+    constexpr int TWE = RA       ? G::tw_off(G::NPASS - 1)
+                        : R2048 ? G::tw_off(G::NPASS - 1) + (G::RL - 1) * (G::ns(G::NPASS - 1) / 2)   // TwLastRegP's
+                                : TwLayout<N>::ENTRIES;
     __shared__ float2 ltab[TWE];
     __shared__ float span_all[GLDS ? F * SPAN : 1];
     const TwTab<N> tw{ltab};
-    using TwL = std::conditional_t<R2048, TwLastRegP<N>, std::conditional_t<RA, TwLastRegA<N, true>, TwTab<N>>>;
+    using TwL = std::conditional_t<RA, TwLastRegA<N, true>, std::conditional_t<R2048, TwLastRegP<N>, TwTab<N>>>;
     TwL twl{};
-    if constexpr (R2048) {
+    if constexpr (RA) {
+        twl.tab = ltab;
+        twl.load(gpass, (int)threadIdx.x % Geo<N>::T);
+    } else if constexpr (R2048) {
         twl.tab = ltab;
         twl.hi = ltab + Geo<N>::tw_off(Geo<N>::NPASS - 1);
-        twl.load(gpass, (int)threadIdx.x % Geo<N>::T);
-    } else if constexpr (RA) {
-        twl.tab = ltab;
         twl.load(gpass, (int)threadIdx.x % Geo<N>::T);
     }
     const int lt = threadIdx.x, slot = lt / G::T, t = lt % G::T;
@@ -764,10 +772,10 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
             if (any && pn < pairs) grab();   // -> the pair after pn
         }
     }
-    if constexpr (R2048) {   // the passes before the last, and the last pass' upper half
-        TwLastRegP<N>::template stage<WG>(ltab, ltab + Geo<N>::tw_off(Geo<N>::NPASS - 1), gpass);
-    } else if constexpr (RA) {   // the passes before the last
+    if constexpr (RA) {   // the passes before the last
         TwLastRegA<N, true>::template stage<WG>(ltab, gpass);
+    } else if constexpr (R2048) {   // the passes before the last, and the last pass' upper half
+        TwLastRegP<N>::template stage<WG>(ltab, ltab + Geo<N>::tw_off(Geo<N>::NPASS - 1), gpass);
     } else {
         stage_twiddles<N, WG>(ltab, gpass, gtab);
     }
