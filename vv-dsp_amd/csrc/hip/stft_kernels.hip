@@ -1387,7 +1387,7 @@ k_stft_stage(const float* sig, long long n, long long nch, long long ch_stride, 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int e = 4 * lane + 256 * u;
-            pre[u] = e < span ? __builtin_nontemporal_load(s + (e >> 2)) : vf4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            pre[u] = e < span ? s[e >> 2] : vf4_t{0.0f, 0.0f, 0.0f, 0.0f};   // plain loads: the span overlaps the next wave's (L2)
         }
     };
     bool stg = p0 < p_end && staged_ok(p0);
