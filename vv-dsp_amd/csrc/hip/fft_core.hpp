@@ -483,6 +483,21 @@ __device__ __forceinline__ void pass_compute(float2* v, int t, const TW& tw) {
 }
 
 // Exchange after pass p: scatter outputs of pass p, gather inputs of pass p+1.
+// Padding of the complex (b64) exchange after pass p: Geo<N>::pad, except the
+// second exchange of N = 4096 (passes 16, 16, 16), where e + (e >> 9) makes the
+// reads conflict-free (Geo::pad: 128 extra LDS cycles per wave and transform;
+// host model in tests/test_lds_banks.py); inside Geo<4096>::LDS float2.
+template <int N, int p>
+__host__ __device__ constexpr int cx_pad(int e) {
+    if constexpr (N == 4096 && p == 1) return e + (e >> 9);
+    else return Geo<N>::pad(e);
+}
+__host__ __device__ constexpr bool cx_pad_check() {
+    for (int e = 1; e < 4096; ++e)
+        if (cx_pad<4096, 1>(e) <= cx_pad<4096, 1>(e - 1)) return false;
+    return cx_pad<4096, 1>(4095) < Geo<4096>::LDS;
+}
+static_assert(cx_pad_check(), "cx_pad<4096, 1>");
 template <int N, int p, bool PAIRED>
 __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
     using G = Geo<N>;
@@ -492,14 +507,14 @@ __device__ __forceinline__ void pass_exchange(float2* v, int t, float2* lds) {
         const int b = bfly<N, p, PAIRED>(t, i);
         const int base = (b / Ns) * Ns * R + (b % Ns);
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[G::pad(base + r * Ns)] = v[i * R + r];
+        for (int r = 0; r < R; ++r) lds[cx_pad<N, p>(base + r * Ns)] = v[i * R + r];
     }
     xsync<G::T>();
 #pragma unroll
     for (int i = 0; i < G::P / R2; ++i) {
         const int b = bfly<N, p + 1, PAIRED>(t, i);
 #pragma unroll
-        for (int r = 0; r < R2; ++r) v[i * R2 + r] = lds[G::pad(b + r * (N / R2))];
+        for (int r = 0; r < R2; ++r) v[i * R2 + r] = lds[cx_pad<N, p>(b + r * (N / R2))];
     }
     if constexpr (G::T > 64) xsync<G::T>();   // next pass' writes must not race these reads
 }
@@ -530,10 +545,19 @@ __host__ __device__ constexpr int ri_floats() {
 #ifndef VVH_RI_B128
 #define VVH_RI_B128 1
 #endif
+// N = 2048 (passes 16, 16, 8; T = 128, mirror-paired last pass): e + (e >> 4)
+// left a 2-way conflict in every 32-lane group of each exchange read (lane 31's
+// b + (b >> 4) wraps onto lane 0's bank: 256 extra LDS cycles per frame pair,
+// half the kernel's LDS-array time, SQ_LDS_BANK_CONFLICT in
+// profiles/r06_pmc_stft256_2048_pow.txt); these per-pass pads are conflict-free
+// for both the writes and the reads (a host model of every access,
+// tests/test_lds_banks.py) and stay inside Geo<2048>::LDS floats.
 template <int N, int p>
 __host__ __device__ constexpr int ri_pad(int e) {
     if constexpr (N == 1024 && p == 0) return VVH_RI_B128 ? e + 4 * (e >> 5) : e + (e >> 5);
     else if constexpr (N == 1024 && p == 1) return e + 4 * (e >> 7) + 8 * (e >> 8);
+    else if constexpr (N == 2048 && p == 0) return e + (e >> 5);
+    else if constexpr (N == 2048 && p == 1) return e + 16 * (e >> 8);
     else return Geo<N>::pad(e);
 }
 
@@ -581,6 +605,13 @@ __host__ __device__ constexpr bool ri1024_check() {
     return ri_pad<1024, 0>(1023) < 1148 && ri_pad<1024, 1>(1023) < 1148;
 }
 static_assert(ri1024_check(), "Ri1024 decomposition of ri_pad");
+// the N = 2048 / 4096 paddings: strictly increasing (one-to-one) and inside the buffer
+__host__ __device__ constexpr bool pads_check() {
+    for (int e = 1; e < 2048; ++e)
+        if (ri_pad<2048, 0>(e) <= ri_pad<2048, 0>(e - 1) || ri_pad<2048, 1>(e) <= ri_pad<2048, 1>(e - 1)) return false;
+    return ri_pad<2048, 0>(2047) < ri_floats<2048>() && ri_pad<2048, 1>(2047) < ri_floats<2048>();
+}
+static_assert(pads_check(), "ri_pad<2048, p>");
 
 template <int BASE, int STEP>
 __device__ __forceinline__ void lds_rd32x16(const float* base, float* o);
