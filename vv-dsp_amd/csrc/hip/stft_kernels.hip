@@ -1399,7 +1399,24 @@ k_stft_stage(const float* sig, long long n, long long nch, long long ch_stride, 
         const bool hb = fa + 1 < frames;
         float xa[G::P], xb[G::P];
         const bool stg0 = stg;
-        if (stg0) {
+        if (stg0 && hop == 64) {
+            // hop 64 (nfft / 4): the span laid out with 16 floats of pad per 128, so
+            // the four slots' frames (128 floats apart) read from four distinct bank
+            // quarters: unpadded, slots ws and ws + 1 of a 32-lane group hit the
+            // same 16 banks on every frame read (a 2-way conflict per instruction)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (4 * lane + 256 * u < span)
+                    *reinterpret_cast<vf4_t*>(wb + 4 * lane + 256 * u + 16 * (lane >> 5) + 32 * u) = pre[u];
+            xsync<64>();
+            const float* fsa = wb + 144 * ws + t;   // element e at e + 16 (e >> 7)
+#pragma unroll
+            for (int r = 0; r < G::P; ++r) {
+                xa[r] = fsa[T * r + 16 * (r >> 3)];
+                xb[r] = fsa[64 + T * r + 16 * ((r + 4) >> 3)];
+            }
+            xsync<64>();
+        } else if (stg0) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (4 * lane + 256 * u < span) *reinterpret_cast<vf4_t*>(wb + 4 * lane + 256 * u) = pre[u];
