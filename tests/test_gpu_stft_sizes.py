@@ -93,7 +93,7 @@ def test_stft_mirror_post_complex_rows(nfft):
 
 
 @pytest.mark.parametrize("nch,n", [(8, 20 * 48000 + 77), (3, 4096 * 9 + 1), (1, 48000 * 30), (5, 4096 + 1024 * 3),
-                                   (2, 5000)])
+                                   (2, 5000), (2, 1000), (3, 1), (1, 4096)])
 def test_stft4096_one_pair_per_slot(nch, n):
     """nfft 4096 magnitude rows on k_stft_one (one frame pair per transform slot,
     no loop; last-pass twiddles as powers in registers) against k_stft_pair_lds
