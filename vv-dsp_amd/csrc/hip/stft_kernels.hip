@@ -522,8 +522,10 @@ k_stft_pair(const float* sig, long long n, long long nch, long long ch_stride, l
     constexpr bool CPXD = BULK && MODE == 1 && G::T == 64 && G::NPASS > 1;
     constexpr bool GLDS = (STAGE || POWD || CPXD) && G::T >= 64;   // input spans by LDS-DMA (launcher checks hop/alignment)
     // floats per transform: hop <= N/2 (MEL: hop <= 256)
-    // (MEL and the ring walk, VAR 3: hop <= 256, so N + 256 floats per span -- for
-    // power rows' VAR 3 that makes 40.8 KB of LDS per workgroup: four per CU)
+    // (MEL: hop <= 256; the ring walks VAR 3 / VAR 5: hop == 256 -- so N + 256
+    // floats per span; for the ring walks that makes 40.8 KB of LDS per workgroup
+    // with the register last-pass twiddles: four per CU, -2.5 % for power rows,
+    // -2..-3 % for the headline's magnitude rows)
     constexpr int SPAN = GLDS ? ((MEL || VAR == 3 || VAR == 5) ? N + 256 : N + N / 2) : 1;
     // T == 64 (one wave per transform): magnitudes go straight from registers as
     // full-line dword stores (DIRECT); otherwise they are staged through LDS and
