@@ -10,6 +10,7 @@
 #include "../../../include/vv_dsp_hip.h"
 #include "vvhip_internal.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -18,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <algorithm>
 #include <vector>
 
 using namespace vvh;
@@ -1441,20 +1443,58 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
     // the fused kernels' layout (MelArgs): chunk c's window of lc bins [lo', lo' + lc),
     // lo' = min(lo, nbins - lc) so it stays inside the row, as a row of lc + 1 floats
     // (weights of the chunk's own bins, zeros elsewhere, then lo' as int bits)
+    // Bank-aware order: the kernel's 64 lanes read their windows' power pairs in
+    // lockstep (one ds_read_b64 per bin step, banks (2 start) mod 64 per 32-lane
+    // group), so chunks whose windows start on the same bank residue (start mod 32)
+    // conflict.  Each window may start anywhere in [lo + len - lc, lo] (inside the
+    // row) -- extra leading / trailing zero weights add exact zeros, so the sums
+    // are bit-identical -- and any chunk may sit in any lane slot, since each slot
+    // writes its partial to its chunk's own index (the row's last float: start |
+    // chunk << 16).  Greedy: chunks with the least slack first, each to the
+    // (32-lane group, start) with the fewest windows on that residue.  The
+    // 40-mel / 1024-point plan: 5 -> 2 extra LDS cycles per bin step.
     std::vector<float> wf;
-    if (fb && m->nc > 0 && lc % 4 == 0 && lc <= (int)nbins) {
-        const int lcs = lc + 1;
-        wf.assign((size_t)m->nc * lcs, 0.0f);
-        for (int c = 0; c < m->nc; ++c) {
-            const int lo = chunks[3 * c], len = chunks[3 * c + 1], off = chunks[3 * c + 2];
-            const int lo2 = lo < (int)nbins - lc ? lo : (int)nbins - lc;
-            for (int j = 0; j < lc; ++j) {
-                const int k = lo2 + j;
-                if (k >= lo && k < lo + len) wf[(size_t)c * lcs + j] = w[(size_t)off + (k - lo)];
+    if (fb && m->nc > 0 && lc % 4 == 0 && lc <= (int)nbins && m->nc < 32768 && nbins < 65536) {
+        const int lcs = lc + 1, nc = m->nc, ng = (nc + 31) / 32, nb = (int)nbins;
+        std::vector<int> order(nc), used((size_t)ng * 32, 0), cnt(ng, 0), slot_chunk(nc), slot_start(nc);
+        std::vector<std::vector<int>> members(ng);
+        auto smin = [&](int c) { const int v = chunks[3 * c] + chunks[3 * c + 1] - lc; return v > 0 ? v : 0; };
+        auto smax = [&](int c) { return chunks[3 * c] < nb - lc ? chunks[3 * c] : nb - lc; };
+        for (int c = 0; c < nc; ++c) order[c] = c;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int a, int b) { return smax(a) - smin(a) < smax(b) - smin(b); });
+        std::vector<int> start(nc);
+        for (int c : order) {
+            int bg = -1, bs = 0, bu = 0, bn = 0;
+            for (int g = 0; g < ng; ++g) {
+                if (cnt[g] >= (nc - 32 * g < 32 ? nc - 32 * g : 32)) continue;
+                for (int st = smax(c); st >= smin(c); --st) {
+                    const int u = used[(size_t)g * 32 + st % 32];
+                    if (bg < 0 || u < bu || (u == bu && cnt[g] < bn)) {
+                        bg = g;
+                        bs = st;
+                        bu = u;
+                        bn = cnt[g];
+                    }
+                }
             }
-            int bits = lo2;
-            std::memcpy(&wf[(size_t)c * lcs + lc], &bits, sizeof bits);
+            ++used[(size_t)bg * 32 + bs % 32];
+            ++cnt[bg];
+            members[bg].push_back(c);
+            start[c] = bs;
         }
+        wf.assign((size_t)nc * lcs, 0.0f);
+        for (int g = 0, slot = 0; g < ng; ++g)
+            for (int c : members[g]) {
+                const int lo = chunks[3 * c], len = chunks[3 * c + 1], off = chunks[3 * c + 2], st = start[c];
+                for (int j = 0; j < lc; ++j) {
+                    const int k = st + j;
+                    if (k >= lo && k < lo + len) wf[(size_t)slot * lcs + j] = w[(size_t)off + (k - lo)];
+                }
+                const int bits = st | (c << 16);
+                std::memcpy(&wf[(size_t)slot * lcs + lc], &bits, sizeof bits);
+                ++slot;
+            }
         m->lc = lc;
     }
     // DCT-II rows cos(pi (j + 1/2) i / M) (dct.c:21-30), and the lifter of mel.c:300-302

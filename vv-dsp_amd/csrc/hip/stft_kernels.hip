@@ -346,10 +346,12 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
     constexpr int T = 64;
     const int nc = mel.nc, M = mel.M, C = mel.C, lc = mel.lc, lcs = mel.lcs;
     float pa[MEL_MAX_ROUNDS], pb[MEL_MAX_ROUNDS];
+    int dc[MEL_MAX_ROUNDS];   // the chunk a slot computes (windows: the host's bank-aware order)
 #pragma unroll
     for (int u = 0; u < MEL_MAX_ROUNDS; ++u) {
         pa[u] = pb[u] = 0.0f;
         const int c = t + T * u;
+        dc[u] = c;
         if (MODE == 3 || mel.cw == 0) {   // the chunk windows (log-mel; MFCC where the table fits three workgroups per CU)
             if (c >= nc) continue;
             // log-mel: the chunk's window of lc bins, the same lc for every lane (a
@@ -362,7 +364,9 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
             // twiddles, 6 KB less static LDS: the 40-mel / 13-coefficient plan);
             // otherwise the packed table (a workgroup per CU fewer: +17 %)
             const float* wr = sW + c * lcs;
-            const vf2_t* pp = reinterpret_cast<const vf2_t*>(P) + __float_as_int(wr[lc]);
+            const int bits = __float_as_int(wr[lc]);   // window start | chunk << 16
+            dc[u] = bits >> 16;
+            const vf2_t* pp = reinterpret_cast<const vf2_t*>(P) + (bits & 0xffff);
             vf2_t ab = {0.0f, 0.0f};
             for (int j = 0; j < lc; j += 4) {
 #pragma unroll
@@ -394,7 +398,7 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
 #pragma unroll
     for (int u = 0; u < MEL_MAX_ROUNDS; ++u) {
         const int c = t + T * u;
-        if (c < nc) *reinterpret_cast<vf2_t*>(P + 2 * c) = vf2_t{pa[u], pb[u]};
+        if (c < nc) *reinterpret_cast<vf2_t*>(P + 2 * dc[u]) = vf2_t{pa[u], pb[u]};
     }
     xsync<T>();
     const vf2_t* part = reinterpret_cast<const vf2_t*>(P);
