@@ -1455,7 +1455,7 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
     // 40-mel / 1024-point plan: 5 -> 2 extra LDS cycles per bin step.
     std::vector<float> wf;
     if (fb && m->nc > 0 && lc % 4 == 0 && lc <= (int)nbins && m->nc < 32768 && nbins < 65536) {
-        const int lcs = lc + 1, nc = m->nc, ng = (nc + 31) / 32, nb = (int)nbins;
+        const int lcs = MelArgs::window_stride(lc), nc = m->nc, ng = (nc + 31) / 32, nb = (int)nbins;
         std::vector<int> order(nc), used((size_t)ng * 32, 0), cnt(ng, 0), slot_chunk(nc), slot_start(nc);
         std::vector<std::vector<int>> members(ng);
         auto smin = [&](int c) { const int v = chunks[3 * c] + chunks[3 * c + 1] - lc; return v > 0 ? v : 0; };

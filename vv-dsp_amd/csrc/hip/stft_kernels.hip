@@ -358,8 +358,10 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
             // uniform loop: scalar trip count, immediate offsets); its zero weights
             // add exact zeros to the (row a, row b) partials, so the sums equal the
             // non-zero range's FMAs in bin order (3.053 -> 2.990 ms, 32 ch x 10 min).
-            // Rows lcs = lc + 1 floats apart (odd: the lanes' weight reads fall in
-            // distinct banks).  MFCC takes them where the windows' larger table
+            // Rows lcs = window_stride(lc) floats apart (16 B aligned, lcs / 4 odd: a
+            // lane's four weights are one ds_read_b128 and the lanes' reads cover
+            // distinct bank blocks; the host deals the chunks to lanes so that the
+            // power reads' start banks collide least).  MFCC takes them where the windows' larger table
             // still leaves three workgroups per CU (with the register last-pass
             // twiddles, 6 KB less static LDS: the 40-mel / 13-coefficient plan);
             // otherwise the packed table (a workgroup per CU fewer: +17 %)
@@ -369,11 +371,9 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
             const vf2_t* pp = reinterpret_cast<const vf2_t*>(P) + (bits & 0xffff);
             vf2_t ab = {0.0f, 0.0f};
             for (int j = 0; j < lc; j += 4) {
+                const vf4_t wq = *reinterpret_cast<const vf4_t*>(wr + j);   // rows 16 B aligned (lcs % 4 == 0)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float w = wr[j + i];
-                    ab = __builtin_elementwise_fma(pp[j + i], vf2_t{w, w}, ab);
-                }
+                for (int i = 0; i < 4; ++i) ab = __builtin_elementwise_fma(pp[j + i], vf2_t{wq[i], wq[i]}, ab);
             }
             pa[u] = ab.x;
             pb[u] = ab.y;
@@ -2041,7 +2041,7 @@ static hipError_t run_stft_mel(const float* sig, long long n, long long nch, lon
         a.chunks = nullptr;
         a.cw = 0;
         a.lc = mel_in.lcw;
-        a.lcs = mel_in.lcw + 1;
+        a.lcs = MelArgs::window_stride(mel_in.lcw);
         a.nnz = mel_in.nc * a.lcs;
     };
     const bool have_w = mel_in.Ww && mel_in.lcw > 0 && mel_in.lcw % 4 == 0;

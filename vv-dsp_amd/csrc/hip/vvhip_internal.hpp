@@ -145,12 +145,16 @@ struct MelArgs {
     const float* lift = nullptr;   // lifter factors [C]
     int nnz = 0, nc = 0, M = 0, C = 0;
     // The layout the kernel reads: cw = 3 -- W packed with the chunk table above;
-    // cw = 0 -- each chunk's window of lc bins as a row of lcs = lc + 1 floats in W,
+    // cw = 0 -- each chunk's window of lc bins as a row of lcs = window_stride(lc) floats in W,
     // [c lcs + j] the weight of bin lo_c + j (zero outside the chunk), [c lcs + lc]
     // lo_c's bits, the window inside the row (lo_c + lc <= n/2 + 1), lc % 4 == 0, no
     // chunk table.  The plan passes the packed layout plus the windows (Ww, lcw);
     // launch_stft_mel gives log-mel the windows and MFCC the packed layout.
     int lc = 0, lcs = 0, cw = 3;
+    // row stride of the chunk windows for lc bins (lc % 4 == 0): the first multiple
+    // of 4 above lc whose quarter is odd, so 16 lanes' 16 B weight reads (rows
+    // lcs floats apart) cover 16 distinct 4-bank blocks
+    static constexpr int window_stride(int lc) { return (lc / 4) % 2 == 0 ? lc + 4 : lc + 8; }
     const float* Ww = nullptr;
     int lcw = 0;
     float eps = 0.0f;
