@@ -1454,12 +1454,20 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
     // (32-lane group, start) with the fewest windows on that residue.  The
     // 40-mel / 1024-point plan: 5 -> 2 extra LDS cycles per bin step.
     std::vector<float> wf;
-    if (fb && m->nc > 0 && lc % 4 == 0 && lc <= (int)nbins && m->nc < 32768 && nbins < 65536) {
-        const int lcs = MelArgs::window_stride(lc), nc = m->nc, ng = (nc + 31) / 32, nb = (int)nbins;
-        std::vector<int> order(nc), used((size_t)ng * 32, 0), cnt(ng, 0), slot_chunk(nc), slot_start(nc);
+    // With MelArgs::W2 the windows are lc + 4 bins (slack >= 4 for every chunk) and
+    // start on even bins (two bins per ds_read_b128: 16-lane read groups)
+    const int lcw = MelArgs::W2 ? lc + 4 : lc, GL = MelArgs::W2 ? 16 : 32, SS = MelArgs::W2 ? 2 : 1;
+    if (fb && m->nc > 0 && lc % 4 == 0 && lcw <= (int)nbins && m->nc < 32768 && nbins < 65536 &&
+        (!MelArgs::W2 || nbins == 513)) {   // W2: the fused kernel's rows (nfft 1024) only
+        const int lc = lcw;   // the windows' length from here on
+        const int lcs = MelArgs::window_stride(lc), nc = m->nc, ng = (nc + GL - 1) / GL, nb = (int)nbins;
+        std::vector<int> order(nc), used((size_t)ng * 32, 0), cnt(ng, 0);
         std::vector<std::vector<int>> members(ng);
         auto smin = [&](int c) { const int v = chunks[3 * c] + chunks[3 * c + 1] - lc; return v > 0 ? v : 0; };
-        auto smax = [&](int c) { return chunks[3 * c] < nb - lc ? chunks[3 * c] : nb - lc; };
+        // W2: a window may reach 3 bins past the row (the kernel zeroes P's bins nb ..
+        // nb + 2), so even the last chunk has an even start
+        const int top = MelArgs::W2 ? nb + 3 - lc : nb - lc;
+        auto smax = [&](int c) { return chunks[3 * c] < top ? chunks[3 * c] : top; };
         for (int c = 0; c < nc; ++c) order[c] = c;
         std::stable_sort(order.begin(), order.end(),
                          [&](int a, int b) { return smax(a) - smin(a) < smax(b) - smin(b); });
@@ -1467,8 +1475,8 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
         for (int c : order) {
             int bg = -1, bs = 0, bu = 0, bn = 0;
             for (int g = 0; g < ng; ++g) {
-                if (cnt[g] >= (nc - 32 * g < 32 ? nc - 32 * g : 32)) continue;
-                for (int st = smax(c); st >= smin(c); --st) {
+                if (cnt[g] >= (nc - GL * g < GL ? nc - GL * g : GL)) continue;
+                for (int st = smax(c) / SS * SS; st >= smin(c); st -= SS) {
                     const int u = used[(size_t)g * 32 + st % 32];
                     if (bg < 0 || u < bu || (u == bu && cnt[g] < bn)) {
                         bg = g;
@@ -1478,11 +1486,15 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
                     }
                 }
             }
+            if (bg < 0) break;   // no start (cannot happen for lc <= nbins): no windows
             ++used[(size_t)bg * 32 + bs % 32];
             ++cnt[bg];
             members[bg].push_back(c);
             start[c] = bs;
         }
+        size_t placed = 0;
+        for (const auto& g : members) placed += g.size();
+        if (placed == (size_t)nc) {
         wf.assign((size_t)nc * lcs, 0.0f);
         for (int g = 0, slot = 0; g < ng; ++g)
             for (int c : members[g]) {
@@ -1496,6 +1508,7 @@ int vvhip_mel_create(const float* fb, size_t n_mels, size_t nbins, size_t n_coef
                 ++slot;
             }
         m->lc = lc;
+        }
     }
     // DCT-II rows cos(pi (j + 1/2) i / M) (dct.c:21-30), and the lifter of mel.c:300-302
     std::vector<float> D(n_coeffs * n_mels), L(n_coeffs, 1.0f);

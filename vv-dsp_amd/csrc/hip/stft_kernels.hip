@@ -324,7 +324,14 @@ __device__ __forceinline__ void mel_rows(const float2* v, int t, float* fa, floa
             }
         }
     });
-    if (t == 0) put(N / 2, ea[0][R / 2], eb[0][R / 2]);
+    if (t == 0) {
+        put(N / 2, ea[0][R / 2], eb[0][R / 2]);
+        if constexpr (MelArgs::W2) {   // bins N/2 + 1 .. N/2 + 3: zeros under the last windows' tails
+            put(N / 2 + 1, 0.0f, 0.0f);
+            put(N / 2 + 2, 0.0f, 0.0f);
+            put(N / 2 + 3, 0.0f, 0.0f);
+        }
+    }
     xsync<T>();
     mel_tail<MODE, true>(t, P, fa, fb, has_b, sink, sW, sCh, sCb, sD, sL, mel);
 }
@@ -370,10 +377,22 @@ __device__ __forceinline__ void mel_tail(int t, float* P, float* fa, float* fb, 
             dc[u] = bits >> 16;
             const vf2_t* pp = reinterpret_cast<const vf2_t*>(P) + (bits & 0xffff);
             vf2_t ab = {0.0f, 0.0f};
-            for (int j = 0; j < lc; j += 4) {
-                const vf4_t wq = *reinterpret_cast<const vf4_t*>(wr + j);   // rows 16 B aligned (lcs % 4 == 0)
+            if constexpr (MelArgs::W2) {   // even starts: two bins' (row a, row b) pairs per 16 B read
+                const vf4_t* p4 = reinterpret_cast<const vf4_t*>(pp);
+                for (int j = 0; j < lc; j += 4) {
+                    const vf4_t wq = *reinterpret_cast<const vf4_t*>(wr + j);
+                    const vf4_t q0 = p4[j / 2], q1 = p4[j / 2 + 1];
+                    ab = __builtin_elementwise_fma(vf2_t{q0[0], q0[1]}, vf2_t{wq[0], wq[0]}, ab);
+                    ab = __builtin_elementwise_fma(vf2_t{q0[2], q0[3]}, vf2_t{wq[1], wq[1]}, ab);
+                    ab = __builtin_elementwise_fma(vf2_t{q1[0], q1[1]}, vf2_t{wq[2], wq[2]}, ab);
+                    ab = __builtin_elementwise_fma(vf2_t{q1[2], q1[3]}, vf2_t{wq[3], wq[3]}, ab);
+                }
+            } else {
+                for (int j = 0; j < lc; j += 4) {
+                    const vf4_t wq = *reinterpret_cast<const vf4_t*>(wr + j);   // rows 16 B aligned (lcs % 4 == 0)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ab = __builtin_elementwise_fma(pp[j + i], vf2_t{wq[i], wq[i]}, ab);
+                    for (int i = 0; i < 4; ++i) ab = __builtin_elementwise_fma(pp[j + i], vf2_t{wq[i], wq[i]}, ab);
+                }
             }
             pa[u] = ab.x;
             pb[u] = ab.y;
@@ -1529,7 +1548,9 @@ k_stft_stage(const float* sig, long long n, long long nch, long long ch_stride, 
 // tables ride in dynamic LDS, so these modes take 8 transform slots per
 // workgroup (512 threads, one workgroup and two waves per SIMD per CU) instead of
 // two workgroups of 4: the same occupancy with one copy of the tables.
-constexpr int R33_BUF = 33 * R32_ROW;   // 33 rows: the mirror read of lane 0 touches row 32
+// 33 rows: the mirror read of lane 0 touches row 32; + 1 keeps every buffer 16 B
+// aligned (the mel tail's 16 B reads of the power pairs in it)
+constexpr int R33_BUF = 33 * R32_ROW + 1;
 template <int MODE>
 __global__ void __launch_bounds__(MODE >= 3 ? 512 : 256, MODE >= 3 ? 1 : 2)
 k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, long long frames, const float* win,
@@ -1772,7 +1793,13 @@ k_stft_r32(const float* sig, long long n, long long nch, long long ch_stride, lo
             }
             float2 na, nb;   // bin 512: Z[512] is its own mirror (lane 0, register 16)
             pair_post<2>(v[16], v[16], &na, &nb);
-            if (m == 0) *reinterpret_cast<vf2_t*>(P + 2 * (N / 2)) = vf2_t{na.x, nb.x};
+            if (m == 0) {
+                *reinterpret_cast<vf2_t*>(P + 2 * (N / 2)) = vf2_t{na.x, nb.x};
+                if constexpr (MelArgs::W2) {   // zeros under the last windows' tails (as mel_rows)
+#pragma unroll
+                    for (int z = 1; z <= 3; ++z) *reinterpret_cast<vf2_t*>(P + 2 * (N / 2 + z)) = vf2_t{0.0f, 0.0f};
+                }
+            }
             xsync<64>();
             const int* mi = reinterpret_cast<const int*>(mel_lds);
             for (int h = 0; h < 2; ++h) {   // the two pairs in turn, each over the whole wave

@@ -155,6 +155,13 @@ struct MelArgs {
     // of 4 above lc whose quarter is odd, so 16 lanes' 16 B weight reads (rows
     // lcs floats apart) cover 16 distinct 4-bank blocks
     static constexpr int window_stride(int lc) { return (lc / 4) % 2 == 0 ? lc + 4 : lc + 8; }
+#ifndef VVH_MEL_W2
+#define VVH_MEL_W2 1
+#endif
+    // VVH_MEL_W2: the chunk windows are 4 bins longer than the chunk schedule's
+    // lc and start on even bins, so the kernel reads their power pairs two bins
+    // per ds_read_b128 (half the read instructions; the 4 extra bins weigh 0)
+    static constexpr bool W2 = VVH_MEL_W2;
     const float* Ww = nullptr;
     int lcw = 0;
     float eps = 0.0f;
