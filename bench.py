@@ -524,6 +524,51 @@ def stft_sizes_leg(ch=CH_SHARD, reps=20, sizes=STFT_SIZES):
     return res
 
 
+def features_leg(ch=CH_SHARD, reps=20, n_mels=40, n_coeffs=13):
+    """SURVEY §8 f1 / f3 on config 5's per-GPU shard (32 ch x 10 min @ 48 kHz, 1024 Hann, hop 256): power rows
+    [ch][frame][513] (|X|^2 of bins 0..nfft/2, the mel stage's input), and signal -> log-mel (40 bands) / MFCC
+    (13 coefficients, lifter 22) rows in one launch each (src/features/mel.c:204-330 after stft.c:112-144).
+    Checks: one power row against NumPy f64; one log-mel and one MFCC row bit for bit against the two-step
+    device pipeline (power rows, then vv_dsp_log_mel_device / vv_dsp_mfcc_process_device)."""
+    nfr = frames_of(SAMPLES)
+    nb = NFFT // 2 + 1
+    try:
+        sig = torch.empty(ch, SAMPLES, device="cuda")
+        for c in range(ch):
+            g = torch.Generator(device="cuda").manual_seed(c)
+            sig[c].uniform_(-1.0, 1.0, generator=g)
+        pw = torch.empty(ch, nfr, nb, device="cuda")
+    except torch.OutOfMemoryError as e:
+        return {"error": repr(e)[:200]}
+    st = vv.Stft(NFFT, HOP, vv.WIN_HANN)
+    mf = vv.Mfcc(NFFT, n_mels, n_coeffs, float(FS), 20.0, 20000.0, lifter=22.0)
+    res = {"workload": f"{ch} ch x 10 min @ 48 kHz, 1024 Hann, hop 256 ({ch * nfr:,} frames): power rows, "
+                       f"log-mel ({n_mels} bands) and MFCC ({n_coeffs} coefficients) from the signal"}
+    avg, best, _ = timed_launches(lambda: st.power(sig, out=pw), reps, warm=10)
+    byts = ch * SAMPLES * 4 + ch * nfr * nb * 4
+    fr = nfr // 3
+    x0 = sig[ch - 1, fr * HOP: fr * HOP + NFFT].double().cpu().numpy()
+    want = np.abs(np.fft.fft(x0 * hann64())[:nb]) ** 2
+    ok = np.allclose(pw[ch - 1, fr].cpu().numpy(), want, rtol=1e-4, atol=1e-4 * NFFT)
+    res["power_rows"] = {"ms_avg": round(avg, 4), "ms_min": round(best, 4), "bytes_per_launch": byts,
+                         "frac": round(byts / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "check_row_vs_numpy_f64": bool(ok)}
+    row = pw[ch - 1, fr:fr + 1].clone()
+    for name, log_mel, width in (("log_mel", True, n_mels), ("mfcc", False, n_coeffs)):
+        out = torch.empty(ch, nfr, width, device="cuda")
+        avg, best, _ = timed_launches(lambda: mf.from_signal(st, sig, log_mel=log_mel, out=out), reps, warm=10)
+        ref = mf.log_mel(row) if log_mel else mf(row)
+        torch.cuda.synchronize()
+        res[name] = {"ms_avg": round(avg, 4), "ms_min": round(best, 4),
+                     "frames_per_s": round(ch * nfr / (avg * 1e-3), 1),
+                     "bytes_per_launch": ch * SAMPLES * 4 + ch * nfr * width * 4,
+                     "check_row_equals_two_step": bool(torch.equal(out[ch - 1, fr:fr + 1], ref))}
+        del out
+    del sig, pw, st, mf
+    torch.cuda.empty_cache()
+    return res
+
+
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -536,11 +581,12 @@ def parse_args():
                     help="channels of the whole job (config 5: 256), split over the ranks (strong scaling)")
     ap.add_argument("--no-extras", action="store_true", help="skip config 2/3/4, shard and CPU baseline legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg (profiling runs)")
-    ap.add_argument("--legs", default="c2c,fir,config3,shard,sizes",
+    ap.add_argument("--legs", default="c2c,fir,config3,shard,sizes,features",
                     help="extra GPU legs: c2c (config 2), fir (config 4), config3, shard (config 5's 32-channel "
                          "per-GPU shard of the N = 8 run), sizes (the reference's STFT sizes 256/512/2048/4096 on "
-                         "that shard); profiling runs leave config3, shard and sizes out so the "
-                         "headline kernel's PMC average covers the headline launches only")
+                         "that shard), features (power rows, log-mel and MFCC on that shard); profiling runs "
+                         "leave config3, shard, sizes and features out so the headline kernel's PMC average "
+                         "covers the headline launches only")
     ap.add_argument("--gather-bins", choices=["half", "full"], default="half",
                     help="gather bins 0..512 and expand on rank 0 (half, default) or all 1024 bins (full)")
     ap.add_argument("--gather", choices=["auto", "on", "off"], default="auto",
@@ -693,6 +739,11 @@ def main_plain(args):
             torch.cuda.empty_cache()
         if "sizes" in legs:
             res["stft_sizes"] = stft_sizes_leg()
+        if "features" in legs:
+            try:   # an informational leg: its failure must not cost the bench line
+                res["features"] = features_leg()
+            except Exception as e:   # noqa: BLE001
+                res["features"] = {"error": repr(e)[:200]}
             torch.cuda.empty_cache()
     if not args.no_extras and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline()
